@@ -1,0 +1,142 @@
+#!/usr/bin/env python3
+"""Headline benchmark (BASELINE.json): output tokens/sec (whole node) + p50 request latency,
+Llama-3-8B bf16, 1/2/4/8 GPU-workers (layer-sharded pipeline over RCCL for N > 1).
+
+Workload = the reference's request shape (worker/app.py:297-305, views.py:351): synthetic
+prompts of --prompt-len random token ids, max_length = 100 tokens INCLUDING the prompt,
+do_sample with temperature 0.8 / top_k 50 / top_p 0.95, random-init weights of the real
+architecture. EOS is ignored so every request generates exactly max_length - prompt_len
+tokens (fixed work per step).
+
+One "step" = one wave of requests served end to end (submit -> last token): --batch
+requests per GPU-worker, so per-GPU work is fixed as N grows (weak scaling). N = 1 runs
+the single-GPU engine; N > 1 splits the 32 layers into N contiguous stages (one per GPU,
+``parallel/pipeline.py``) with N microbatches of --batch requests in flight.
+
+    python bench.py                               # N=1 defaults
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8
+
+Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "output tokens/sec (whole node) + p50 request latency, Llama-3-8B 1/2/4/8 shards"
+
+
+def _baseline_value():
+    """Reference-strategy number measured on MI355X by scripts/bench_reference.py."""
+    p = ROOT / "profiles" / "reference_strategy.json"
+    if p.exists():
+        try:
+            return float(json.loads(p.read_text())["value"])
+        except Exception:  # noqa: BLE001
+            return None
+    return None
+
+
+def make_prompts(n, prompt_len, vocab, seed):
+    rng = np.random.default_rng(seed)
+    lo, hi = (1000, vocab - 1000) if vocab > 4000 else (3, vocab - 1)
+    return [rng.integers(lo, hi, size=prompt_len).tolist() for _ in range(n)]
+
+
+def run_single(args):
+    from distributed_llm_inferencing_amd.engine import SamplingParams
+    from distributed_llm_inferencing_amd.engine.llm_engine import LLMEngine
+
+    dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
+    eng = LLMEngine(args.model, device=str(dev), max_batch=args.batch,
+                    max_model_len=args.max_model_len, seed=0,
+                    max_prefill_tokens=max(args.batch * args.prompt_len, 8192))
+    sp = SamplingParams(max_length=args.max_length, temperature=0.8, top_k=50, top_p=0.95,
+                        ignore_eos=True)
+    eng.warmup()
+
+    def wave(seed):
+        prompts = make_prompts(args.batch, args.prompt_len, eng.cfg.vocab_size, seed)
+        outs = eng.generate(prompts, sp)
+        return sum(len(o.output_ids) for o in outs), [o.latency_s for o in outs]
+
+    for w in range(args.warmup):
+        wave(10_000 + w)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    toks, lats = 0, []
+    for s in range(args.steps):
+        n, l = wave(s)
+        toks += n
+        lats += l
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return {"tokens": toks, "seconds": dt, "latencies": lats, "global_batch": args.batch,
+            "parallelism": "single", "engine": eng.stats.snapshot()}
+
+
+def run_pipeline(args, world, rank):
+    from distributed_llm_inferencing_amd.parallel.pipeline import bench_pipeline
+    return bench_pipeline(args, world, rank, make_prompts)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--batch", type=int, default=256, help="requests per GPU-worker per wave")
+    ap.add_argument("--prompt-len", type=int, default=32)
+    ap.add_argument("--max-length", type=int, default=100)
+    ap.add_argument("--max-model-len", type=int, default=512)
+    a = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1 or a.gpus > 1:
+        res = run_pipeline(a, world, rank)
+    else:
+        res = run_single(a)
+    if rank != 0 or res is None:
+        return
+    tok_s = res["tokens"] / res["seconds"]
+    p50 = statistics.median(res["latencies"]) if res["latencies"] else None
+    base = _baseline_value()
+    line = {
+        "metric": METRIC,
+        "value": round(tok_s, 2),
+        "unit": "tokens/s",
+        "n_gpus": max(a.gpus, world),
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(1000 * res["seconds"] / max(1, a.steps), 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(tok_s / base, 3) if base else None,
+        "dtype": "bf16",
+        "data": "synthetic prompts, random-init weights",
+        "p50_latency_s": round(p50, 4) if p50 is not None else None,
+        "config": {"model": a.model, "global_batch": res["global_batch"],
+                   "seq_len": a.max_length, "prompt_len": a.prompt_len,
+                   "parallelism": res["parallelism"],
+                   "sampling": "T=0.8 top_k=50 top_p=0.95"},
+    }
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

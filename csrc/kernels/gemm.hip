@@ -1,0 +1,292 @@
+// bf16 GEMM on CDNA4 matrix cores: C[M,N] = A[M,K] . W[N,K]^T (+ fused epilogue).
+// SURVEY.md §2.4 K4/K9-K12 (dense projections) and K16 (MoE grouped GEMM).
+//
+// Structure (cdna_hip_programming.md §5):
+//  * 256 threads = 4 waves in a 2x2 grid; block tile BM x BN x 64; wave tile (BM/2) x (BN/2)
+//    built from v_mfma_f32_16x16x32_bf16 (the bf16 shape that holds the higher clock on random
+//    data, MI355X_MICROARCH.md 'DVFS give-back' item 7).
+//  * global -> LDS by global_load_lds_dwordx4 (16 B per lane, no VGPR round trip), 2 LDS
+//    buffers: the next K-tile's DMA is issued before the current tile's ds_reads + MFMAs.
+//  * LDS rows are 128 B (64 bf16); the 16-B chunk c of row r is stored at physical chunk
+//    c ^ ((r >> 1) & 7). glds writes lane-linearly, so the permutation is applied to the
+//    per-lane GLOBAL source address and the same XOR on the ds_read_b128 address (rule 21);
+//    verified conflict-free for all four ds_read_b128 lane groups of the 16x16x32 A/B maps.
+//  * XCD-aware bijective block remap (T1) with n-major tile order so consecutive tiles share
+//    one W panel in an XCD's L2.
+//  * split-K over grid.y writes fp32 slabs; a second pass reduces and applies the epilogue.
+//  * grouped mode (MoE): grid.z = expert; rows of group g are [off[g], off[g+1]) of A/C,
+//    weights W + g*N*ldw. Rows past the group end are skipped.
+// Epilogues: 0 bf16 store, 1 fp32 store (logits), 2 SiLU(gate)*up over the 16-row-interleaved
+// gate/up weight (output width N/2), 3 bias + tanh-GELU, 4 bias.
+#include "common.h"
+
+#define GEMM_THREADS 256
+#define BK 64
+
+enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_SILU = 2, EPI_BIAS_GELU = 3, EPI_BIAS = 4 };
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef const __attribute__((address_space(1))) void gbl_void;
+
+__device__ __forceinline__ float silu_f(float x) { return x / (1.f + __expf(-x)); }
+__device__ __forceinline__ float gelu_f(float x) {
+  return 0.5f * x * (1.f + tanhf(0.7978845608028654f * (x + 0.044715f * x * x * x)));
+}
+
+template <int EPI>
+__device__ __forceinline__ void store_pair_or_one(void* C, int ldc, int row, int col, float v,
+                                                  const u16* bias) {
+  if (EPI == EPI_F32) {
+    ((float*)C)[(long)row * ldc + col] = v;
+  } else {
+    if (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) v += bf2f(bias[col]);
+    if (EPI == EPI_BIAS_GELU) v = gelu_f(v);
+    ((u16*)C)[(long)row * ldc + col] = f2bf(v);
+  }
+}
+
+template <int BM, int BN, int EPI>
+__global__ void __launch_bounds__(GEMM_THREADS) gemm_bf16_kernel(
+    const u16* __restrict__ A, int lda, const u16* __restrict__ W, int ldw,
+    void* __restrict__ C, int ldc, int M, int N, int K, int k_split_len,
+    const u16* __restrict__ bias, float* __restrict__ ws, const int* __restrict__ group_off) {
+  constexpr int MI = BM / 32, NI = BN / 32;        // 16x16 blocks per wave (wave = BM/2 x BN/2)
+  constexpr int A_BYTES = BM * BK * 2, W_BYTES = BN * BK * 2;
+  constexpr int BUF = A_BYTES + W_BYTES;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  // ---- tile coordinates
+  int row0 = 0, Mg = M;
+  const u16* Wg = W;
+  if (group_off != nullptr) {
+    row0 = group_off[blockIdx.z];
+    Mg = group_off[blockIdx.z + 1] - row0;
+    Wg = W + (long)blockIdx.z * N * ldw;
+  }
+  const int tiles_m = (M + BM - 1) / BM;           // M = max rows per group in grouped mode
+  const int tiles_n = (N + BN - 1) / BN;
+  const int nwg = tiles_m * tiles_n;
+  const int tile = xcd_remap(blockIdx.x, nwg);
+  const int tn = tile / tiles_m, tm = tile % tiles_m;
+  const int m0 = tm * BM, n0 = tn * BN;
+  if (m0 >= Mg) return;                             // grouped: empty tile (block-uniform)
+  const int kb = blockIdx.y * k_split_len;
+  const int nk = min(k_split_len, K - kb) / BK;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const u16* Ab = A + (long)row0 * lda;
+
+  // ---- per-lane glds source pointers (row clamped in range; swizzled chunk)
+  constexpr int A_INSTR = BM / 32, W_INSTR = BN / 32;   // glds per wave per K-tile
+  const u16* a_src[A_INSTR];
+  const u16* w_src[W_INSTR];
+#pragma unroll
+  for (int i = 0; i < A_INSTR; ++i) {
+    const int r = (i * 4 + wid) * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    const int gr = min(m0 + r, Mg - 1);
+    a_src[i] = Ab + (long)gr * lda + kb + c * 8;
+  }
+#pragma unroll
+  for (int i = 0; i < W_INSTR; ++i) {
+    const int r = (i * 4 + wid) * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    const int gr = min(n0 + r, N - 1);
+    w_src[i] = Wg + (long)gr * ldw + kb + c * 8;
+  }
+  auto stage = [&](int buf, int kt) {
+    char* base = smem + buf * BUF;
+#pragma unroll
+    for (int i = 0; i < A_INSTR; ++i)
+      __builtin_amdgcn_global_load_lds((gbl_void*)(a_src[i] + kt * BK),
+                                       (lds_void*)(base + (i * 4 + wid) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int i = 0; i < W_INSTR; ++i)
+      __builtin_amdgcn_global_load_lds((gbl_void*)(w_src[i] + kt * BK),
+                                       (lds_void*)(base + A_BYTES + (i * 4 + wid) * 1024), 16,
+                                       0, 0);
+  };
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // per-lane fragment read offsets (bytes, within a buffer), chunk XOR applied per k-step
+  const int fr = lane & 15, fq = lane >> 4;
+  int a_row[MI], w_row[NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) a_row[i] = wm * (BM / 2) + i * 16 + fr;
+#pragma unroll
+  for (int j = 0; j < NI; ++j) w_row[j] = wn * (BN / 2) + j * 16 + fr;
+
+  if (nk > 0) stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
+    const char* abuf = smem + cur * BUF;
+    const char* wbuf = abuf + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int c = kk * 4 + fq;
+      bf16x8 af[MI], bfr[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int r = a_row[i];
+        af[i] = *reinterpret_cast<const bf16x8*>(abuf + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int r = w_row[j];
+        bfr[j] = *reinterpret_cast<const bf16x8*>(wbuf + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- epilogue. acc[i][j][r] = C[m0 + wm*BM/2 + 16i + 4fq + r][n0 + wn*BN/2 + 16j + fr]
+  const bool split = gridDim.y > 1;
+  if (split) {
+    float* slab = ws + (long)blockIdx.y * M * N;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * (BM / 2) + 16 * i + 4 * fq + r;
+        if (row >= Mg) continue;
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int col = n0 + wn * (BN / 2) + 16 * j + fr;
+          if (col < N) slab[(long)(row0 + row) * N + col] = acc[i][j][r];
+        }
+      }
+    return;
+  }
+  if (EPI == EPI_SILU) {
+    // column blocks j (even) = gate, j+1 = up of the same 16 features
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * (BM / 2) + 16 * i + 4 * fq + r;
+        if (row >= Mg) continue;
+#pragma unroll
+        for (int j = 0; j < NI; j += 2) {
+          const int gcol = n0 + wn * (BN / 2) + 16 * j;       // first gate row of the pair
+          if (gcol < N) {
+            const int f = (gcol >> 5) * 16 + fr;
+            const float v = silu_f(acc[i][j][r]) * acc[i][j + 1][r];
+            ((u16*)C)[(long)(row0 + row) * ldc + f] = f2bf(v);
+          }
+        }
+      }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = m0 + wm * (BM / 2) + 16 * i + 4 * fq + r;
+      if (row >= Mg) continue;
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int col = n0 + wn * (BN / 2) + 16 * j + fr;
+        if (col < N) store_pair_or_one<EPI>(C, ldc, row0 + row, col, acc[i][j][r], bias);
+      }
+    }
+}
+
+// split-K reduction + epilogue: one thread per output element group of 4 columns
+template <int EPI>
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(void* __restrict__ C, int ldc,
+                                                            const float* __restrict__ ws, int M,
+                                                            int N, int splits,
+                                                            const u16* __restrict__ bias) {
+  const int outN = (EPI == EPI_SILU) ? N / 2 : N;
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (long)M * outN) return;
+  const int row = (int)(gid / outN), col = (int)(gid % outN);
+  if (EPI == EPI_SILU) {
+    const int grp = col >> 4, in = col & 15;
+    const long gi = (long)row * N + grp * 32 + in, ui = gi + 16;
+    float g = 0.f, u = 0.f;
+    for (int s = 0; s < splits; ++s) { g += ws[(long)s * M * N + gi]; u += ws[(long)s * M * N + ui]; }
+    ((u16*)C)[(long)row * ldc + col] = f2bf(silu_f(g) * u);
+  } else {
+    float v = 0.f;
+    for (int s = 0; s < splits; ++s) v += ws[(long)s * M * N + (long)row * N + col];
+    store_pair_or_one<EPI>(C, ldc, row, col, v, bias);
+  }
+}
+
+template <int BM, int BN, int EPI>
+static int launch_cfg(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M,
+                      int N, int K, int splits, const void* bias, void* ws,
+                      const int* group_off, int groups, hipStream_t st) {
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  int ksl = K / splits;
+  ksl = (ksl / BK) * BK;
+  if (ksl * splits != K) return (int)hipErrorInvalidValue;
+  const size_t lds = 2 * (size_t)(BM + BN) * BK * 2;
+  static bool attr_done = false;                   // > 64 KiB dynamic LDS needs the opt-in
+  if (!attr_done) {
+    hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, EPI>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_done = true;
+  }
+  dim3 grid(tiles, splits, groups);
+  gemm_bf16_kernel<BM, BN, EPI><<<grid, GEMM_THREADS, lds, st>>>(
+      (const u16*)A, lda, (const u16*)W, ldw, C, ldc, M, N, K, ksl, (const u16*)bias,
+      (float*)ws, group_off);
+  if (splits > 1) {
+    const int outN = (EPI == EPI_SILU) ? N / 2 : N;
+    const long total = (long)M * outN;
+    splitk_reduce_kernel<EPI><<<(int)((total + 255) / 256), 256, 0, st>>>(
+        C, ldc, (const float*)ws, M, N, splits, (const u16*)bias);
+  }
+  DLI_RETURN_LAUNCH();
+}
+
+template <int EPI>
+static int dispatch_tile(int tile_cfg, const void* A, int lda, const void* W, int ldw, void* C,
+                         int ldc, int M, int N, int K, int splits, const void* bias, void* ws,
+                         const int* go, int groups, hipStream_t st) {
+  switch (tile_cfg) {
+    case 0: return launch_cfg<64, 64, EPI>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
+    case 1: return launch_cfg<64, 128, EPI>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
+    case 2: return launch_cfg<128, 128, EPI>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
+    case 3: return launch_cfg<128, 256, EPI>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
+    case 4: return launch_cfg<256, 128, EPI>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
+// tile_cfg: 0=64x64 1=64x128 2=128x128 3=128x256 4=256x128. ws: fp32 [splits, M, N] when splits>1.
+// group_off (nullable): int[groups+1] row offsets; M is then the max rows of any group.
+extern "C" int dli_gemm(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M,
+                        int N, int K, int epi, int tile_cfg, int splits, const void* bias,
+                        void* ws, const int* group_off, int groups, hipStream_t st) {
+  if (M <= 0 || N <= 0) return 0;
+  if (K % BK || lda % 8 || ldw % 8 || splits < 1) return (int)hipErrorInvalidValue;
+  if (epi == EPI_SILU && N % 32) return (int)hipErrorInvalidValue;
+  if (splits > 1 && (ws == nullptr || group_off != nullptr)) return (int)hipErrorInvalidValue;
+  if (groups < 1) groups = 1;
+  switch (epi) {
+    case EPI_BF16: return dispatch_tile<EPI_BF16>(tile_cfg, A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, group_off, groups, st);
+    case EPI_F32: return dispatch_tile<EPI_F32>(tile_cfg, A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, group_off, groups, st);
+    case EPI_SILU: return dispatch_tile<EPI_SILU>(tile_cfg, A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, group_off, groups, st);
+    case EPI_BIAS_GELU: return dispatch_tile<EPI_BIAS_GELU>(tile_cfg, A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, group_off, groups, st);
+    case EPI_BIAS: return dispatch_tile<EPI_BIAS>(tile_cfg, A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, group_off, groups, st);
+    default: return (int)hipErrorInvalidValue;
+  }
+}

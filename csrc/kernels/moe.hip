@@ -1,0 +1,134 @@
+// Mixture-of-experts routing / permutation kernels (Mixtral) — SURVEY.md §2.4 K15/K16.
+//   route   : softmax over E router logits -> top-k -> renormalise (HF MixtralSparseMoeBlock)
+//   align   : per-expert counts, exclusive offsets, permuted position of every (token, slot)
+//   gather  : x_perm[p] = x[src[p]]            (16-B row copies)
+//   combine : out[t] = sum_slot w[t,slot] * y_perm[pos[t,slot]]   (fp32 sum, bf16 out)
+// The expert MLPs themselves run as grouped GEMMs (gemm.hip, grid.z = expert).
+#include "common.h"
+
+__global__ void moe_route_kernel(float* __restrict__ topk_w, int* __restrict__ topk_ids,
+                                 const u16* __restrict__ logits, int T, int E, int k) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= T) return;
+  float p[64];
+  float mx = -INFINITY;
+  for (int e = 0; e < E; ++e) { p[e] = bf2f(logits[(long)t * E + e]); mx = fmaxf(mx, p[e]); }
+  float s = 0.f;
+  for (int e = 0; e < E; ++e) { p[e] = __expf(p[e] - mx); s += p[e]; }
+  float wsum = 0.f;
+  for (int j = 0; j < k; ++j) {
+    int best = 0; float bv = -1.f;
+    for (int e = 0; e < E; ++e) if (p[e] > bv) { bv = p[e]; best = e; }
+    topk_ids[t * k + j] = best;
+    topk_w[t * k + j] = bv / s;
+    wsum += bv / s;
+    p[best] = -2.f;
+  }
+  for (int j = 0; j < k; ++j) topk_w[t * k + j] /= wsum;
+}
+
+extern "C" int dli_moe_route(float* topk_w, int* topk_ids, const void* logits, int T, int E, int k,
+                             hipStream_t st) {
+  if (T <= 0) return 0;
+  if (E > 64 || k > E) return (int)hipErrorInvalidValue;
+  moe_route_kernel<<<(T + 255) / 256, 256, 0, st>>>(topk_w, topk_ids, (const u16*)logits, T, E, k);
+  DLI_RETURN_LAUNCH();
+}
+
+// Single workgroup. ids: [n] expert ids (n = T*k); experts outside [e0, e0+E_local) are dropped
+// (pos = -1). offsets: [E_local + 1]; pos: [n]; src: [n] (token of each permuted row).
+__global__ void __launch_bounds__(1024) moe_align_kernel(int* __restrict__ offsets,
+                                                         int* __restrict__ pos,
+                                                         int* __restrict__ src,
+                                                         const int* __restrict__ ids, int n,
+                                                         int k, int e0, int E_local) {
+  __shared__ int cnt[256];
+  __shared__ int off[257];
+  for (int i = threadIdx.x; i < E_local; i += blockDim.x) cnt[i] = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int e = ids[i] - e0;
+    if (e >= 0 && e < E_local) atomicAdd(&cnt[e], 1);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int run = 0;
+    for (int e = 0; e < E_local; ++e) { off[e] = run; run += cnt[e]; cnt[e] = 0; }
+    off[E_local] = run;
+    for (int e = 0; e <= E_local; ++e) offsets[e] = off[e];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int e = ids[i] - e0;
+    if (e >= 0 && e < E_local) {
+      const int p = off[e] + atomicAdd(&cnt[e], 1);
+      pos[i] = p;
+      src[p] = i / k;
+    } else {
+      pos[i] = -1;
+    }
+  }
+}
+
+extern "C" int dli_moe_align(int* offsets, int* pos, int* src, const int* ids, int n, int k,
+                             int e0, int E_local, hipStream_t st) {
+  if (E_local > 256) return (int)hipErrorInvalidValue;
+  moe_align_kernel<<<1, 1024, 0, st>>>(offsets, pos, src, ids, n, k, e0, E_local);
+  DLI_RETURN_LAUNCH();
+}
+
+// rows p >= *count (the routed total, offsets[E_local]) are left untouched: src is undefined there
+__global__ void __launch_bounds__(256) moe_gather_kernel(u16* __restrict__ out,
+                                                         const u16* __restrict__ x,
+                                                         const int* __restrict__ src, int P,
+                                                         int dim, const int* __restrict__ count) {
+  const int chunks = dim >> 3;
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (long)P * chunks) return;
+  const int p = (int)(gid / chunks), c = (int)(gid % chunks);
+  if (count != nullptr && p >= *count) return;
+  *reinterpret_cast<uint4*>(out + (long)p * dim + c * 8) =
+      *reinterpret_cast<const uint4*>(x + (long)src[p] * dim + c * 8);
+}
+
+extern "C" int dli_moe_gather(void* out, const void* x, const int* src, int P, int dim,
+                              const int* count, hipStream_t st) {
+  if (P <= 0) return 0;
+  if (dim % 8) return (int)hipErrorInvalidValue;
+  const long total = (long)P * (dim / 8);
+  moe_gather_kernel<<<(int)((total + 255) / 256), 256, 0, st>>>((u16*)out, (const u16*)x, src, P,
+                                                                dim, count);
+  DLI_RETURN_LAUNCH();
+}
+
+__global__ void __launch_bounds__(256) moe_combine_kernel(u16* __restrict__ out,
+                                                          const u16* __restrict__ y,
+                                                          const float* __restrict__ w,
+                                                          const int* __restrict__ pos, int T,
+                                                          int k, int dim) {
+  const int chunks = dim >> 3;
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (long)T * chunks) return;
+  const int t = (int)(gid / chunks), c = (int)(gid % chunks);
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int j = 0; j < k; ++j) {
+    const int p = pos[t * k + j];
+    if (p < 0) continue;
+    float v[8];
+    load8(y + (long)p * dim + c * 8, v);
+    const float ww = w[t * k + j];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] += ww * v[q];
+  }
+  store8(out + (long)t * dim + c * 8, acc);
+}
+
+extern "C" int dli_moe_combine(void* out, const void* y, const float* w, const int* pos, int T,
+                               int k, int dim, hipStream_t st) {
+  if (T <= 0) return 0;
+  if (dim % 8) return (int)hipErrorInvalidValue;
+  const long total = (long)T * (dim / 8);
+  moe_combine_kernel<<<(int)((total + 255) / 256), 256, 0, st>>>((u16*)out, (const u16*)y, w, pos,
+                                                                 T, k, dim);
+  DLI_RETURN_LAUNCH();
+}

@@ -1,0 +1,230 @@
+// On-device token sampling with HF `generate` semantics — SURVEY.md §2.4 K13/K14.
+//
+// HF warper order (transformers/generation/utils.py): Temperature -> TopK -> TopP -> softmax
+// -> multinomial. One 512-thread workgroup per row (vocab up to ~256k), no full-vocab sort:
+//   * greedy (temperature <= 0 or top_k == 1): block argmax (first index on ties, like torch).
+//   * top_k <= 0 and top_p >= 1: exact Gumbel-max sampling over the whole row in one pass.
+//   * otherwise: radix select (8-bit digits, early exit) finds the bin holding the k-th
+//     largest logit; every element at or above it (<= CAP) is gathered into LDS, bitonic-
+//     sorted, cut to the top-k (ties kept, as HF's `scores < kth` mask keeps them), then
+//     temperature-softmax, top-p truncation (keep j while the mass of strictly larger tokens
+//     < top_p, i.e. HF's `cumsum_asc <= 1-top_p` removal) and an inverse-CDF draw.
+// top_k is capped at CAP (2048). Randomness: Philox4x32-10 keyed by a per-row 64-bit seed
+// supplied by the engine (seed = f(request seed, output index)), so a request samples the
+// same tokens regardless of how it is batched.
+#include "common.h"
+
+#define SMP_THREADS 512
+#define SMP_CAP 2048
+
+__device__ __forceinline__ uint32_t f2key(float f) {
+  uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float key2f(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+// Philox4x32-10
+__device__ __forceinline__ uint4 philox(uint2 key, uint4 ctr) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint32_t hi0 = __umulhi(M0, ctr.x), lo0 = M0 * ctr.x;
+    const uint32_t hi1 = __umulhi(M1, ctr.z), lo1 = M1 * ctr.z;
+    ctr = make_uint4(hi1 ^ ctr.y ^ key.x, lo1, hi0 ^ ctr.w ^ key.y, lo0);
+    key.x += W0; key.y += W1;
+  }
+  return ctr;
+}
+__device__ __forceinline__ float u01(uint32_t x) {           // (0, 1)
+  return ((x >> 8) + 0.5f) * (1.0f / 16777216.0f);
+}
+
+struct ArgMax { float v; int i; };
+__device__ __forceinline__ ArgMax amax(ArgMax a, ArgMax b) {
+  if (b.v > a.v || (b.v == a.v && b.i < a.i)) return b;
+  return a;
+}
+__device__ ArgMax block_argmax(ArgMax a, float* sv, int* si) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    ArgMax b{__shfl_xor(a.v, o, 64), __shfl_xor(a.i, o, 64)};
+    a = amax(a, b);
+  }
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) { sv[w] = a.v; si[w] = a.i; }
+  __syncthreads();
+  ArgMax r{sv[0], si[0]};
+  for (int i = 1; i < nw; ++i) r = amax(r, ArgMax{sv[i], si[i]});
+  return r;
+}
+
+// inclusive block scan of one float per thread (512 threads)
+__device__ float block_scan(float v, float* tmp) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  __syncthreads();
+  if (lane == 63) tmp[w] = v;
+  __syncthreads();
+  float add = 0.f;
+  for (int i = 0; i < w; ++i) add += tmp[i];
+  (void)nw;
+  return v + add;
+}
+
+__global__ void __launch_bounds__(SMP_THREADS) sample_kernel(
+    int* __restrict__ out_tokens, const float* __restrict__ logits, long row_stride, int V,
+    const float* __restrict__ temperature, const int* __restrict__ top_k,
+    const float* __restrict__ top_p, const long long* __restrict__ seeds) {
+  __shared__ uint32_t hist[256];
+  __shared__ uint32_t ckey[SMP_CAP];
+  __shared__ int cidx[SMP_CAP];
+  __shared__ float cprob[SMP_CAP];
+  __shared__ float sv[16];
+  __shared__ int si[16];
+  __shared__ uint32_t s_digit, s_above, s_inbin, s_cnt;
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const float* x = logits + (long)row * row_stride;
+  const float T = temperature[row];
+  const int K = top_k[row];
+  const float P = top_p[row];
+  const unsigned long long sd = (unsigned long long)seeds[row];
+  const uint2 key = make_uint2((uint32_t)sd, (uint32_t)(sd >> 32));
+
+  if (T <= 0.f || K == 1) {                                  // greedy
+    ArgMax a{-INFINITY, 0x7fffffff};
+    for (int i = tid; i < V; i += blockDim.x) a = amax(a, ArgMax{x[i], i});
+    a = block_argmax(a, sv, si);
+    if (tid == 0) out_tokens[row] = a.i < V ? a.i : 0;
+    return;
+  }
+  const float invT = 1.f / T;
+  if (K <= 0 && P >= 1.f) {                                  // plain temperature: Gumbel-max
+    ArgMax a{-INFINITY, 0x7fffffff};
+    for (int base = tid * 4; base < V; base += blockDim.x * 4) {
+      const uint4 r = philox(key, make_uint4((uint32_t)(base >> 2), 0u, 0x5a5a5a5au, 0u));
+      const uint32_t rr[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int i = base + j;
+        if (i < V) {
+          const float g = -__logf(-__logf(u01(rr[j])));
+          a = amax(a, ArgMax{x[i] * invT + g, i});
+        }
+      }
+    }
+    a = block_argmax(a, sv, si);
+    if (tid == 0) out_tokens[row] = a.i < V ? a.i : 0;
+    return;
+  }
+  int Keff = (K <= 0 || K > SMP_CAP) ? SMP_CAP : K;
+  if (Keff > V) Keff = V;
+
+  // ---- radix select on order-preserving keys (largest first), 8-bit digits
+  uint32_t prefix = 0, pmask = 0, k_rem = (uint32_t)Keff, above_total = 0;
+  for (int pass = 0; pass < 4; ++pass) {
+    const int shift = 24 - 8 * pass;
+    for (int i = tid; i < 256; i += blockDim.x) hist[i] = 0;
+    __syncthreads();
+    for (int i = tid; i < V; i += blockDim.x) {
+      const uint32_t k = f2key(x[i]);
+      if ((k & pmask) == prefix) atomicAdd(&hist[(k >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t cum = 0, d = 0;
+      for (int b = 255; b >= 0; --b) {
+        if (cum + hist[b] >= k_rem) { d = (uint32_t)b; break; }
+        cum += hist[b];
+      }
+      s_digit = d; s_above = cum; s_inbin = hist[d];
+    }
+    __syncthreads();
+    k_rem -= s_above;
+    above_total += s_above;
+    prefix |= s_digit << shift;
+    pmask |= 255u << shift;
+    if (above_total + s_inbin <= SMP_CAP) break;
+  }
+  // ---- gather everything at or above the boundary bin
+  if (tid == 0) s_cnt = 0;
+  __syncthreads();
+  for (int i = tid; i < V; i += blockDim.x) {
+    const uint32_t k = f2key(x[i]);
+    if ((k & pmask) >= prefix) {
+      const uint32_t pos = atomicAdd(&s_cnt, 1u);
+      if (pos < SMP_CAP) { ckey[pos] = k; cidx[pos] = i; }
+    }
+  }
+  __syncthreads();
+  const int n = (int)min(s_cnt, (uint32_t)SMP_CAP);
+  int npow = 1;
+  while (npow < n) npow <<= 1;
+  for (int i = n + tid; i < npow; i += blockDim.x) { ckey[i] = 0u; cidx[i] = 0x7fffffff; }
+  __syncthreads();
+  // ---- bitonic sort descending by key (ties: smaller index first)
+  for (int size = 2; size <= npow; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = tid; i < npow / 2; i += blockDim.x) {
+        const int lo = 2 * i - (i & (stride - 1));
+        const int hi = lo + stride;
+        const bool desc = ((lo & size) == 0);
+        const uint32_t a = ckey[lo], b = ckey[hi];
+        const int ia = cidx[lo], ib = cidx[hi];
+        const bool a_first = (a > b) || (a == b && ia < ib);
+        if (a_first != desc) {
+          ckey[lo] = b; ckey[hi] = a; cidx[lo] = ib; cidx[hi] = ia;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // ---- top-k cut (ties with the k-th value kept)
+  const int kk = min(Keff, n);
+  const uint32_t tau = ckey[kk - 1];
+  int m = kk;
+  while (m < n && ckey[m] == tau) ++m;
+  // ---- temperature softmax over the m survivors, top-p, inverse CDF
+  const float xmax = key2f(ckey[0]);
+  constexpr int PER = SMP_CAP / SMP_THREADS;                 // 4 consecutive entries / thread
+  float loc[PER], lsum = 0.f;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int e = tid * PER + j;
+    loc[j] = e < m ? __expf((key2f(ckey[e]) - xmax) * invT) : 0.f;
+    lsum += loc[j];
+  }
+  const float incl = block_scan(lsum, sv);
+  float run = incl - lsum;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) { run += loc[j]; cprob[tid * PER + j] = run; }
+  __syncthreads();
+  const float Z = cprob[m - 1];
+  // keep entries whose exclusive prefix < P * Z
+  if (tid == 0) {
+    const float lim = P * Z;
+    int c = 1;
+    while (c < m && cprob[c - 1] < lim) ++c;
+    const float zk = cprob[c - 1];
+    const uint4 r = philox(key, make_uint4(0xfffffffu, 1u, 0xa5a5a5a5u, 7u));
+    const float u = u01(r.x) * zk;
+    int j = 0;
+    while (j < c - 1 && cprob[j] <= u) ++j;
+    out_tokens[row] = cidx[j];
+  }
+}
+
+extern "C" int dli_sample(int* out_tokens, const float* logits, long row_stride, int B, int V,
+                          const float* temperature, const int* top_k, const float* top_p,
+                          const long long* seeds, hipStream_t st) {
+  if (B <= 0) return 0;
+  sample_kernel<<<B, SMP_THREADS, 0, st>>>(out_tokens, logits, row_stride, V, temperature, top_k,
+                                           top_p, seeds);
+  DLI_RETURN_LAUNCH();
+}

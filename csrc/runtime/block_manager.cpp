@@ -1,0 +1,149 @@
+// Paged KV-cache block allocator + per-step metadata builders (host C++).
+//
+// Replaces HF's per-request `past_key_values` tensors (grown by torch.cat every step,
+// SURVEY.md §2.4 K6) with a fixed pool of `num_blocks` blocks of `block_size` tokens per
+// layer, sized from HBM at engine start (288 GB per MI355X => millions of tokens). The
+// scheduler (Python) asks this allocator for blocks; the batch builders below emit the
+// int32 block tables and slot mappings the HIP kernels consume, so per-step metadata for a
+// 256-sequence batch is built without a Python loop over tokens.
+//
+// C ABI (ctypes): every function returns >= 0 on success, negative on failure.
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <mutex>
+#include <unordered_map>
+#include <vector>
+
+namespace {
+
+struct BlockManager {
+  int num_blocks;
+  int block_size;
+  std::vector<int> free_list;                              // stack of free block ids
+  std::unordered_map<long long, std::vector<int>> tables;  // seq id -> blocks
+  std::mutex mu;
+
+  BlockManager(int nb, int bs) : num_blocks(nb), block_size(bs) {
+    free_list.reserve(nb);
+    // hand out low block ids first (LIFO stack, reversed fill)
+    for (int b = nb - 1; b >= 0; --b) free_list.push_back(b);
+  }
+  int blocks_for(long long tokens) const {
+    return (int)((tokens + block_size - 1) / block_size);
+  }
+};
+
+inline BlockManager* H(void* h) { return reinterpret_cast<BlockManager*>(h); }
+
+}  // namespace
+
+extern "C" {
+
+void* dli_bm_create(int num_blocks, int block_size) {
+  if (num_blocks <= 0 || block_size <= 0) return nullptr;
+  return new BlockManager(num_blocks, block_size);
+}
+
+void dli_bm_destroy(void* h) { delete H(h); }
+
+int dli_bm_num_free(void* h) {
+  std::lock_guard<std::mutex> g(H(h)->mu);
+  return (int)H(h)->free_list.size();
+}
+
+int dli_bm_num_blocks(void* h) { return H(h)->num_blocks; }
+int dli_bm_block_size(void* h) { return H(h)->block_size; }
+
+// Blocks still needed so that `seq` covers `total_tokens` tokens.
+int dli_bm_blocks_needed(void* h, long long seq, long long total_tokens) {
+  auto* m = H(h);
+  std::lock_guard<std::mutex> g(m->mu);
+  auto it = m->tables.find(seq);
+  const int have = it == m->tables.end() ? 0 : (int)it->second.size();
+  return std::max(0, m->blocks_for(total_tokens) - have);
+}
+
+// Grow `seq`'s table to cover `total_tokens`; all-or-nothing. Returns blocks added or -1.
+int dli_bm_ensure(void* h, long long seq, long long total_tokens) {
+  auto* m = H(h);
+  std::lock_guard<std::mutex> g(m->mu);
+  auto& tab = m->tables[seq];
+  const int need = m->blocks_for(total_tokens) - (int)tab.size();
+  if (need <= 0) return 0;
+  if ((int)m->free_list.size() < need) {
+    if (tab.empty()) m->tables.erase(seq);
+    return -1;
+  }
+  for (int i = 0; i < need; ++i) {
+    tab.push_back(m->free_list.back());
+    m->free_list.pop_back();
+  }
+  return need;
+}
+
+// Release every block of `seq`. Returns the number released.
+int dli_bm_free(void* h, long long seq) {
+  auto* m = H(h);
+  std::lock_guard<std::mutex> g(m->mu);
+  auto it = m->tables.find(seq);
+  if (it == m->tables.end()) return 0;
+  const int n = (int)it->second.size();
+  for (auto it2 = it->second.rbegin(); it2 != it->second.rend(); ++it2)
+    m->free_list.push_back(*it2);
+  m->tables.erase(it);
+  return n;
+}
+
+int dli_bm_table(void* h, long long seq, int* out, int max_blocks) {
+  auto* m = H(h);
+  std::lock_guard<std::mutex> g(m->mu);
+  auto it = m->tables.find(seq);
+  if (it == m->tables.end()) return 0;
+  const int n = std::min((int)it->second.size(), max_blocks);
+  std::memcpy(out, it->second.data(), sizeof(int) * n);
+  return n;
+}
+
+// Padded [n, max_blocks] block tables (pad = 0: a valid block id that kernels never read
+// past context_lens). Returns the widest table or -1 if a table exceeds max_blocks.
+int dli_bm_fill_tables(void* h, const long long* seqs, int n, int* out, int max_blocks) {
+  auto* m = H(h);
+  std::lock_guard<std::mutex> g(m->mu);
+  int widest = 0;
+  for (int i = 0; i < n; ++i) {
+    int* row = out + (long)i * max_blocks;
+    auto it = m->tables.find(seqs[i]);
+    int cnt = 0;
+    if (it != m->tables.end()) {
+      cnt = (int)it->second.size();
+      if (cnt > max_blocks) return -1;
+      std::memcpy(row, it->second.data(), sizeof(int) * cnt);
+    }
+    std::fill(row + cnt, row + max_blocks, 0);
+    widest = std::max(widest, cnt);
+  }
+  return widest;
+}
+
+// slot ids for tokens [start_i, start_i + count_i) of each sequence, concatenated.
+int dli_bm_slot_mapping(void* h, const long long* seqs, const int* starts, const int* counts,
+                        int n, int* out) {
+  auto* m = H(h);
+  std::lock_guard<std::mutex> g(m->mu);
+  long o = 0;
+  const int bs = m->block_size;
+  for (int i = 0; i < n; ++i) {
+    auto it = m->tables.find(seqs[i]);
+    if (it == m->tables.end()) return -1;
+    const auto& tab = it->second;
+    for (int t = starts[i]; t < starts[i] + counts[i]; ++t) {
+      const int b = t / bs;
+      if (b >= (int)tab.size()) return -1;
+      out[o++] = tab[b] * bs + (t % bs);
+    }
+  }
+  return (int)o;
+}
+
+}  // extern "C"

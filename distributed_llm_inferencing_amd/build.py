@@ -1,0 +1,123 @@
+"""In-tree native build: hipcc for gfx950, no torch headers, no JIT cache.
+
+Produces two shared objects inside the package (they travel to the GPU box with the
+repo snapshot; they are git-ignored):
+
+* ``lib/libdli_kernels.so`` — every HIP/CDNA4 kernel in ``csrc/kernels`` behind a plain
+  ``extern "C"`` ABI (called through ctypes with torch's current HIP stream).
+* ``lib/libdli_runtime.so`` — the host-side C++ runtime in ``csrc/runtime`` (paged-KV
+  block allocator, continuous-batching scheduler core, safetensors weight loader with
+  pinned staging + hipMemcpyAsync, byte tokenizer).
+
+Both link ``libamdhip64.so.7``; at run time the copy torch already loaded is reused
+(same SONAME), so kernels launched here and torch's own kernels share one HIP runtime.
+
+Usage: ``python -m distributed_llm_inferencing_amd.build [--force] [-j N]``
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import hashlib
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+REPO = PKG.parent
+CSRC = REPO / "csrc"
+LIBDIR = PKG / "lib"
+OBJDIR = REPO / "build" / "obj"
+ARCH = os.environ.get("DLI_OFFLOAD_ARCH", "gfx950")
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and Path(cand).exists():
+            return cand
+    raise RuntimeError("hipcc not found (set HIPCC or install ROCm)")
+
+
+KERNEL_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffast-math",
+                "-fno-gpu-rdc", "-munsafe-fp-atomics", "-Wno-unused-result"]
+RUNTIME_FLAGS = ["-O2", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",
+                 "-Wno-unused-result"]
+
+
+def _digest(paths, flags) -> str:
+    h = hashlib.sha1()
+    for p in sorted(paths):
+        h.update(p.name.encode())
+        h.update(p.read_bytes())
+    h.update(" ".join(flags).encode())
+    return h.hexdigest()
+
+
+def _compile(src: Path, obj: Path, flags, headers) -> Path:
+    stamp = obj.with_suffix(".sha1")
+    dig = _digest([src, *headers], flags)
+    if obj.exists() and stamp.exists() and stamp.read_text() == dig:
+        return obj
+    obj.parent.mkdir(parents=True, exist_ok=True)
+    cmd = [_hipcc(), *flags, "-I", str(CSRC / "kernels"), "-I", str(CSRC / "runtime"),
+           "-c", str(src), "-o", str(obj)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src.name}:\n{' '.join(cmd)}\n{r.stderr[-6000:]}")
+    stamp.write_text(dig)
+    return obj
+
+
+def _link(objs, out: Path, extra=()):
+    out.parent.mkdir(parents=True, exist_ok=True)
+    tmp = out.with_suffix(".so.tmp")
+    cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(tmp),
+           *extra]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed for {out.name}:\n{r.stderr[-4000:]}")
+    os.replace(tmp, out)
+
+
+def _build_group(srcs, headers, flags, out: Path, jobs: int, extra=()):
+    objs_dir = OBJDIR / out.stem
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        futs = [ex.submit(_compile, s, objs_dir / (s.stem + ".o"), flags, headers) for s in srcs]
+        objs = [f.result() for f in futs]
+    newest = max(o.stat().st_mtime for o in objs)
+    if not out.exists() or out.stat().st_mtime < newest:
+        _link(objs, out, extra)
+    return out
+
+
+def build(force: bool = False, jobs: int = 0, verbose: bool = True) -> dict:
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    if force and OBJDIR.exists():
+        shutil.rmtree(OBJDIR)
+    k_srcs = sorted((CSRC / "kernels").glob("*.hip"))
+    k_hdrs = sorted((CSRC / "kernels").glob("*.h"))
+    r_srcs = sorted((CSRC / "runtime").glob("*.cpp"))
+    r_hdrs = sorted((CSRC / "runtime").glob("*.h"))
+    out = {}
+    out["kernels"] = _build_group(k_srcs, k_hdrs, KERNEL_FLAGS, LIBDIR / "libdli_kernels.so", jobs)
+    if r_srcs:
+        out["runtime"] = _build_group(r_srcs, r_hdrs, RUNTIME_FLAGS, LIBDIR / "libdli_runtime.so",
+                                      jobs, extra=("-lpthread",))
+    if verbose:
+        for k, v in out.items():
+            print(f"[dli.build] {k}: {v} ({v.stat().st_size // 1024} KiB)")
+    return out
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", type=int, default=0)
+    a = ap.parse_args(argv)
+    build(force=a.force, jobs=a.j)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

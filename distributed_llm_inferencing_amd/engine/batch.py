@@ -1,0 +1,161 @@
+"""Per-step batch metadata shared by the scheduler, the model and the pipeline transport.
+
+A step is either all-prefill (packed prompts, causal varlen attention over the prompt) or
+all-decode (one token per running sequence, paged attention over the cache). The host
+builds the metadata once per step as ONE packed int32 buffer (``pack``/``unpack``) so it
+can travel with the activations between pipeline stages in a single message, and be
+copied into static device buffers for hipGraph replay.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+PREFILL, DECODE, EMPTY, STOP = 1, 2, 0, 3
+HEADER_LEN = 16
+
+
+@dataclass
+class StepMeta:
+    """Host-side description of one step (plain Python / numpy)."""
+    kind: int
+    seq_ids: List[int] = field(default_factory=list)       # engine slot ids, one per sequence
+    input_ids: Optional[np.ndarray] = None                  # [T] int32 (head stage only)
+    positions: Optional[np.ndarray] = None                  # [T] int32
+    slot_mapping: Optional[np.ndarray] = None               # [T] int32
+    seq_lens: Optional[np.ndarray] = None                   # [S] prefill: prompt lens
+    context_lens: Optional[np.ndarray] = None               # [S] decode: ctx incl. new token
+    block_tables: Optional[np.ndarray] = None               # [S, max_blocks] int32
+    temperature: Optional[np.ndarray] = None                # [S] float32
+    top_k: Optional[np.ndarray] = None                      # [S] int32
+    top_p: Optional[np.ndarray] = None                      # [S] float32
+    seeds: Optional[np.ndarray] = None                      # [S] int64
+    microbatch: int = 0
+    step_id: int = 0
+
+    @property
+    def num_seqs(self) -> int:
+        return len(self.seq_ids)
+
+    @property
+    def num_tokens(self) -> int:
+        return 0 if self.positions is None else int(self.positions.shape[0])
+
+    # ---- wire format: header (int64) + payload (int32) ------------------------------------
+    def pack(self) -> (np.ndarray, np.ndarray):
+        S, T = self.num_seqs, self.num_tokens
+        mb = 0 if self.block_tables is None else int(self.block_tables.shape[1])
+        parts = [np.asarray(self.seq_ids, dtype=np.int32),
+                 _i32(self.input_ids, T), _i32(self.positions, T), _i32(self.slot_mapping, T),
+                 _i32(self.seq_lens, S), _i32(self.context_lens, S),
+                 _i32(self.block_tables, S * mb).reshape(-1),
+                 _f32_as_i32(self.temperature, S), _i32(self.top_k, S),
+                 _f32_as_i32(self.top_p, S),
+                 (np.zeros(S, np.int64) if self.seeds is None else
+                  self.seeds.astype(np.int64)).view(np.int32)]
+        payload = np.concatenate(parts).astype(np.int32)
+        header = np.zeros(HEADER_LEN, dtype=np.int64)
+        header[:7] = [self.kind, S, T, mb, payload.shape[0], self.microbatch, self.step_id]
+        header[7] = 1 if self.input_ids is not None else 0
+        return header, payload
+
+    @staticmethod
+    def unpack(header: np.ndarray, payload: np.ndarray) -> "StepMeta":
+        kind, S, T, mb, _n, micro, step = (int(v) for v in header[:7])
+        o = 0
+
+        def take(n, dt=np.int32):
+            nonlocal o
+            a = payload[o:o + n]
+            o += n
+            return a.view(dt).copy() if dt != np.int32 else a.copy()
+
+        seq_ids = take(S).tolist()
+        input_ids = take(T)
+        positions, slots = take(T), take(T)
+        seq_lens, ctx = take(S), take(S)
+        bt = take(S * mb).reshape(S, mb)
+        temp = take(S, np.float32)
+        topk = take(S)
+        topp = take(S, np.float32)
+        seeds = take(2 * S).view(np.int64).copy()
+        return StepMeta(kind=kind, seq_ids=seq_ids,
+                        input_ids=input_ids if header[7] else None, positions=positions,
+                        slot_mapping=slots, seq_lens=seq_lens, context_lens=ctx,
+                        block_tables=bt, temperature=temp, top_k=topk, top_p=topp, seeds=seeds,
+                        microbatch=micro, step_id=step)
+
+
+def _i32(a, n):
+    if a is None:
+        return np.zeros(n, dtype=np.int32)
+    return np.ascontiguousarray(a, dtype=np.int32).reshape(-1)
+
+
+def _f32_as_i32(a, n):
+    if a is None:
+        return np.zeros(n, dtype=np.int32)
+    return np.ascontiguousarray(a, dtype=np.float32).reshape(-1).view(np.int32)
+
+
+@dataclass
+class DeviceBatch:
+    """Device tensors for one step (what the model consumes)."""
+    kind: int
+    num_seqs: int
+    num_tokens: int
+    input_ids: Optional[torch.Tensor]
+    positions: torch.Tensor
+    slot_mapping: torch.Tensor
+    cu_seqlens: Optional[torch.Tensor] = None
+    max_seqlen: int = 0
+    last_token_idx: Optional[torch.Tensor] = None
+    block_tables: Optional[torch.Tensor] = None
+    context_lens: Optional[torch.Tensor] = None
+    max_context: int = 0
+    temperature: Optional[torch.Tensor] = None
+    top_k: Optional[torch.Tensor] = None
+    top_p: Optional[torch.Tensor] = None
+    seeds: Optional[torch.Tensor] = None
+
+    @property
+    def is_prefill(self) -> bool:
+        return self.kind == PREFILL
+
+
+def to_device(meta: StepMeta, device, pin: bool = True) -> DeviceBatch:
+    """One H2D copy of the packed payload, then device-side views/casts."""
+    dev = torch.device(device)
+    S, T = meta.num_seqs, meta.num_tokens
+
+    def t(a, dt):
+        if a is None:
+            return None
+        x = torch.from_numpy(np.ascontiguousarray(a))
+        if dev.type == "cuda":
+            x = x.pin_memory() if pin else x
+            return x.to(dev, non_blocking=True).to(dt)
+        return x.to(dt)
+
+    db = DeviceBatch(kind=meta.kind, num_seqs=S, num_tokens=T,
+                     input_ids=t(meta.input_ids, torch.int32),
+                     positions=t(meta.positions, torch.int32),
+                     slot_mapping=t(meta.slot_mapping, torch.int32),
+                     temperature=t(meta.temperature, torch.float32),
+                     top_k=t(meta.top_k, torch.int32), top_p=t(meta.top_p, torch.float32),
+                     seeds=t(meta.seeds, torch.int64))
+    if meta.kind == PREFILL:
+        lens = np.asarray(meta.seq_lens, dtype=np.int64)
+        cu = np.zeros(S + 1, dtype=np.int32)
+        cu[1:] = np.cumsum(lens)
+        db.cu_seqlens = t(cu, torch.int32)
+        db.max_seqlen = int(lens.max()) if S else 0
+        db.last_token_idx = t(cu[1:] - 1, torch.int64)
+    else:
+        db.block_tables = t(meta.block_tables, torch.int32)
+        db.context_lens = t(meta.context_lens, torch.int32)
+        db.max_context = int(np.max(meta.context_lens)) if S else 0
+    return db

@@ -1,0 +1,157 @@
+"""Single-pipeline-stage inference engine (one GPU, or CPU): the worker's model runtime.
+
+Replaces the reference worker's ``model.generate`` call path (``worker/app.py:278-308``,
+L1 in SURVEY.md §1) with: C++ paged-KV allocator + continuous-batching scheduler +
+hipGraph decode on our HIP kernels. Multi-GPU pipelines use the same pieces through
+``parallel/pipeline.py``.
+"""
+from __future__ import annotations
+
+import itertools
+import time
+from dataclasses import dataclass, field
+from typing import Dict, Iterable, List, Optional, Union
+
+import numpy as np
+import torch
+
+from ..models.configs import ModelConfig, get_config
+from ..models.model import TransformerLM
+from ..runtime import BlockManager
+from ..tokenizer import load_tokenizer
+from .kv_cache import KVCache, auto_num_blocks
+from .runner import StageRunner
+from .scheduler import Scheduler
+from .sequence import RequestOutput, SamplingParams, Sequence
+
+
+@dataclass
+class EngineStats:
+    steps: int = 0
+    prefill_steps: int = 0
+    decode_steps: int = 0
+    tokens_out: int = 0
+    prompt_tokens: int = 0
+    busy_s: float = 0.0
+    finished: int = 0
+    latencies: List[float] = field(default_factory=list)
+
+    def snapshot(self) -> dict:
+        lat = sorted(self.latencies[-4096:])
+        pct = lambda q: lat[min(len(lat) - 1, int(q * len(lat)))] if lat else None  # noqa: E731
+        return {"steps": self.steps, "prefill_steps": self.prefill_steps,
+                "decode_steps": self.decode_steps, "output_tokens": self.tokens_out,
+                "prompt_tokens": self.prompt_tokens, "finished_requests": self.finished,
+                "busy_s": round(self.busy_s, 4),
+                "tokens_per_s": (self.tokens_out / self.busy_s) if self.busy_s > 0 else 0.0,
+                "p50_latency_s": pct(0.5), "p99_latency_s": pct(0.99)}
+
+
+def seq_to_output(seq: Sequence, tokenizer=None) -> RequestOutput:
+    end = seq.finish_time or time.perf_counter()
+    out = RequestOutput(request_id=seq.request_id, prompt_ids=seq.prompt_ids,
+                        output_ids=list(seq.output_ids), finish_reason=seq.finish_reason or "",
+                        latency_s=end - seq.arrival,
+                        ttft_s=(seq.first_token_time - seq.arrival) if seq.first_token_time else None)
+    if tokenizer is not None:
+        # HF semantics: generate() returns prompt + continuation; the reference decodes
+        # outputs[0] (prompt included) with skip_special_tokens=True (worker/app.py:308)
+        out.text = tokenizer.decode(out.all_ids, skip_special_tokens=True)
+    return out
+
+
+class LLMEngine:
+    def __init__(self, model: Union[str, ModelConfig], device: str = "cpu",
+                 dtype=torch.bfloat16, max_batch: int = 256, max_model_len: int = 2048,
+                 block_size: int = 16, num_blocks: Optional[int] = None,
+                 kv_fraction: float = 0.85, seed: int = 0, use_graphs: Optional[bool] = None,
+                 params: Optional[Dict[str, torch.Tensor]] = None, tokenizer_path=None,
+                 max_prefill_tokens: int = 16384, num_layers: Optional[int] = None):
+        self.cfg = get_config(model, num_layers) if isinstance(model, str) else model
+        self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        cfg = self.cfg
+        if params is None:
+            self.model = TransformerLM.random(cfg, device=self.device, dtype=dtype, seed=seed)
+        else:
+            self.model = TransformerLM(cfg, {k: v.to(self.device) for k, v in params.items()},
+                                       device=self.device)
+        max_model_len = min(max_model_len, cfg.max_position)
+        if num_blocks is None:
+            num_blocks = auto_num_blocks(cfg, cfg.num_layers, block_size, self.device,
+                                         kv_fraction,
+                                         cap_tokens=max(max_batch * max_model_len, 1 << 16))
+        self.kv = KVCache(cfg, cfg.num_layers, num_blocks, block_size, self.device, dtype)
+        self.bm = BlockManager(num_blocks, block_size)
+        self.scheduler = Scheduler(self.bm, max_seqs_per_mb=max_batch,
+                                   max_prefill_tokens=max_prefill_tokens,
+                                   eos_token_id=cfg.eos_token_id, max_model_len=max_model_len)
+        self.runner = StageRunner(self.model, self.kv, max_batch, self.scheduler.table_width,
+                                  use_graphs=use_graphs)
+        self.tokenizer = load_tokenizer(cfg, tokenizer_path)
+        self.stats = EngineStats()
+        self._ids = itertools.count()
+        self.max_batch = max_batch
+        self.max_model_len = max_model_len
+
+    # ------------------------------------------------------------------ API
+    def add_request(self, prompt: Union[str, List[int]], params: Optional[SamplingParams] = None,
+                    request_id: Optional[str] = None) -> str:
+        rid = request_id or f"req-{next(self._ids)}"
+        ids = self.tokenizer.encode(prompt) if isinstance(prompt, str) else list(prompt)
+        self.scheduler.add_request(rid, ids, params)
+        return rid
+
+    def abort(self, request_id: str) -> bool:
+        return self.scheduler.abort(request_id)
+
+    def has_work(self) -> bool:
+        return self.scheduler.has_work()
+
+    def warmup(self, buckets=None):
+        """Capture decode graphs ahead of serving (and touch every GEMM plan)."""
+        self.runner.capture(buckets)
+
+    def step(self) -> List[RequestOutput]:
+        meta = self.scheduler.schedule(0)
+        if meta is not None:
+            t0 = time.perf_counter()
+            tokens = self.runner.run(meta)
+            tok = tokens.cpu().numpy() if tokens.is_cuda else tokens.numpy()
+            self.scheduler.update(meta, tok)
+            self.stats.busy_s += time.perf_counter() - t0
+            self.stats.steps += 1
+            self.stats.tokens_out += meta.num_seqs
+            if meta.kind == 1:
+                self.stats.prefill_steps += 1
+                self.stats.prompt_tokens += meta.num_tokens
+            else:
+                self.stats.decode_steps += 1
+        outs = []
+        for seq in self.scheduler.pop_finished():
+            o = seq_to_output(seq, self.tokenizer)
+            self.stats.finished += 1
+            self.stats.latencies.append(o.latency_s)
+            outs.append(o)
+        return outs
+
+    def generate(self, prompts: Iterable[Union[str, List[int]]],
+                 params: Optional[SamplingParams] = None) -> List[RequestOutput]:
+        rids = [self.add_request(p, params) for p in prompts]
+        done: Dict[str, RequestOutput] = {}
+        while self.has_work():
+            for o in self.step():
+                done[o.request_id] = o
+        for o in self.step():           # flush requests finished at admission
+            done[o.request_id] = o
+        return [done[r] for r in rids]
+
+    def memory_report(self) -> dict:
+        rep = {"weights_bytes": self.model.param_bytes(), "kv_bytes": self.kv.nbytes,
+               "kv_capacity_tokens": self.kv.capacity_tokens,
+               "num_blocks": self.kv.num_blocks, "free_blocks": self.bm.num_free}
+        if self.device.type == "cuda":
+            free, total = torch.cuda.mem_get_info(self.device)
+            rep.update({"hbm_free": free, "hbm_total": total})
+        return rep

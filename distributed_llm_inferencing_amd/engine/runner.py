@@ -1,0 +1,182 @@
+"""Executes steps of one pipeline stage on its device, with hipGraph-captured decode.
+
+Decode steps have a fixed shape per batch-size bucket, so each bucket's whole stage forward
+(all layers, and on the last stage the LM head + sampler) is captured once into a
+``torch.cuda.CUDAGraph`` (a hipGraph on ROCm) and replayed: one graph launch per step per
+stage instead of ~10 kernel launches per layer. All per-step metadata
+lives in ONE static int32 device buffer refreshed by ONE pinned H2D copy before replay.
+Padded rows (bucket > live sequences) carry slot = -1 (no KV write) and context 0.
+
+Prefill steps (variable packed length) run eagerly.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+from ..models.model import TransformerLM
+from .batch import DECODE, PREFILL, DeviceBatch, StepMeta, to_device
+from .kv_cache import KVCache
+
+DEFAULT_BUCKETS = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192, 256, 320, 384, 448, 512)
+
+
+class StageRunner:
+    def __init__(self, model: TransformerLM, kv: KVCache, max_batch: int, table_width: int,
+                 use_graphs: Optional[bool] = None, buckets=DEFAULT_BUCKETS):
+        self.model = model
+        self.kv = kv
+        self.kv_layers = kv.layers()
+        self.device = model.device
+        self.max_batch = max_batch
+        self.W = table_width
+        if use_graphs is None:
+            use_graphs = self.device.type == "cuda" and os.environ.get("DLI_NO_GRAPHS", "0") != "1"
+        self.use_graphs = use_graphs
+        self.buckets = sorted({b for b in buckets if b < max_batch} | {max_batch})
+        self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
+        self.graph_out: Dict[int, torch.Tensor] = {}
+        self._pool = None
+        if self.use_graphs:
+            self._init_static()
+
+    # ------------------------------------------------------------------ static buffers
+    def _init_static(self):
+        B, W = self.max_batch, self.W
+        # layout (int32 words): ids | pos | slots | ctx | temp | topk | topp | seeds(2B) | tables(B*W)
+        self._off = {}
+        o = 0
+        for name, n in (("ids", B), ("pos", B), ("slots", B), ("ctx", B), ("temp", B),
+                        ("topk", B), ("topp", B), ("seeds", 2 * B), ("tables", B * W)):
+            self._off[name] = (o, n)
+            o += n
+        self._nwords = o
+        self.meta_dev = torch.zeros(o, dtype=torch.int32, device=self.device)
+        self.meta_host = torch.zeros(o, dtype=torch.int32).pin_memory()
+        self._host_np = self.meta_host.numpy()
+        self._upload_done = torch.cuda.Event()      # pinned buffer reuse guard
+        self.hidden_in = None
+        if not self.model.is_first:
+            self.hidden_in = torch.zeros(B, self.model.cfg.hidden_size, dtype=torch.bfloat16,
+                                         device=self.device)
+
+    def _view(self, name, b, dtype=torch.int32):
+        o, n = self._off[name]
+        v = self.meta_dev[o:o + n]
+        if dtype == torch.float32:
+            v = v.view(torch.float32)
+        elif dtype == torch.int64:
+            v = v.view(torch.int64)
+        if name == "tables":
+            return v.view(self.max_batch, self.W)[:b]
+        return v[:b]
+
+    def _static_batch(self, b: int) -> DeviceBatch:
+        return DeviceBatch(kind=DECODE, num_seqs=b, num_tokens=b,
+                           input_ids=self._view("ids", b), positions=self._view("pos", b),
+                           slot_mapping=self._view("slots", b),
+                           block_tables=self._view("tables", b),
+                           context_lens=self._view("ctx", b),
+                           max_context=self.W * self.kv.block_size,
+                           temperature=self._view("temp", b, torch.float32),
+                           top_k=self._view("topk", b), top_p=self._view("topp", b, torch.float32),
+                           seeds=self._view("seeds", b, torch.int64))
+
+    def _fill_host(self, meta: StepMeta, b: int):
+        self._upload_done.synchronize()             # previous async H2D has consumed the buffer
+        h = self._host_np
+        S = meta.num_seqs
+
+        def put(name, arr, pad):
+            o, _ = self._off[name]
+            a = np.asarray(arr).reshape(-1)
+            h[o:o + a.shape[0]] = a.view(np.int32) if a.dtype != np.int32 else a
+            extra = (b - S) * (2 if name == "seeds" else 1)
+            if extra > 0:
+                h[o + a.shape[0]:o + a.shape[0] + extra] = pad
+        put("ids", meta.input_ids if meta.input_ids is not None else np.zeros(S, np.int32), 0)
+        put("pos", meta.positions, 0)
+        put("slots", meta.slot_mapping, -1)
+        put("ctx", meta.context_lens, 0)
+        put("temp", meta.temperature.astype(np.float32), 0)
+        put("topk", meta.top_k, 1)
+        put("topp", meta.top_p.astype(np.float32), np.float32(1.0).view(np.int32))
+        put("seeds", meta.seeds.astype(np.int64), 0)
+        o, _ = self._off["tables"]
+        tb = np.asarray(meta.block_tables, dtype=np.int32)
+        if tb.shape[1] != self.W:
+            t2 = np.zeros((S, self.W), np.int32)
+            t2[:, :min(self.W, tb.shape[1])] = tb[:, :self.W]
+            tb = t2
+        h[o:o + S * self.W] = tb.reshape(-1)
+        if b > S:
+            h[o + S * self.W:o + b * self.W] = 0
+
+    def _upload(self, b: int):
+        # tables occupy the tail; copy everything up to the last used table row
+        o, _ = self._off["tables"]
+        n = o + b * self.W
+        self.meta_dev[:n].copy_(self.meta_host[:n], non_blocking=True)
+        self._upload_done.record()
+
+    def _bucket(self, S: int) -> int:
+        for b in self.buckets:
+            if b >= S:
+                return b
+        raise ValueError(f"decode batch {S} exceeds max_batch {self.max_batch}")
+
+    # ------------------------------------------------------------------ capture
+    def _forward_static(self, b: int):
+        db = self._static_batch(b)
+        hidden = self.hidden_in[:b] if self.hidden_in is not None else None
+        return self.model.forward(db, self.kv_layers, hidden=hidden)
+
+    def capture(self, buckets=None):
+        """Warm up and capture decode graphs for the given buckets (default: all)."""
+        if not self.use_graphs:
+            return
+        for b in (buckets or self.buckets):
+            if b in self.graphs:
+                continue
+            # warmup: all rows padded (slot -1, ctx 0) -> no cache writes, no attention reads
+            h = self._host_np
+            h[:] = 0
+            for name, pad in (("slots", -1), ("topk", 1)):
+                o, n = self._off[name]
+                h[o:o + n] = pad
+            self.meta_dev.copy_(self.meta_host)
+            s = torch.cuda.Stream(self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):
+                for _ in range(2):
+                    self._forward_static(b)
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            torch.cuda.synchronize(self.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self._pool):
+                out = self._forward_static(b)
+            if self._pool is None:
+                self._pool = g.pool()
+            self.graphs[b] = g
+            self.graph_out[b] = out
+        torch.cuda.synchronize(self.device)
+
+    # ------------------------------------------------------------------ execution
+    def run(self, meta: StepMeta, hidden: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Returns int32 tokens [S] on the last stage, else the hidden state [T, D]."""
+        if meta.kind == DECODE and self.use_graphs and meta.num_seqs <= self.max_batch:
+            S = meta.num_seqs
+            b = self._bucket(S)
+            if b not in self.graphs:
+                self.capture([b])
+            self._fill_host(meta, b)
+            self._upload(b)
+            if self.hidden_in is not None:
+                self.hidden_in[:S].copy_(hidden[:S])
+            self.graphs[b].replay()
+            return self.graph_out[b][:S]
+        db = to_device(meta, self.device)
+        return self.model.forward(db, self.kv_layers, hidden=hidden)

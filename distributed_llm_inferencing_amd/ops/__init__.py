@@ -1,0 +1,308 @@
+"""Op API used by the models. CUDA(HIP) tensors -> gfx950 kernels; CPU tensors -> PyTorch
+reference (``ops/reference.py``). There is no silent fallback on a GPU: if the kernel
+library is missing, the first GPU op raises (``_native.require_native``).
+
+All functions take/return torch tensors and launch on torch's current stream.
+"""
+from __future__ import annotations
+
+import math
+import time
+from typing import Optional
+
+import torch
+
+from . import _native as N
+from . import gemm as G
+from . import reference as R
+
+_native_call = N.call
+_p = N.ptr
+
+
+def _use_native(t: torch.Tensor) -> bool:
+    return t.is_cuda and N.native_enabled()
+
+
+def _st():
+    return N.stream_ptr()
+
+
+# ----------------------------------------------------------------------------- norms
+def rmsnorm(x, w, eps, residual_copy: Optional[torch.Tensor] = None):
+    """out = rmsnorm(x)*w; if residual_copy is given it receives a copy of x."""
+    if not _use_native(x):
+        if residual_copy is not None:
+            residual_copy.copy_(x)
+        return R.rmsnorm(x, w, eps)
+    out = torch.empty_like(x)
+    rows, dim = x.shape
+    _native_call("dli_rmsnorm", _p(out), _p(residual_copy), _p(x), _p(w), rows, dim, eps, _st())
+    return out
+
+
+def add_rmsnorm(x, residual, w, eps):
+    """residual += x (in place); returns rmsnorm(residual)*w."""
+    if not _use_native(x):
+        out, r = R.fused_add_rmsnorm(x, residual, w, eps)
+        residual.copy_(r)
+        return out
+    out = torch.empty_like(x)
+    rows, dim = x.shape
+    _native_call("dli_fused_add_rmsnorm", _p(out), _p(residual), _p(x), _p(w), rows, dim, eps,
+                 _st())
+    return out
+
+
+def layernorm(x, w, b, eps, residual_copy: Optional[torch.Tensor] = None):
+    if not _use_native(x):
+        if residual_copy is not None:
+            residual_copy.copy_(x)
+        return R.layernorm(x, w, b, eps)
+    out = torch.empty_like(x)
+    rows, dim = x.shape
+    _native_call("dli_layernorm", _p(out), _p(residual_copy), _p(x), _p(w), _p(b), rows, dim,
+                 eps, _st())
+    return out
+
+
+def add_layernorm(x, residual, w, b, eps):
+    if not _use_native(x):
+        out, r = R.fused_add_layernorm(x, residual, w, b, eps)
+        residual.copy_(r)
+        return out
+    out = torch.empty_like(x)
+    rows, dim = x.shape
+    _native_call("dli_fused_add_layernorm", _p(out), _p(residual), _p(x), _p(w), _p(b), rows,
+                 dim, eps, _st())
+    return out
+
+
+# ----------------------------------------------------------------------------- embedding
+def embedding(ids, table, pos_table=None, positions=None):
+    if not _use_native(table):
+        return R.embedding(ids, table, pos_table, positions)
+    T = ids.shape[0]
+    out = torch.empty(T, table.shape[1], dtype=table.dtype, device=table.device)
+    _native_call("dli_embedding", _p(out), _p(ids), _p(table), _p(pos_table), _p(positions), T,
+                 table.shape[1], _st())
+    return out
+
+
+# ----------------------------------------------------------------------------- GEMM
+def _gemm_native(x, w, epi: str, bias=None, out=None, plan: Optional[G.GemmPlan] = None,
+                 groups: int = 1, group_off=None, rows_per_group: Optional[int] = None):
+    M, K = x.shape
+    Nn = w.shape[-2]
+    if plan is None:
+        plan = G.plan(M if group_off is None else rows_per_group, Nn, K, epi)
+    out_n = Nn // 2 if epi == "silu_mul" else Nn
+    if out is None:
+        dt = torch.float32 if epi == "f32" else x.dtype
+        out = torch.empty(M, out_n, dtype=dt, device=x.device)
+    if plan.backend == "hipblaslt" and epi == "none" and group_off is None:
+        torch.matmul(x, w.t(), out=out)
+        return out
+    splits = plan.splits if group_off is None else 1
+    ws = None
+    if splits > 1:
+        ws = G.workspace(x.device, splits * M * Nn * 4)
+    m_arg = M if group_off is None else rows_per_group
+    _native_call("dli_gemm", _p(x), x.stride(0), _p(w), w.stride(-2), _p(out), out.stride(0),
+                 m_arg, Nn, K, G.EPI[epi], plan.tile, splits, _p(bias), _p(ws), _p(group_off),
+                 groups, _st())
+    return out
+
+
+def linear(x, w, bias=None, epi: str = "none", out=None):
+    """y = epi(x @ w.T (+bias)). epi in {none, f32, silu_mul, bias_gelu, bias}.
+    silu_mul expects the 16-row interleaved gate/up weight and returns width N/2."""
+    if bias is not None and epi == "none":
+        epi = "bias"
+    if not _use_native(x):
+        if epi == "silu_mul":
+            y = R.silu_mul(R.linear(x, w))
+        elif epi == "f32":
+            y = R.linear(x, w, out_dtype=torch.float32)
+        elif epi == "bias_gelu":
+            y = R.gelu_tanh(R.linear(x, w, bias))
+        else:
+            y = R.linear(x, w, bias)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+    if x.stride(-1) != 1 or w.stride(-1) != 1:
+        raise ValueError("linear: inner dims must be contiguous")
+    return _gemm_native(x, w, epi, bias=bias, out=out)
+
+
+def silu_mul(gu):
+    if not _use_native(gu):
+        return R.silu_mul(gu)
+    T, F2 = gu.shape
+    out = torch.empty(T, F2 // 2, dtype=gu.dtype, device=gu.device)
+    _native_call("dli_silu_mul", _p(out), _p(gu), T, F2 // 2, _st())
+    return out
+
+
+def bias_act_(x, bias, act: str = "none"):
+    if not _use_native(x):
+        y = x.float() + (bias.float() if bias is not None else 0)
+        if act == "gelu":
+            y = torch.nn.functional.gelu(y, approximate="tanh")
+        x.copy_(y.to(x.dtype))
+        return x
+    T, Nn = x.shape
+    _native_call("dli_bias_act", _p(x), _p(bias), T, Nn, 1 if act == "gelu" else 0, _st())
+    return x
+
+
+# ----------------------------------------------------------------------------- RoPE / KV cache
+def rope_and_cache(qkv, positions, slot_mapping, cos_sin, k_cache, v_cache, hq, hkv, hd,
+                   use_rope: bool = True):
+    """In-place RoPE on q,k inside qkv + paged cache write. Returns views (q, k, v)."""
+    if not _use_native(qkv):
+        return R.rope_and_cache(qkv, positions, slot_mapping, cos_sin, k_cache, v_cache, hq, hkv,
+                                hd, use_rope)
+    T = qkv.shape[0]
+    bs = k_cache.shape[2] if k_cache is not None else 16
+    _native_call("dli_rope_cache", _p(qkv), qkv.stride(0), _p(positions), _p(slot_mapping),
+                 _p(cos_sin), _p(k_cache), _p(v_cache), T, hq, hkv, hd, bs, int(use_rope), _st())
+    return R.split_qkv(qkv, hq, hkv, hd)
+
+
+# ----------------------------------------------------------------------------- attention
+def prefill_attention(qkv, cu_seqlens, max_seqlen: int, hq, hkv, hd, scale, out=None):
+    """Causal varlen attention over the packed prompt tokens in ``qkv``; returns [T, Hq*hd]."""
+    T = qkv.shape[0]
+    if not _use_native(qkv):
+        q, k, v = R.split_qkv(qkv, hq, hkv, hd)
+        o = R.prefill_attention(q, k, v, cu_seqlens, scale).reshape(T, hq * hd)
+        if out is not None:
+            out.copy_(o)
+            return out
+        return o
+    if out is None:
+        out = torch.empty(T, hq * hd, dtype=qkv.dtype, device=qkv.device)
+    nseq = cu_seqlens.shape[0] - 1
+    _native_call("dli_prefill_attention", _p(out), out.stride(0), _p(qkv), qkv.stride(0),
+                 _p(cu_seqlens), nseq, max_seqlen, hq, hkv, hd, scale, _st())
+    return out
+
+
+def decode_num_splits(B: int, hkv: int, max_context: int) -> int:
+    """KV splits so that B*Hkv*splits workgroups cover the chip for long contexts."""
+    wgs = B * hkv
+    splits = 1
+    while wgs * splits < 512 and max_context // (splits * 2) >= 256:
+        splits *= 2
+    return splits
+
+
+def decode_attention(qkv, k_cache, v_cache, block_tables, context_lens, max_context: int,
+                     hq, hkv, hd, scale, out=None, num_splits: Optional[int] = None):
+    """One query per row of ``qkv`` (rows = sequences) against its paged KV; [B, Hq*hd]."""
+    B = qkv.shape[0]
+    if not _use_native(qkv):
+        q = qkv[:, : hq * hd].reshape(B, hq, hd)
+        o = R.decode_attention(q, k_cache, v_cache, block_tables, context_lens,
+                               scale).reshape(B, hq * hd)
+        if out is not None:
+            out.copy_(o)
+            return out
+        return o
+    if out is None:
+        out = torch.empty(B, hq * hd, dtype=qkv.dtype, device=qkv.device)
+    if num_splits is None:
+        num_splits = decode_num_splits(B, hkv, max_context)
+    ws = None
+    if num_splits > 1:
+        nbytes = B * hq * num_splits * (hd + 2) * 4
+        ws = G.workspace(qkv.device, nbytes)
+    bs = k_cache.shape[2]
+    _native_call("dli_decode_attention", _p(out), _p(qkv), qkv.stride(0), _p(k_cache),
+                 _p(v_cache), _p(block_tables), block_tables.stride(0), _p(context_lens), B, hq,
+                 hkv, hd, bs, scale, max_context, num_splits, _p(ws), _st())
+    return out
+
+
+# ----------------------------------------------------------------------------- sampling
+def sample(logits, temperature, top_k, top_p, seeds, generator=None):
+    """logits fp32 [B, V] -> int32 tokens [B]. temperature<=0 -> greedy."""
+    if not _use_native(logits):
+        return R.sample(logits, temperature, top_k, top_p, generator=generator)
+    B, V = logits.shape
+    out = torch.empty(B, dtype=torch.int32, device=logits.device)
+    _native_call("dli_sample", _p(out), _p(logits), logits.stride(0), B, V, _p(temperature),
+                 _p(top_k), _p(top_p), _p(seeds), _st())
+    return out
+
+
+# ----------------------------------------------------------------------------- MoE
+def moe_route(router_logits, k: int):
+    if not _use_native(router_logits):
+        return R.router_topk(router_logits, k)
+    T, E = router_logits.shape
+    w = torch.empty(T, k, dtype=torch.float32, device=router_logits.device)
+    ids = torch.empty(T, k, dtype=torch.int32, device=router_logits.device)
+    _native_call("dli_moe_route", _p(w), _p(ids), _p(router_logits), T, E, k, _st())
+    return w, ids
+
+
+def moe_mlp(x, w_gu, w_down, topk_w, topk_ids, expert_offset: int = 0):
+    """Experts [expert_offset, expert_offset+E_local) of one MoE layer; returns the weighted
+    sum over the token's selected local experts (zeros for tokens routed elsewhere)."""
+    if not _use_native(x):
+        return R.moe_mlp(x, w_gu, w_down, topk_w, topk_ids, expert_offset)
+    T, D = x.shape
+    k = topk_ids.shape[1]
+    E_local, F2, _ = w_gu.shape
+    n = T * k
+    dev = x.device
+    offsets = torch.empty(E_local + 1, dtype=torch.int32, device=dev)
+    pos = torch.empty(n, dtype=torch.int32, device=dev)
+    src = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    _native_call("dli_moe_align", _p(offsets), _p(pos), _p(src), _p(topk_ids), n, k,
+                 expert_offset, E_local, _st())
+    # permuted rows: at most n (all local); rows past offsets[E_local] are never touched
+    xp = torch.empty(max(n, 1), D, dtype=x.dtype, device=dev)
+    _native_call("dli_moe_gather", _p(xp), _p(x), _p(src), n, D, _p(offsets[E_local:]), _st())
+    act = torch.empty(max(n, 1), F2 // 2, dtype=x.dtype, device=dev)
+    _gemm_native(xp, w_gu, "silu_mul", out=act, groups=E_local, group_off=offsets,
+                 rows_per_group=n)
+    y = torch.empty(max(n, 1), D, dtype=x.dtype, device=dev)
+    _gemm_native(act, w_down, "none", out=y, groups=E_local, group_off=offsets,
+                 rows_per_group=n)
+    out = torch.empty_like(x)
+    _native_call("dli_moe_combine", _p(out), _p(y), _p(topk_w), _p(pos), T, k, D, _st())
+    return out
+
+
+# ----------------------------------------------------------------------------- misc
+def native_library_path():
+    return N.loaded_path()
+
+
+def benchmark(fn, iters: int = 20, warmup: int = 3) -> float:
+    """Median milliseconds of fn() on the current stream (GPU) or wall clock (CPU)."""
+    for _ in range(warmup):
+        fn()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+        times = []
+        for _ in range(iters):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            fn()
+            e.record()
+            e.synchronize()
+            times.append(s.elapsed_time(e))
+    else:
+        times = []
+        for _ in range(iters):
+            t0 = time.perf_counter()
+            fn()
+            times.append((time.perf_counter() - t0) * 1e3)
+    times.sort()
+    return times[len(times) // 2]

@@ -1,0 +1,113 @@
+"""GEMM planning: tile shape / split-K choice for the MFMA kernel, plus optional autotune.
+
+The projection GEMMs of a decode step are skinny (M = batch) and of a prefill step fat
+(M = batch * prompt). The planner picks, per (M, N, K, epilogue):
+
+* a tile from {64x64, 64x128, 128x128, 128x256, 256x128} sized to M,
+* a split-K factor so the grid covers the 256 CUs (cdna_hip_programming.md §5 'Projection
+  GEMM at M = 256': choose SPLITK so that tiles * SPLITK ~ 0.5-1x the CU count),
+* the backend. Fused epilogues (SiLU*mul, bias+GELU, fp32 logits) always run on our kernel.
+  Plain bf16 GEMMs may run on hipBLASLt (torch.matmul) if the autotuner measured it
+  faster on this shape (``DLI_GEMM_AUTOTUNE=1``), or if forced with ``DLI_GEMM_BACKEND``.
+
+Split-K partial slabs live in a grow-only per-device workspace; engines warm every shape
+up before hipGraph capture so no allocation happens inside a capture.
+"""
+from __future__ import annotations
+
+import os
+import threading
+from dataclasses import dataclass
+
+import torch
+
+TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256), 4: (256, 128)}
+EPI = {"none": 0, "f32": 1, "silu_mul": 2, "bias_gelu": 3, "bias": 4}
+NUM_CUS = int(os.environ.get("DLI_NUM_CUS", "256"))
+
+
+@dataclass(frozen=True)
+class GemmPlan:
+    backend: str      # "dli" | "hipblaslt"
+    tile: int
+    splits: int
+
+
+_plan_cache: dict = {}
+_ws_lock = threading.Lock()
+_workspaces: dict = {}
+
+
+def workspace(device: torch.device, nbytes: int) -> torch.Tensor:
+    """Grow-only scratch (bytes) per device."""
+    key = (device.type, device.index)
+    with _ws_lock:
+        ws = _workspaces.get(key)
+        if ws is None or ws.numel() < nbytes:
+            ws = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+            _workspaces[key] = ws
+        return ws
+
+
+def _heuristic(M: int, N: int, K: int, epi: str) -> GemmPlan:
+    if M <= 64:
+        tile = 0 if N <= 8192 else 1
+    elif M <= 256:
+        tile = 2
+    else:
+        tile = 2
+    bm, bn = TILES[tile]
+    tiles = -(-M // bm) * -(-N // bn)
+    splits = 1
+    # split K until the grid covers ~the CU count, keeping >= 512 K per slice
+    while (tiles * splits * 2 <= NUM_CUS and K % (64 * splits * 2) == 0
+           and K // (splits * 2) >= 512):
+        splits *= 2
+    return GemmPlan("dli", tile, splits)
+
+
+def _bucket(M: int) -> int:
+    b = 1
+    while b < M:
+        b <<= 1
+    return b
+
+
+def plan(M: int, N: int, K: int, epi: str) -> GemmPlan:
+    key = (_bucket(M), N, K, epi)
+    p = _plan_cache.get(key)
+    if p is not None:
+        return p
+    forced = os.environ.get("DLI_GEMM_BACKEND", "")
+    p = _heuristic(M, N, K, epi)
+    if forced == "hipblaslt" and epi == "none":
+        p = GemmPlan("hipblaslt", p.tile, 1)
+    _plan_cache[key] = p
+    return p
+
+
+def set_plan(M: int, N: int, K: int, epi: str, p: GemmPlan) -> None:
+    _plan_cache[(_bucket(M), N, K, epi)] = p
+
+
+def clear_plans() -> None:
+    _plan_cache.clear()
+
+
+def candidate_plans(M: int, N: int, K: int, epi: str):
+    out = []
+    for tile, (bm, bn) in TILES.items():
+        if M <= 64 and bm > 64:
+            continue
+        if M > 512 and bm < 128:
+            continue
+        for splits in (1, 2, 4, 8):
+            if K % (64 * splits) or K // splits < 256:
+                continue
+            tiles = -(-M // bm) * -(-N // bn)
+            if splits > 1 and tiles * splits > 4 * NUM_CUS:
+                continue
+            out.append(GemmPlan("dli", tile, splits))
+    if epi == "none":
+        out.append(GemmPlan("hipblaslt", 0, 1))
+    return out

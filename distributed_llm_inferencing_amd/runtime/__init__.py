@@ -1,0 +1,172 @@
+"""Bindings for the host C++ runtime (``lib/libdli_runtime.so``, sources in csrc/runtime):
+
+* ``BlockManager`` — paged-KV block allocator + batched block-table / slot-mapping builders
+* ``SafetensorsFile`` — mmap'd safetensors reader with a pinned-staging ring feeding
+  ``hipMemcpyAsync`` (GPU) or plain memcpy (CPU)
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+from pathlib import Path
+from typing import Dict, List, Sequence
+
+import numpy as np
+import torch
+
+LIB_PATH = Path(__file__).resolve().parent.parent / "lib" / "libdli_runtime.so"
+_lib = None
+_lock = threading.Lock()
+
+_P, _I, _LL = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong
+_SIGS = {
+    "dli_bm_create": ([_I, _I], _P),
+    "dli_bm_destroy": ([_P], None),
+    "dli_bm_num_free": ([_P], _I),
+    "dli_bm_num_blocks": ([_P], _I),
+    "dli_bm_block_size": ([_P], _I),
+    "dli_bm_blocks_needed": ([_P, _LL, _LL], _I),
+    "dli_bm_ensure": ([_P, _LL, _LL], _I),
+    "dli_bm_free": ([_P, _LL], _I),
+    "dli_bm_table": ([_P, _LL, _P, _I], _I),
+    "dli_bm_fill_tables": ([_P, _P, _I, _P, _I], _I),
+    "dli_bm_slot_mapping": ([_P, _P, _P, _P, _I, _P], _I),
+    "dli_st_open": ([ctypes.c_char_p], _P),
+    "dli_st_close": ([_P], None),
+    "dli_st_count": ([_P], _I),
+    "dli_st_info": ([_P, _I, ctypes.c_char_p, _I, ctypes.c_char_p, _I, _P, _P, _P], _I),
+    "dli_st_find": ([_P, ctypes.c_char_p], _I),
+    "dli_st_copy_to_host": ([_P, _I, _P], _I),
+    "dli_st_load_to_device": ([_P, _P, _P, _I, _P], _LL),
+}
+
+
+def lib():
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not LIB_PATH.exists():
+                from .. import build as _build
+                _build.build(verbose=False)
+            L = ctypes.CDLL(str(LIB_PATH))
+            for name, (args, res) in _SIGS.items():
+                fn = getattr(L, name)
+                fn.argtypes = args
+                fn.restype = res
+            _lib = L
+    return _lib
+
+
+def _np_ptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class BlockManager:
+    """Paged KV allocator (C++). Sequence ids are arbitrary 64-bit ints."""
+
+    def __init__(self, num_blocks: int, block_size: int):
+        self._h = lib().dli_bm_create(int(num_blocks), int(block_size))
+        if not self._h:
+            raise ValueError("invalid block manager geometry")
+        self.num_blocks = int(num_blocks)
+        self.block_size = int(block_size)
+
+    def __del__(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h and _lib is not None:
+            _lib.dli_bm_destroy(h)
+
+    @property
+    def num_free(self) -> int:
+        return lib().dli_bm_num_free(self._h)
+
+    def blocks_needed(self, seq_id: int, total_tokens: int) -> int:
+        return lib().dli_bm_blocks_needed(self._h, seq_id, total_tokens)
+
+    def ensure(self, seq_id: int, total_tokens: int) -> bool:
+        return lib().dli_bm_ensure(self._h, seq_id, total_tokens) >= 0
+
+    def free(self, seq_id: int) -> int:
+        return lib().dli_bm_free(self._h, seq_id)
+
+    def table(self, seq_id: int) -> List[int]:
+        cap = max(1, self.num_blocks)
+        buf = np.zeros(min(cap, 1 << 16), dtype=np.int32)
+        n = lib().dli_bm_table(self._h, seq_id, _np_ptr(buf), buf.shape[0])
+        return buf[:n].tolist()
+
+    def fill_tables(self, seq_ids: Sequence[int], max_blocks: int) -> np.ndarray:
+        ids = np.asarray(seq_ids, dtype=np.int64)
+        out = np.zeros((len(ids), max(1, max_blocks)), dtype=np.int32)
+        r = lib().dli_bm_fill_tables(self._h, _np_ptr(ids), len(ids), _np_ptr(out), out.shape[1])
+        if r < 0:
+            raise RuntimeError("block table wider than max_blocks")
+        return out
+
+    def slot_mapping(self, seq_ids, starts, counts) -> np.ndarray:
+        ids = np.asarray(seq_ids, dtype=np.int64)
+        st = np.asarray(starts, dtype=np.int32)
+        ct = np.asarray(counts, dtype=np.int32)
+        out = np.zeros(int(ct.sum()), dtype=np.int32)
+        r = lib().dli_bm_slot_mapping(self._h, _np_ptr(ids), _np_ptr(st), _np_ptr(ct), len(ids),
+                                      _np_ptr(out))
+        if r < 0:
+            raise RuntimeError("slot mapping beyond allocated blocks")
+        return out
+
+
+_DT = {"BF16": torch.bfloat16, "F16": torch.float16, "F32": torch.float32, "I32": torch.int32,
+       "I64": torch.int64, "U8": torch.uint8, "I8": torch.int8}
+
+
+class SafetensorsFile:
+    def __init__(self, path: str):
+        self.path = str(path)
+        self._h = lib().dli_st_open(self.path.encode())
+        if not self._h:
+            raise IOError(f"cannot open safetensors file {path}")
+        self.meta: Dict[str, tuple] = {}
+        self._index: Dict[str, int] = {}
+        name = ctypes.create_string_buffer(512)
+        dt = ctypes.create_string_buffer(16)
+        shape = (ctypes.c_longlong * 8)()
+        nd, nb = ctypes.c_int(), ctypes.c_longlong()
+        for i in range(lib().dli_st_count(self._h)):
+            lib().dli_st_info(self._h, i, name, 512, dt, 16, ctypes.byref(shape), ctypes.byref(nd),
+                              ctypes.byref(nb))
+            n = name.value.decode()
+            self.meta[n] = (dt.value.decode(), tuple(shape[d] for d in range(nd.value)), nb.value)
+            self._index[n] = i
+
+    def close(self):
+        if self._h:
+            lib().dli_st_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    def keys(self):
+        return list(self.meta)
+
+    def load(self, names=None, device="cpu") -> Dict[str, torch.Tensor]:
+        names = list(self.meta) if names is None else list(names)
+        dev = torch.device(device)
+        out = {n: torch.empty(self.meta[n][1], dtype=_DT[self.meta[n][0]], device=dev)
+               for n in names}
+        if dev.type == "cuda":
+            idx = (ctypes.c_int * len(names))(*[self._index[n] for n in names])
+            ptrs = (ctypes.c_void_p * len(names))(*[out[n].data_ptr() for n in names])
+            stream = torch.cuda.current_stream(dev).cuda_stream
+            r = lib().dli_st_load_to_device(self._h, idx, ptrs, len(names), stream)
+            if r < 0:
+                raise RuntimeError(f"device load failed ({r})")
+        else:
+            for n in names:
+                if lib().dli_st_copy_to_host(self._h, self._index[n],
+                                             ctypes.c_void_p(out[n].data_ptr())) != 0:
+                    raise RuntimeError(f"host load failed for {n}")
+        return out

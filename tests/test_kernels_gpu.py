@@ -1,0 +1,254 @@
+"""T3 kernel golden tests: every HIP kernel vs the PyTorch fp32 reference of the same op
+(ops/reference.py), on the GPU. Run on an MI355X via gpurun."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from distributed_llm_inferencing_amd import ops
+from distributed_llm_inferencing_amd.ops import gemm as G
+from distributed_llm_inferencing_amd.ops import reference as R
+
+pytestmark = pytest.mark.gpu
+BF = torch.bfloat16
+
+
+def rnd(*shape, dev, scale=1.0, dtype=BF):
+    return (torch.randn(*shape, device=dev) * scale).to(dtype)
+
+
+def close(a, b, rtol=2e-2, atol=2e-2):
+    a, b = a.float(), b.float()
+    err = (a - b).abs().max().item()
+    tol = atol + rtol * b.abs().max().item()
+    assert err <= tol, f"max err {err} > tol {tol}"
+
+
+@pytest.mark.parametrize("T,D", [(1, 256), (7, 768), (64, 4096), (33, 8192)])
+def test_rmsnorm_and_fused_add(gpu, T, D):
+    torch.manual_seed(0)
+    x, r, w = rnd(T, D, dev=gpu), rnd(T, D, dev=gpu), rnd(D, dev=gpu)
+    close(ops.rmsnorm(x, w, 1e-5), R.rmsnorm(x, w, 1e-5))
+    res = r.clone()
+    out = ops.add_rmsnorm(x, res, w, 1e-5)
+    ref_out, ref_res = R.fused_add_rmsnorm(x, r, w, 1e-5)
+    close(out, ref_out)
+    assert torch.equal(res, ref_res)
+    copy = torch.empty_like(x)
+    ops.rmsnorm(x, w, 1e-5, residual_copy=copy)
+    assert torch.equal(copy, x)
+
+
+@pytest.mark.parametrize("T,D", [(5, 768), (40, 256)])
+def test_layernorm_and_fused_add(gpu, T, D):
+    torch.manual_seed(1)
+    x, r, w, b = rnd(T, D, dev=gpu), rnd(T, D, dev=gpu), rnd(D, dev=gpu), rnd(D, dev=gpu)
+    close(ops.layernorm(x, w, b, 1e-5), R.layernorm(x, w, b, 1e-5))
+    res = r.clone()
+    out = ops.add_layernorm(x, res, w, b, 1e-5)
+    ro, rr = R.fused_add_layernorm(x, r, w, b, 1e-5)
+    close(out, ro)
+    assert torch.equal(res, rr)
+
+
+def test_embedding(gpu):
+    tab, pos = rnd(1000, 256, dev=gpu), rnd(64, 256, dev=gpu)
+    ids = torch.randint(0, 1000, (37,), device=gpu, dtype=torch.int32)
+    p = torch.randint(0, 64, (37,), device=gpu, dtype=torch.int32)
+    assert torch.equal(ops.embedding(ids, tab), R.embedding(ids, tab))
+    close(ops.embedding(ids, tab, pos, p), R.embedding(ids, tab, pos, p), rtol=1e-2, atol=1e-2)
+
+
+GEMM_SHAPES = [(1, 256, 256), (7, 768, 2304), (64, 4096, 4096), (100, 1000, 512),
+               (256, 6144, 4096), (300, 4096, 14336), (1024, 512, 1024), (33, 50257, 768)]
+
+
+@pytest.mark.parametrize("M,N,K", GEMM_SHAPES)
+def test_gemm_bf16_all_tiles(gpu, M, N, K):
+    torch.manual_seed(2)
+    x, w = rnd(M, K, dev=gpu), rnd(N, K, dev=gpu, scale=0.05)
+    ref = R.linear(x, w, out_dtype=torch.float32)
+    for tile in G.TILES:
+        for splits in (1, 2, 4):
+            if K % (64 * splits):
+                continue
+            out = ops._gemm_native(x, w, "none", plan=G.GemmPlan("dli", tile, splits))
+            close(out, ref, rtol=1e-2, atol=1e-2)
+
+
+def test_gemm_asymmetric_identity(gpu):
+    """A = I with asymmetric B catches a transposed C write (cdna_hip_programming.md §3)."""
+    n = 128
+    eye = torch.eye(n, device=gpu, dtype=BF)
+    w = (torch.arange(n * n, device=gpu).reshape(n, n) % 97).to(BF)
+    for tile in G.TILES:
+        out = ops._gemm_native(eye, w, "none", plan=G.GemmPlan("dli", tile, 1))
+        assert torch.equal(out, w.t().contiguous()), tile
+
+
+@pytest.mark.parametrize("epi", ["f32", "silu_mul", "bias_gelu", "bias"])
+@pytest.mark.parametrize("M,N,K", [(5, 512, 256), (128, 1024, 512), (260, 3072, 768)])
+def test_gemm_epilogues(gpu, epi, M, N, K):
+    torch.manual_seed(3)
+    x, w, b = rnd(M, K, dev=gpu), rnd(N, K, dev=gpu, scale=0.05), rnd(N, dev=gpu)
+    if epi == "silu_mul":
+        ref = R.silu_mul(R.linear(x, w).float().to(BF))
+    elif epi == "f32":
+        ref = R.linear(x, w, out_dtype=torch.float32)
+    elif epi == "bias_gelu":
+        ref = R.gelu_tanh(R.linear(x, w, b))
+    else:
+        ref = R.linear(x, w, b)
+    for tile in (0, 2):
+        for splits in (1, 2):
+            out = ops._gemm_native(x, w, epi, bias=b if "bias" in epi else None,
+                                   plan=G.GemmPlan("dli", tile, splits))
+            close(out, ref, rtol=2e-2, atol=2e-2)
+            if epi == "f32":
+                assert out.dtype == torch.float32
+
+
+def test_silu_mul_and_bias_act(gpu):
+    gu = rnd(9, 2 * 512, dev=gpu)
+    close(ops.silu_mul(gu), R.silu_mul(gu))
+    x, b = rnd(9, 768, dev=gpu), rnd(768, dev=gpu)
+    y = x.clone()
+    ops.bias_act_(y, b, "gelu")
+    close(y, R.gelu_tanh((x.float() + b.float()).to(BF)))
+
+
+def _paged_setup(gpu, lens, hq, hkv, hd, bs, nblk=64, seed=4):
+    torch.manual_seed(seed)
+    T = sum(lens)
+    qkv = rnd(T, (hq + 2 * hkv) * hd, dev=gpu)
+    pos = torch.cat([torch.arange(n) for n in lens]).to(gpu, torch.int32)
+    kc = torch.zeros(nblk, hkv, bs, hd, device=gpu, dtype=BF)
+    vc = torch.zeros(nblk, hkv, hd, bs, device=gpu, dtype=BF)
+    perm = torch.randperm(nblk).tolist()
+    tables, slots, o = [], [], 0
+    maxb = max(-(-n // bs) for n in lens)
+    for n in lens:
+        nb = -(-n // bs)
+        blocks = perm[o:o + nb]
+        o += nb
+        tables.append(blocks + [0] * (maxb - nb))
+        slots += [blocks[t // bs] * bs + t % bs for t in range(n)]
+    return (qkv, pos, torch.tensor(slots, device=gpu, dtype=torch.int32), kc, vc,
+            torch.tensor(tables, device=gpu, dtype=torch.int32))
+
+
+@pytest.mark.parametrize("hq,hkv,hd", [(32, 8, 128), (12, 12, 64), (4, 2, 64)])
+def test_rope_cache(gpu, hq, hkv, hd):
+    lens = [5, 17, 1]
+    qkv, pos, slots, kc, vc, _ = _paged_setup(gpu, lens, hq, hkv, hd, 16)
+    cs = R.rope_cos_sin(256, hd, 500000.0, device=gpu)
+    q1, kc1, vc1 = qkv.clone(), kc.clone(), vc.clone()
+    R.rope_and_cache(q1, pos, slots, cs, kc1, vc1, hq, hkv, hd)
+    q2 = qkv.clone()
+    ops.rope_and_cache(q2, pos, slots, cs, kc, vc, hq, hkv, hd)
+    close(q2, q1, rtol=1e-2, atol=1e-2)
+    close(kc, kc1, rtol=1e-2, atol=1e-2)
+    assert torch.equal(vc, vc1)
+
+
+@pytest.mark.parametrize("hq,hkv,hd", [(32, 8, 128), (12, 12, 64), (8, 1, 128)])
+@pytest.mark.parametrize("lens", [[1], [7, 33, 64], [130, 5]])
+def test_prefill_attention(gpu, hq, hkv, hd, lens):
+    qkv, *_ = _paged_setup(gpu, lens, hq, hkv, hd, 16)
+    cu = torch.tensor([0] + list(np.cumsum(lens)), device=gpu, dtype=torch.int32)
+    scale = 1 / math.sqrt(hd)
+    out = ops.prefill_attention(qkv, cu, max(lens), hq, hkv, hd, scale)
+    q, k, v = R.split_qkv(qkv, hq, hkv, hd)
+    ref = R.prefill_attention(q, k, v, cu, scale).reshape(len(qkv), -1)
+    close(out, ref, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("hq,hkv,hd,bs", [(32, 8, 128, 16), (12, 12, 64, 32), (8, 1, 128, 16)])
+@pytest.mark.parametrize("lens", [[1, 2, 3], [100, 31, 64, 17], [700, 1025]])
+def test_decode_attention_paged(gpu, hq, hkv, hd, bs, lens):
+    nblk = sum(-(-n // bs) for n in lens) + 8
+    qkv_all, pos, slots, kc, vc, tables = _paged_setup(gpu, lens, hq, hkv, hd, bs, nblk)
+    cs = R.rope_cos_sin(2048, hd, 10000.0, device=gpu)
+    ops.rope_and_cache(qkv_all, pos, slots, cs, kc, vc, hq, hkv, hd)
+    qkv = rnd(len(lens), (hq + 2 * hkv) * hd, dev=gpu)
+    ctx = torch.tensor(lens, device=gpu, dtype=torch.int32)
+    scale = 1 / math.sqrt(hd)
+    q = qkv[:, : hq * hd].reshape(len(lens), hq, hd)
+    ref = R.decode_attention(q, kc, vc, tables, ctx, scale).reshape(len(lens), -1)
+    for splits in (1, 2, 4):
+        out = ops.decode_attention(qkv, kc, vc, tables, ctx, max(lens), hq, hkv, hd, scale,
+                                   num_splits=splits)
+        close(out, ref, rtol=2e-2, atol=2e-2)
+
+
+def test_sampling_greedy_and_support(gpu):
+    torch.manual_seed(5)
+    B, V = 64, 128256
+    logits = torch.randn(B, V, device=gpu) * 3
+    z = torch.zeros(B, device=gpu)
+    ones = torch.ones(B, device=gpu)
+    seeds = torch.arange(B, device=gpu, dtype=torch.int64) * 7919
+    k1 = torch.ones(B, device=gpu, dtype=torch.int32)
+    tok = ops.sample(logits, z, k1, ones, seeds)
+    assert torch.equal(tok.long(), logits.argmax(-1))
+    temp = torch.full((B,), 0.8, device=gpu)
+    topk = torch.full((B,), 50, device=gpu, dtype=torch.int32)
+    topp = torch.full((B,), 0.95, device=gpu)
+    filt = R.topk_topp_filter(logits, temp, topk, topp)
+    for rep in range(4):
+        tok = ops.sample(logits, temp, topk, topp, seeds + rep)
+        sel = filt.gather(1, tok.long()[:, None]).squeeze(1)
+        assert torch.isfinite(sel).all(), "sampled a token outside the top-k/top-p support"
+
+
+def test_sampling_distribution_matches_reference(gpu):
+    """Small vocab, many rows with distinct seeds: empirical frequencies ~ HF probabilities."""
+    torch.manual_seed(6)
+    V, B = 64, 20000
+    row = torch.randn(V, device=gpu) * 2
+    logits = row[None].repeat(B, 1).contiguous()
+    temp = torch.full((B,), 0.8, device=gpu)
+    topk = torch.full((B,), 10, device=gpu, dtype=torch.int32)
+    topp = torch.full((B,), 0.9, device=gpu)
+    seeds = torch.arange(B, device=gpu, dtype=torch.int64) * 104729 + 11
+    tok = ops.sample(logits, temp, topk, topp, seeds)
+    p_ref = R.topk_topp_filter(logits[:1], temp[:1], topk[:1], topp[:1]).softmax(-1)[0]
+    freq = torch.bincount(tok.long(), minlength=V).float() / B
+    assert (freq[p_ref == 0] == 0).all()
+    assert (freq - p_ref).abs().max().item() < 0.02
+
+
+def test_sampling_pure_temperature_gumbel(gpu):
+    torch.manual_seed(7)
+    V, B = 32, 20000
+    row = torch.randn(V, device=gpu)
+    logits = row[None].repeat(B, 1).contiguous()
+    temp = torch.full((B,), 1.3, device=gpu)
+    tok = ops.sample(logits, temp, torch.zeros(B, device=gpu, dtype=torch.int32),
+                     torch.ones(B, device=gpu), torch.arange(B, device=gpu, dtype=torch.int64))
+    p = (row / 1.3).softmax(-1)
+    freq = torch.bincount(tok.long(), minlength=V).float() / B
+    assert (freq - p).abs().max().item() < 0.02
+
+
+@pytest.mark.parametrize("T,E,k", [(1, 8, 2), (37, 8, 2), (300, 4, 2)])
+def test_moe_route_and_mlp(gpu, T, E, k):
+    torch.manual_seed(8)
+    D, F = 256, 512
+    x = rnd(T, D, dev=gpu)
+    rl = rnd(T, E, dev=gpu)
+    w, ids = ops.moe_route(rl, k)
+    rw, rids = R.router_topk(rl, k)
+    assert torch.equal(ids.long().sort(-1).values, rids.long().sort(-1).values)
+    close(w.sort(-1).values, rw.sort(-1).values, rtol=1e-3, atol=1e-3)
+    wgu = rnd(E, 2 * F, D, dev=gpu, scale=0.05)
+    wd = rnd(E, D, F, dev=gpu, scale=0.05)
+    out = ops.moe_mlp(x, wgu, wd, rw, rids)
+    ref = R.moe_mlp(x, wgu, wd, rw, rids)
+    close(out, ref, rtol=3e-2, atol=3e-2)
+    # expert-parallel shard: only experts [2, 4) local
+    if E >= 4:
+        out2 = ops.moe_mlp(x, wgu[2:4].contiguous(), wd[2:4].contiguous(), rw, rids, 2)
+        ref2 = R.moe_mlp(x, wgu[2:4], wd[2:4], rw, rids, 2)
+        close(out2, ref2, rtol=3e-2, atol=3e-2)
