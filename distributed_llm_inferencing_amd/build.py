@@ -40,8 +40,10 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found (set HIPCC or install ROCm)")
 
 
-KERNEL_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffast-math",
-                "-fno-gpu-rdc", "-munsafe-fp-atomics", "-Wno-unused-result"]
+# NOTE: no -ffast-math: it implies no-infs, and the attention/sampling kernels rely on
+# -inf as the masked-score / running-max sentinel (poison under ninf -> NaNs).
+KERNEL_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-fno-gpu-rdc",
+                "-munsafe-fp-atomics", "-Wno-unused-result"]
 RUNTIME_FLAGS = ["-O2", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",
                  "-Wno-unused-result"]
 

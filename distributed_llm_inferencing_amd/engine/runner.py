@@ -92,8 +92,10 @@ class StageRunner:
 
         def put(name, arr, pad):
             o, _ = self._off[name]
-            a = np.asarray(arr).reshape(-1)
-            h[o:o + a.shape[0]] = a.view(np.int32) if a.dtype != np.int32 else a
+            a = np.ascontiguousarray(arr).reshape(-1)
+            if a.dtype != np.int32:
+                a = a.view(np.int32)
+            h[o:o + a.shape[0]] = a
             extra = (b - S) * (2 if name == "seeds" else 1)
             if extra > 0:
                 h[o + a.shape[0]:o + a.shape[0] + extra] = pad

@@ -1,0 +1,26 @@
+#!/bin/bash
+# One bounded GPU session: kernel tests -> engine tests -> short bench. Stops after any
+# fault-type exit (abort/segv/timeout); plain test failures (rc=1) continue.
+set -u
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+step() {  # step <name> <timeout_s> <cmd...>
+  local name=$1 t=$2; shift 2
+  echo "=== $name" ; date
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "rc[$name]=$rc"; tail -25 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ] && [ $rc -ne 5 ]; then echo "fatal rc=$rc, stopping"; exit $rc; fi
+  return 0
+}
+python -c "import torch;print(torch.cuda.get_device_name(0), torch.cuda.mem_get_info())"
+for s in "$@"; do
+  case $s in
+    kernels) step kernels 900 python -m pytest tests/test_kernels_gpu.py -q -m gpu -x ;;
+    engine)  step engine 900 python -m pytest tests/test_engine_gpu.py -q -m gpu -x ;;
+    gputests) step gputests 1200 python -m pytest tests -q -m gpu ;;
+    smoke)   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench)   step bench 900 python bench.py --steps 2 --warmup 1 ;;
+    bench_small) step bench_small 600 python bench.py --steps 2 --warmup 1 --batch 64 ;;
+  esac
+done
