@@ -21,6 +21,9 @@ for s in "$@"; do
     gputests) step gputests 1200 python -m pytest tests -q -m gpu ;;
     smoke)   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)   step bench 900 python bench.py --steps 2 --warmup 1 ;;
+    reference) step reference 900 python scripts/bench_reference.py --out gpurun_out/reference_strategy.json ;;
+    prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+          step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- python bench.py --steps 1 --warmup 1 ;;
     bench_small) step bench_small 600 python bench.py --steps 2 --warmup 1 --batch 64 ;;
   esac
 done
