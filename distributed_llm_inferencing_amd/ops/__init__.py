@@ -231,7 +231,7 @@ def decode_attention(qkv, k_cache, v_cache, block_tables, context_lens, max_cont
 def sample(logits, temperature, top_k, top_p, seeds, generator=None):
     """logits fp32 [B, V] -> int32 tokens [B]. temperature<=0 -> greedy."""
     if not _use_native(logits):
-        return R.sample(logits, temperature, top_k, top_p, generator=generator)
+        return R.sample(logits, temperature, top_k, top_p, generator=generator, seeds=seeds)
     B, V = logits.shape
     out = torch.empty(B, dtype=torch.int32, device=logits.device)
     _native_call("dli_sample", _p(out), _p(logits), logits.stride(0), B, V, _p(temperature),

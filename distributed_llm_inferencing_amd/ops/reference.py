@@ -235,9 +235,12 @@ def topk_topp_filter(logits: torch.Tensor, temperature: torch.Tensor, top_k: tor
 
 
 def sample(logits: torch.Tensor, temperature: torch.Tensor, top_k: torch.Tensor,
-           top_p: torch.Tensor, generator: Optional[torch.Generator] = None) -> torch.Tensor:
-    """Returns int32 token ids [B]. temperature<=0 -> greedy argmax."""
-    greedy = temperature <= 0
+           top_p: torch.Tensor, generator: Optional[torch.Generator] = None,
+           seeds: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Returns int32 token ids [B]. temperature<=0 (or top_k == 1) -> greedy argmax.
+    With per-row ``seeds`` each row draws from its own generator, so a request's tokens do
+    not depend on its batch neighbours (same contract as the HIP sampler)."""
+    greedy = (temperature <= 0) | (top_k == 1)
     out = torch.empty(logits.shape[0], dtype=torch.int32, device=logits.device)
     if greedy.any():
         out[greedy] = logits[greedy].float().argmax(-1).to(torch.int32)
@@ -245,7 +248,15 @@ def sample(logits: torch.Tensor, temperature: torch.Tensor, top_k: torch.Tensor,
     if ng.any():
         filt = topk_topp_filter(logits[ng], temperature[ng], top_k[ng], top_p[ng])
         probs = filt.softmax(-1)
-        out[ng] = torch.multinomial(probs, 1, generator=generator).squeeze(-1).to(torch.int32)
+        if seeds is None:
+            out[ng] = torch.multinomial(probs, 1, generator=generator).squeeze(-1).to(torch.int32)
+        else:
+            rows = ng.nonzero().squeeze(-1).tolist()
+            sd = seeds.tolist()
+            for j, r in enumerate(rows):
+                g = torch.Generator(device=probs.device)
+                g.manual_seed(int(sd[r]) & 0x7FFF_FFFF_FFFF_FFFF)
+                out[r] = torch.multinomial(probs[j], 1, generator=g).to(torch.int32)[0]
     return out
 
 

@@ -1,0 +1,168 @@
+"""Inter-stage transport for the layer-sharded pipeline.
+
+The reference has NO inter-shard data plane (its "sharded" path runs shard 0 alone,
+``worker/app.py:334-336``). Here activations move between pipeline stages by RCCL
+point-to-point over xGMI (``torch.distributed`` backend "nccl" == RCCL on ROCm), or gloo
+on CPU for tests.
+
+Ring protocol. Every rank exchanges once per tick with a grouped
+``batch_isend_irecv({send msg_k -> next, recv msg_{k+1} <- prev})`` (two phases: a fixed
+size control message, then the data tensor whose shape the control message announced).
+With M = N microbatches in flight, rank r's exchange at tick k pairs only with exchanges
+on the same anti-diagonal r + k (including the tail -> head token return edge), so the
+schedule is deadlock-free by construction regardless of how the backend progresses sends.
+
+Message = (ctrl int32[CTRL_WORDS], data tensor). ctrl = 16 int64 header words (as 32
+int32) + the packed StepMeta payload inline (up to CTRL_MAX words; larger payloads ride in
+phase 2 ahead of the data).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ..engine.batch import HEADER_LEN
+
+HDR32 = 2 * HEADER_LEN
+CTRL_MAX = int(os.environ.get("DLI_CTRL_MAX_WORDS", str(24 * 1024)))
+CTRL_WORDS = HDR32 + CTRL_MAX
+
+# header word indices (int64 units) beyond StepMeta's own first 8
+H_DATA_KIND, H_DATA_ROWS, H_DATA_COLS, H_INLINE, H_TICK = 8, 9, 10, 11, 12
+DATA_NONE, DATA_HIDDEN, DATA_TOKENS = 0, 1, 2
+
+
+@dataclass
+class Message:
+    header: np.ndarray                 # int64[HEADER_LEN]
+    payload: np.ndarray                # int32[n]
+    data: Optional[torch.Tensor]       # bf16 [rows, D] or int32 [S]
+
+
+class Transport:
+    rank: int
+    world: int
+
+    @property
+    def next(self) -> int:
+        return (self.rank + 1) % self.world
+
+    @property
+    def prev(self) -> int:
+        return (self.rank - 1) % self.world
+
+    def exchange(self, send: Optional[Message], recv: bool) -> Optional[Message]:
+        raise NotImplementedError
+
+    def barrier(self):
+        pass
+
+
+class TorchDistTransport(Transport):
+    """Ring transport over an initialised torch.distributed process group."""
+
+    def __init__(self, device: torch.device, hidden_size: int, dtype=torch.bfloat16,
+                 group=None):
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.group = group
+        self.device = device
+        self.hidden = hidden_size
+        self.dtype = dtype
+        self.comm_device = device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+        self._ctrl_send = torch.zeros(CTRL_WORDS, dtype=torch.int32, device=self.comm_device)
+        self._ctrl_recv = torch.zeros(CTRL_WORDS, dtype=torch.int32, device=self.comm_device)
+        self._ctrl_host = torch.zeros(CTRL_WORDS, dtype=torch.int32).pin_memory() \
+            if self.comm_device.type == "cuda" else None
+
+    def _peer(self, r):
+        return dist.get_global_rank(self.group, r) if self.group is not None else r
+
+    def _run(self, ops):
+        if not ops:
+            return
+        reqs = dist.batch_isend_irecv(ops)
+        for r in reqs:
+            r.wait()
+
+    def exchange(self, send: Optional[Message], recv: bool) -> Optional[Message]:
+        nxt, prv = self._peer(self.next), self._peer(self.prev)
+        # ---- phase 1: control words
+        ops = []
+        if send is not None:
+            hdr = send.header.copy()
+            inline = send.payload.shape[0] <= CTRL_MAX
+            hdr[H_INLINE] = 1 if inline else 0
+            words = np.zeros(CTRL_WORDS, dtype=np.int32)
+            words[:HDR32] = hdr.view(np.int32)
+            if inline:
+                words[HDR32:HDR32 + send.payload.shape[0]] = send.payload
+            self._ctrl_send.copy_(torch.from_numpy(words))
+            ops.append(dist.P2POp(dist.isend, self._ctrl_send, nxt, self.group))
+        if recv:
+            ops.append(dist.P2POp(dist.irecv, self._ctrl_recv, prv, self.group))
+        self._run(ops)
+        got = None
+        if recv:
+            if self._ctrl_host is not None:
+                self._ctrl_host.copy_(self._ctrl_recv)
+                words = self._ctrl_host.numpy().copy()
+            else:
+                words = self._ctrl_recv.numpy().copy()
+            rh = words[:HDR32].view(np.int64).copy()
+            got = rh
+        # ---- phase 2: overflow payload + data
+        ops = []
+        if send is not None:
+            if send.payload.shape[0] > CTRL_MAX:
+                pl = torch.from_numpy(send.payload).to(self.comm_device)
+                ops.append(dist.P2POp(dist.isend, pl, nxt, self.group))
+            if send.data is not None and send.data.numel() > 0:
+                d = send.data if send.data.device == self.comm_device else send.data.to(self.comm_device)
+                ops.append(dist.P2POp(dist.isend, d.contiguous(), nxt, self.group))
+        rpl = rdata = None
+        if recv:
+            n_pl = int(got[4])
+            if not got[H_INLINE]:
+                rpl = torch.empty(n_pl, dtype=torch.int32, device=self.comm_device)
+                ops.append(dist.P2POp(dist.irecv, rpl, prv, self.group))
+            kind, rows, cols = int(got[H_DATA_KIND]), int(got[H_DATA_ROWS]), int(got[H_DATA_COLS])
+            if kind == DATA_HIDDEN and rows > 0:
+                rdata = torch.empty(rows, cols, dtype=self.dtype, device=self.comm_device)
+            elif kind == DATA_TOKENS and rows > 0:
+                rdata = torch.empty(rows, dtype=torch.int32, device=self.comm_device)
+            if rdata is not None:
+                ops.append(dist.P2POp(dist.irecv, rdata, prv, self.group))
+        self._run(ops)
+        if not recv:
+            return None
+        n_pl = int(got[4])
+        payload = (words[HDR32:HDR32 + n_pl].copy() if got[H_INLINE]
+                   else rpl.cpu().numpy())
+        if rdata is not None and rdata.device != self.device:
+            rdata = rdata.to(self.device)
+        return Message(header=got, payload=payload, data=rdata)
+
+    def barrier(self):
+        dist.barrier(self.group)
+
+
+def init_distributed(backend: Optional[str] = None, device: Optional[torch.device] = None):
+    """Initialise torch.distributed from torchrun env vars (127.0.0.1 rendezvous)."""
+    if dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29511")
+    if backend is None:
+        backend = os.environ.get("DLI_DIST_BACKEND") or (
+            "nccl" if torch.cuda.is_available() else "gloo")
+    kw = {}
+    if backend == "nccl" and device is not None:
+        kw["device_id"] = device
+    dist.init_process_group(backend=backend, **kw)
+    return dist.get_rank(), dist.get_world_size()

@@ -58,3 +58,18 @@ def test_llama3_8b_smoke(gpu):
     outs = eng.generate(["The MI355X has 288 GB of HBM3E"], SamplingParams(max_length=40))
     assert len(outs[0].output_ids) == 40 - len(outs[0].prompt_ids)
     assert all(0 <= t < eng.cfg.vocab_size for t in outs[0].output_ids)
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_loopback_pipeline_on_gpu_matches_single_stage(gpu, n):
+    """All stages on cuda:0 (loopback transport): graphs on non-first stages, metadata
+    round-trips, microbatch schedule — token-identical to the single-stage engine."""
+    from distributed_llm_inferencing_amd.parallel.pipeline import LocalPipeline
+    prompts = [IDS[:5], IDS[:9], IDS[3:14], IDS[:2], IDS[1:4]]
+    for sp in (SamplingParams(max_length=30, do_sample=False, ignore_eos=True),
+               SamplingParams(max_length=30, seed=9, ignore_eos=True)):
+        ref = LLMEngine("llama-tiny", device="cuda", max_batch=8, max_model_len=128,
+                        num_blocks=64, seed=2).generate(prompts, sp)
+        pp = LocalPipeline("llama-tiny", n, device="cuda", max_batch=8, max_model_len=128,
+                           num_blocks=64, seed=2)
+        assert [o.all_ids for o in pp.generate(prompts, sp)] == [o.all_ids for o in ref]

@@ -1,0 +1,104 @@
+"""Pipeline parallelism: loopback (single process) and real multi-process rings over gloo
+must produce exactly the single-stage engine's tokens."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from distributed_llm_inferencing_amd.engine import SamplingParams
+from distributed_llm_inferencing_amd.engine.llm_engine import LLMEngine
+from distributed_llm_inferencing_amd.parallel.pipeline import LocalPipeline
+from distributed_llm_inferencing_amd.shard.planner import even_split, plan_stages
+from distributed_llm_inferencing_amd.models import get_config
+
+PROMPTS = [[5, 6, 7, 8], [9, 10, 11], [1, 2, 3, 4, 5, 6, 7], [100, 200], [7] * 9, [3, 4], [8] * 3]
+
+
+def _ref(model, sp):
+    eng = LLMEngine(model, device="cpu", dtype=torch.float32, max_batch=8, max_model_len=64,
+                    num_blocks=64)
+    return [o.all_ids for o in eng.generate(PROMPTS, sp)]
+
+
+@pytest.mark.parametrize("model", ["llama-tiny", "gpt2-tiny", "mixtral-tiny"])
+@pytest.mark.parametrize("n", [2, 4])
+def test_loopback_pipeline_matches_single_stage(model, n):
+    cfg = get_config(model)
+    if n > cfg.num_layers:
+        pytest.skip("more stages than layers")
+    for sp in (SamplingParams(max_length=20, do_sample=False, ignore_eos=True),
+               SamplingParams(max_length=20, seed=11, ignore_eos=True)):
+        pp = LocalPipeline(model, n, device="cpu", dtype=torch.float32, max_batch=8,
+                           max_model_len=64, num_blocks=64)
+        assert [o.all_ids for o in pp.generate(PROMPTS, sp)] == _ref(model, sp)
+
+
+def test_planner_rules():
+    assert even_split(32, 3) == [(0, 10), (10, 20), (20, 32)]          # reference rule
+    assert even_split(12, 4) == [(0, 3), (3, 6), (6, 9), (9, 12)]
+    cfg = get_config("llama3-70b")
+    for pol in ("even", "hbm", "balanced"):
+        plans = plan_stages(cfg, 8, pol)
+        assert plans[0].start_layer == 0 and plans[-1].end_layer == 80
+        assert all(a.end_layer == b.start_layer for a, b in zip(plans, plans[1:]))
+        assert max(p.weight_bytes for p in plans) < 288 * 2**30
+    bal = plan_stages(get_config("llama3-8b"), 8, "balanced")
+    # the LM-head stage carries fewer layers
+    assert bal[-1].end_layer - bal[-1].start_layer < bal[0].end_layer - bal[0].start_layer
+    plan_stages(cfg, 1, "even")                # 70B bf16 (141 GB) fits one 288 GB MI355X
+    with pytest.raises(ValueError):            # ...but not a 96 GB device
+        plan_stages(cfg, 1, "even", hbm_bytes=96 * 2**30)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, model, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    import torch.distributed as dist
+    from distributed_llm_inferencing_amd.parallel.pipeline import DistributedPipelineEngine
+    eng = DistributedPipelineEngine(model, "cpu", max_batch=8, max_model_len=64, num_blocks=64,
+                                    dtype=torch.float32)
+    if rank == 0:
+        res = []
+        for sp in (SamplingParams(max_length=20, do_sample=False, ignore_eos=True),
+                   SamplingParams(max_length=20, seed=11, ignore_eos=True)):
+            res.append([o.all_ids for o in eng.generate(PROMPTS, sp)])
+        # a second session on the same ring (sessions start/stop cleanly)
+        res.append([o.all_ids for o in eng.generate(PROMPTS[:2], SamplingParams(
+            max_length=12, do_sample=False, ignore_eos=True))])
+        eng.shutdown()
+        q.put(res)
+    else:
+        eng.serve()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_ring_matches_single_stage(world):
+    model = "llama-tiny"
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, model, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    greedy = SamplingParams(max_length=20, do_sample=False, ignore_eos=True)
+    assert res[0] == _ref(model, greedy)
+    assert res[1] == _ref(model, SamplingParams(max_length=20, seed=11, ignore_eos=True))
+    eng = LLMEngine(model, device="cpu", dtype=torch.float32, max_batch=8, max_model_len=64,
+                    num_blocks=64)
+    assert res[2] == [o.all_ids for o in eng.generate(PROMPTS[:2], SamplingParams(
+        max_length=12, do_sample=False, ignore_eos=True))]
