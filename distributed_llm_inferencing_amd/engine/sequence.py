@@ -44,7 +44,7 @@ class SeqState(enum.Enum):
     FINISHED = 2
 
 
-@dataclass
+@dataclass(eq=False)          # identity semantics: list.remove / `in` must not compare fields
 class Sequence:
     seq_id: int
     request_id: str
