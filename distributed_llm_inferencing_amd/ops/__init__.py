@@ -100,8 +100,20 @@ def _gemm_native(x, w, epi: str, bias=None, out=None, plan: Optional[G.GemmPlan]
     if out is None:
         dt = torch.float32 if epi == "f32" else x.dtype
         out = torch.empty(M, out_n, dtype=dt, device=x.device)
-    if plan.backend == "hipblaslt" and epi == "none" and group_off is None:
-        torch.matmul(x, w.t(), out=out)
+    if plan.backend == "hipblaslt" and group_off is None:
+        # plain library GEMM (hipBLASLt) + our epilogue kernel as a separate pass
+        if epi == "none":
+            torch.matmul(x, w.t(), out=out)
+            return out
+        y = torch.matmul(x, w.t())
+        if epi == "silu_mul":
+            _native_call("dli_silu_mul", _p(out), _p(y), M, out_n, _st())
+        elif epi in ("bias", "bias_gelu"):
+            _native_call("dli_bias_act", _p(y), _p(bias), M, Nn, 1 if epi == "bias_gelu" else 0,
+                         _st())
+            out.copy_(y)
+        else:  # f32
+            out.copy_(y)
         return out
     splits = plan.splits if group_off is None else 1
     ws = None

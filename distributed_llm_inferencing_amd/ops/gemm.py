@@ -49,19 +49,28 @@ def workspace(device: torch.device, nbytes: int) -> torch.Tensor:
         return ws
 
 
+LARGE_M = int(os.environ.get("DLI_GEMM_LARGE_M", "1024"))
+
+
 def _heuristic(M: int, N: int, K: int, epi: str) -> GemmPlan:
-    if M <= 64:
+    """Fitted to profiles/r1_gemm/gemm_bench.json (MI355X, random bf16 operands):
+    skinny decode GEMMs (M <= 512) run on our kernel, 1.1-1.9x faster than hipBLASLt there;
+    fat prefill GEMMs (M >= LARGE_M) on hipBLASLt, which is 1.6-1.9x faster than our 128^2
+    2-stage structure at M >= 2048 (fused epilogues then run as a separate pass)."""
+    if M >= LARGE_M and os.environ.get("DLI_GEMM_NO_BLAS", "0") != "1":
+        return GemmPlan("hipblaslt", 2, 1)
+    if M <= 128:
         tile = 0 if N <= 8192 else 1
     elif M <= 256:
-        tile = 2
+        tile = 1 if N <= 8192 else 2
     else:
         tile = 2
     bm, bn = TILES[tile]
     tiles = -(-M // bm) * -(-N // bn)
     splits = 1
-    # split K until the grid covers ~the CU count, keeping >= 512 K per slice
-    while (tiles * splits * 2 <= NUM_CUS and K % (64 * splits * 2) == 0
-           and K // (splits * 2) >= 512):
+    # split K until the grid is ~2-3 waves over the 256 CUs, keeping >= 512 K per slice
+    while (tiles * splits * 2 <= 3 * NUM_CUS and K % (64 * splits * 2) == 0
+           and K // (splits * 2) >= 512 and splits < 8):
         splits *= 2
     return GemmPlan("dli", tile, splits)
 

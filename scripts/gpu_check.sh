@@ -26,6 +26,7 @@ for s in "$@"; do
           step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- python bench.py --steps 1 --warmup 1 ;;
     pp2) step pp2 900 env DLI_DIST_BACKEND=gloo DLI_SAME_DEVICE=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 1 --warmup 1 --batch 64 ;;
     pp4) step pp4 900 env DLI_DIST_BACKEND=gloo DLI_SAME_DEVICE=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 4 --steps 1 --warmup 1 --batch 32 ;;
+    gemm) step gemm 1100 python scripts/bench_gemm.py ;;
     bench_small) step bench_small 600 python bench.py --steps 2 --warmup 1 --batch 64 ;;
   esac
 done
