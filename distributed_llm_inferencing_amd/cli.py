@@ -1,0 +1,131 @@
+"""Command-line entry: ``python -m distributed_llm_inferencing_amd.cli <command>``.
+
+Replaces the reference's ``manage.py`` (runserver / shard_model) and its
+docker-compose topology (X6: master + 2 worker containers + redis) with a single-node
+launcher for an 8-GPU MI355X box.
+
+    serve-master    [--port 8000]                       Flask master (dashboard + API)
+    serve-worker    [--port 5000] [--gpu i]             one worker bound to one GPU (or CPU)
+    serve-node      --gpus N [--base-port 5000] [--master URL]
+                    one worker process per GPU (HIP_VISIBLE_DEVICES=i, port base+i), each
+                    registered with the master as a node
+    serve-pipeline  --model M --gpus N [--port 5000]    N-rank layer-sharded pipeline; rank 0
+                    serves the worker API and reports the stages as loaded shards
+    shard-model     --model_name M --num_shards N [--output_dir D] [--policy even|hbm|balanced]
+    bench           ... (bench.py)
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+import time
+
+
+def _serve_node(argv):
+    import argparse
+
+    import requests
+    ap = argparse.ArgumentParser("dli serve-node")
+    ap.add_argument("--gpus", type=int, default=8)
+    ap.add_argument("--base-port", type=int, default=5000)
+    ap.add_argument("--master", default=None, help="e.g. http://127.0.0.1:8000")
+    ap.add_argument("--preload", default="")
+    a = ap.parse_args(argv)
+    procs = []
+    for i in range(a.gpus):
+        env = dict(os.environ, HIP_VISIBLE_DEVICES=str(i), USE_GPU="1",
+                   HSA_ENABLE_IPC_MODE_LEGACY="0")
+        cmd = [sys.executable, "-m", "distributed_llm_inferencing_amd.worker.server",
+               "--port", str(a.base_port + i), "--gpu", "0", "--preload", a.preload]
+        procs.append(subprocess.Popen(cmd, env=env))
+    if a.master:
+        for i in range(a.gpus):
+            port = a.base_port + i
+            for _ in range(120):
+                try:
+                    r = requests.post(f"{a.master}/api/nodes/add/",
+                                      data={"hostname": f"gpu{i}", "ip_address": "127.0.0.1",
+                                            "port": port}, timeout=10)
+                    if r.status_code == 200:
+                        break
+                except requests.RequestException:
+                    pass
+                time.sleep(1)
+    try:
+        for p in procs:
+            p.wait()
+    except KeyboardInterrupt:
+        for p in procs:
+            p.terminate()
+
+
+def _serve_pipeline(argv):
+    """Run under torchrun: rank 0 = HTTP worker + pipeline head; others = stage loops."""
+    import argparse
+    import logging
+    ap = argparse.ArgumentParser("dli serve-pipeline")
+    ap.add_argument("--model", required=True)
+    ap.add_argument("--port", type=int, default=5000)
+    ap.add_argument("--max-batch", type=int, default=256)
+    ap.add_argument("--max-model-len", type=int, default=2048)
+    ap.add_argument("--policy", default="balanced")
+    a = ap.parse_args(argv)
+    import torch
+    from .config import get_settings
+    from .parallel.pipeline import DistributedPipelineEngine
+    from .worker.server import WorkerState, create_worker_app
+    from .worker.service import PipelineService
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = f"cuda:{local}" if torch.cuda.is_available() else "cpu"
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)
+    eng = DistributedPipelineEngine(a.model, dev, max_batch=a.max_batch,
+                                    max_model_len=a.max_model_len, policy=a.policy)
+    eng.warmup()
+    if eng.rank != 0:
+        eng.serve()
+        return
+    logging.basicConfig(level=logging.INFO)
+    s = get_settings()
+    s.use_gpu = torch.cuda.is_available()
+    st = WorkerState(s, dev)
+    st.pipeline_model = a.model
+    st.pipeline_service = PipelineService(eng, name=a.model)
+    st.tokenizers[a.model] = eng.head.tok
+    st.pipeline_shards = [
+        {"model_name": a.model, "shard_id": p.shard_id, "path": f"rank{p.shard_id}",
+         "metadata": p.to_metadata(a.model, len(eng.plans), eng.cfg.num_layers)}
+        for p in eng.plans]
+    app = create_worker_app(s, state=st)
+    app.run(host="0.0.0.0", port=a.port, threaded=True)
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    if not argv or argv[0] in ("-h", "--help"):
+        print(__doc__)
+        return 0
+    cmd, rest = argv[0], argv[1:]
+    if cmd == "serve-master":
+        from .control.master import main as m
+        return m(rest)
+    if cmd == "serve-worker":
+        from .worker.server import main as m
+        return m(rest)
+    if cmd == "serve-node":
+        return _serve_node(rest)
+    if cmd == "serve-pipeline":
+        return _serve_pipeline(rest)
+    if cmd == "shard-model":
+        from .shard.writer import main as m
+        return m(rest)
+    if cmd == "bench":
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        return subprocess.call([sys.executable, os.path.join(root, "bench.py"), *rest])
+    print(f"unknown command {cmd}\n{__doc__}")
+    return 2
+
+
+if __name__ == "__main__":
+    sys.exit(main())

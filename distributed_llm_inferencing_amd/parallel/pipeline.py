@@ -266,10 +266,10 @@ class LocalPipeline:
     def __init__(self, model, num_stages: int, device="cpu", max_batch: int = 64,
                  max_model_len: int = 512, block_size: int = 16, num_blocks: int = 256,
                  policy: str = "even", seed: int = 0, use_graphs=None, params=None,
-                 dtype=torch.bfloat16):
+                 dtype=torch.bfloat16, plans: Optional[List[StagePlan]] = None):
         self.cfg = get_config(model) if isinstance(model, str) else model
         self.N = num_stages
-        self.plans = plan_stages(self.cfg, num_stages, policy)
+        self.plans = plans or plan_stages(self.cfg, num_stages, policy)
         tw = -(-max_model_len // block_size)
         self.stages = []
         for p in self.plans:

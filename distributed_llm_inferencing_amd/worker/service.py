@@ -1,0 +1,156 @@
+"""EngineService: one engine per loaded model, driven by a background thread.
+
+The reference worker runs one sync gunicorn worker (``worker/Dockerfile:45``): every
+``/inference`` call runs its own ``generate`` at batch 1 while others wait. Here HTTP handler
+threads only enqueue; a single engine thread admits everything queued into the
+continuous-batching scheduler and steps it, so concurrent requests share every decode step
+(and every GEMM weight read).
+"""
+from __future__ import annotations
+
+import queue
+import threading
+import time
+from concurrent.futures import Future
+from typing import Any, Optional
+
+from ..engine.sequence import SamplingParams
+
+
+class EngineService:
+    def __init__(self, engine, name: str = "engine"):
+        self.engine = engine
+        self.name = name
+        self._inbox: "queue.Queue[tuple]" = queue.Queue()
+        self._futures = {}
+        self._stop = threading.Event()
+        self._wake = threading.Event()
+        self._ids = 0
+        self._lock = threading.Lock()
+        self.error: Optional[BaseException] = None
+        self._t = threading.Thread(target=self._run, name=f"dli-engine-{name}", daemon=True)
+        self._t.start()
+
+    def submit(self, prompt, params: Optional[SamplingParams] = None) -> Future:
+        fut: Future = Future()
+        with self._lock:
+            self._ids += 1
+            rid = f"{self.name}-{self._ids}"
+        self._inbox.put((rid, prompt, params, fut))
+        self._wake.set()
+        return fut
+
+    def generate(self, prompt, params: Optional[SamplingParams] = None,
+                 timeout: Optional[float] = None):
+        return self.submit(prompt, params).result(timeout=timeout)
+
+    def _admit(self):
+        while True:
+            try:
+                rid, prompt, params, fut = self._inbox.get_nowait()
+            except queue.Empty:
+                return
+            try:
+                self.engine.add_request(prompt, params, request_id=rid)
+                self._futures[rid] = fut
+            except Exception as e:  # noqa: BLE001
+                fut.set_exception(e)
+
+    def _run(self):
+        while not self._stop.is_set():
+            self._admit()
+            if not self.engine.has_work():
+                self._wake.wait(0.05)
+                self._wake.clear()
+                continue
+            try:
+                outs = self.engine.step()
+            except BaseException as e:  # noqa: BLE001 — fail every pending request loudly
+                self.error = e
+                for f in self._futures.values():
+                    if not f.done():
+                        f.set_exception(e)
+                self._futures.clear()
+                time.sleep(0.1)
+                continue
+            for o in outs:
+                f = self._futures.pop(o.request_id, None)
+                if f is not None and not f.done():
+                    f.set_result(o)
+
+    def stats(self) -> dict:
+        s = self.engine.stats.snapshot() if hasattr(self.engine, "stats") else {}
+        s["queued"] = self._inbox.qsize()
+        s["in_flight"] = len(self._futures)
+        return s
+
+    def close(self):
+        self._stop.set()
+        self._wake.set()
+        self._t.join(5)
+
+
+class PipelineService:
+    """Same interface, backed by the rank-0 head of a DistributedPipelineEngine: requests
+    are batched into ring sessions."""
+
+    def __init__(self, pipe_engine, name: str = "pipeline"):
+        self.engine = pipe_engine
+        self.name = name
+        self._inbox: "queue.Queue[tuple]" = queue.Queue()
+        self._stop = threading.Event()
+        self._ids = 0
+        self._lock = threading.Lock()
+        self._t = threading.Thread(target=self._run, name=f"dli-pipe-{name}", daemon=True)
+        self._t.start()
+
+    def submit(self, prompt, params=None) -> Future:
+        fut: Future = Future()
+        with self._lock:
+            self._ids += 1
+            rid = f"{self.name}-{self._ids}"
+        self._inbox.put((rid, prompt, params, fut))
+        return fut
+
+    def generate(self, prompt, params=None, timeout=None):
+        return self.submit(prompt, params).result(timeout=timeout)
+
+    def _run(self):
+        head = self.engine.head
+        while not self._stop.is_set():
+            try:
+                first = self._inbox.get(timeout=0.05)
+            except queue.Empty:
+                continue
+            batch = [first]
+            while True:
+                try:
+                    batch.append(self._inbox.get_nowait())
+                except queue.Empty:
+                    break
+            futs = {}
+            for rid, prompt, params, fut in batch:
+                try:
+                    self.engine.add_request(prompt, params, request_id=rid)
+                    futs[rid] = fut
+                except Exception as e:  # noqa: BLE001
+                    fut.set_exception(e)
+            try:
+                outs = head.run_session()
+            except BaseException as e:  # noqa: BLE001
+                for f in futs.values():
+                    f.set_exception(e)
+                continue
+            for o in outs:
+                f = futs.pop(o.request_id, None)
+                if f is not None:
+                    f.set_result(o)
+
+    def stats(self) -> dict:
+        s = self.engine.head.stats.snapshot()
+        s["queued"] = self._inbox.qsize()
+        return s
+
+    def close(self):
+        self._stop.set()
+        self._t.join(5)

@@ -1,0 +1,271 @@
+"""T1/T2 control-plane tests: sqlite store, queues, master API contract (Appendix A),
+worker API contract (Appendix B), and master -> worker dispatch over real HTTP on localhost
+with the CPU engine (config 1: gpt2 on a CPU worker)."""
+import threading
+import time
+
+import pytest
+import requests
+from werkzeug.serving import make_server
+
+from distributed_llm_inferencing_amd.config import Settings
+from distributed_llm_inferencing_amd.control.master import create_master_app
+from distributed_llm_inferencing_amd.control.queue import InProcQueue, SqliteQueue, make_queue
+from distributed_llm_inferencing_amd.control.store import NotFound, Store
+from distributed_llm_inferencing_amd.worker.server import create_worker_app
+
+SMALL = dict(max_batch=8, max_model_len=128, num_blocks=64)
+
+
+class Server:
+    def __init__(self, app):
+        self.srv = make_server("127.0.0.1", 0, app, threaded=True)
+        self.port = self.srv.server_port
+        self.t = threading.Thread(target=self.srv.serve_forever, daemon=True)
+        self.t.start()
+
+    @property
+    def url(self):
+        return f"http://127.0.0.1:{self.port}"
+
+    def close(self):
+        self.srv.shutdown()
+
+
+def settings(tmp_path, **kw):
+    s = Settings()
+    s.master_db = str(tmp_path / "db.sqlite3")
+    s.model_cache_dir = str(tmp_path / "cache")
+    for k, v in kw.items():
+        setattr(s, k, v)
+    return s
+
+
+# ----------------------------------------------------------------------------- store / queue
+def test_store_state_machine(tmp_path):
+    st = Store(str(tmp_path / "s.db"))
+    n = st.add_node("w1", "127.0.0.1", 5000)
+    assert st.get_node(n)["url"] == "http://127.0.0.1:5000"
+    st.add_shard(n, "gpt2", 0, True)
+    st.add_shard(n, "gpt2", 0, True)                 # unique (model, shard) -> upsert
+    assert len(st.shards("gpt2")) == 1
+    rid = st.create_request("gpt2", "hi")
+    assert st.get_request(rid)["status"] == "pending"
+    st.mark_processing(rid, n)
+    assert st.recover() == [rid] and st.get_request(rid)["status"] == "pending"
+    st.mark_processing(rid, n)
+    st.mark_completed(rid, "out", 0.5)
+    r = st.get_request(rid)
+    assert r["status"] == "completed" and r["result"] == "out" and r["completed_at"]
+    st.delete_node(n)                                # cascade removes shards
+    assert st.shards() == []
+    with pytest.raises(NotFound):
+        st.get_node(n)
+
+
+def test_queues(tmp_path):
+    q = InProcQueue()
+    q.put(3)
+    assert q.get(0.1) == 3 and q.get(0.01) is None
+    st = Store(str(tmp_path / "q.db"))
+    sq = SqliteQueue(st)
+    a, b = st.create_request("m", "p"), st.create_request("m", "p")
+    assert sq.get(0.5) == a and sq.get(0.5) == b and sq.get(0.05) is None
+    assert make_queue("redis", st, Settings()).name in ("redis", "inproc")
+
+
+# ----------------------------------------------------------------------------- worker API
+@pytest.fixture()
+def worker(tmp_path):
+    app = create_worker_app(settings(tmp_path), device="cpu", engine_kwargs=SMALL)
+    return app.test_client()
+
+
+def test_worker_health_and_load(worker):
+    h = worker.get("/health").get_json()
+    assert h["status"] == "healthy"
+    assert set(h["resources"]) >= {"cpu", "memory", "gpu", "gpu_available", "device"}
+    assert h["resources"]["device"] == "cpu"
+    assert worker.post("/load_model", json={}).status_code == 400
+    r = worker.post("/load_model", json={"model_name": "gpt2-tiny"}).get_json()
+    assert r["status"] == "success" and "loaded successfully on cpu" in r["message"]
+    r = worker.post("/load_model", json={"model_name": "gpt2-tiny"}).get_json()
+    assert "already loaded" in r["message"]
+    assert worker.get("/health").get_json()["loaded_models"] == ["gpt2-tiny"]
+    assert worker.post("/load_model", json={"model_name": "nope"}).status_code == 500
+    assert worker.post("/unload_model", json={"model_name": "gpt2-tiny"}).status_code == 200
+    assert worker.get("/health").get_json()["loaded_models"] == []
+
+
+def test_worker_inference_contract(worker):
+    assert worker.post("/inference", json={"model_name": "gpt2-tiny"}).status_code == 400
+    r = worker.post("/inference", json={"model_name": "llama-tiny", "prompt": "Hello",
+                                        "max_length": 20})
+    d = r.get_json()
+    assert r.status_code == 200 and d["status"] == "success"
+    assert d["result"].startswith("Hello") and d["execution_time"] > 0
+    assert d["output_tokens"] == 20 - 5
+
+
+def test_worker_concurrent_requests_are_batched(worker):
+    worker.post("/load_model", json={"model_name": "llama-tiny"})
+    out = [None] * 6
+
+    def call(i):
+        out[i] = worker.post("/inference", json={"model_name": "llama-tiny",
+                                                 "prompt": f"req {i}", "max_length": 24})
+    ts = [threading.Thread(target=call, args=(i,)) for i in range(6)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    assert all(r.status_code == 200 for r in out)
+    m = worker.get("/metrics").get_json()["engines"]["llama-tiny"]
+    assert m["finished_requests"] == 6
+    assert m["decode_steps"] < 6 * 17            # shared decode steps
+
+
+def test_worker_timeout_408(worker):
+    r = worker.post("/inference", json={"model_name": "llama-tiny", "prompt": "x" * 10,
+                                        "max_length": 120, "timeout": 0})
+    assert r.status_code == 408
+
+
+def test_worker_auth(tmp_path):
+    app = create_worker_app(settings(tmp_path, auth_enabled=True, auth_key="k"), device="cpu",
+                            engine_kwargs=SMALL).test_client()
+    assert app.get("/health").status_code == 401
+    assert app.get("/health", headers={"Authorization": "Bearer k"}).status_code == 200
+
+
+def test_worker_ssh_setup_contract(worker):
+    assert worker.post("/ssh_setup", json={"host": "h"}).status_code == 400
+    r = worker.post("/ssh_setup", json={"host": "127.0.0.1", "port": 1, "username": "u",
+                                        "password": "p"})
+    assert r.status_code == 500 and "SSH connection failed" in r.get_json()["message"]
+
+
+def test_shard_export_load_and_sharded_inference(tmp_path, worker):
+    from distributed_llm_inferencing_amd.shard.writer import export_shards
+    paths = export_shards("llama-tiny", 2, str(tmp_path / "shards"), log=lambda *a: None)
+    meta = (paths[1] / "metadata.json").read_text()
+    assert '"end_layer": 3' in meta and '"total_layers": 4' in meta
+    # shard_id 0 accepted (the reference rejected it)
+    r = worker.post("/load_shard", json={"model_name": "llama-tiny", "shard_id": 0,
+                                         "shard_path": str(paths[0])})
+    assert r.status_code == 200, r.get_json()
+    # a partial shard set must be refused, not run as a whole model
+    r = worker.post("/inference", json={"model_name": "llama-tiny", "prompt": "abc",
+                                        "shard_ids": [0]})
+    assert r.status_code == 500 and "cannot run a partial model" in r.get_json()["message"]
+    worker.post("/load_shard", json={"model_name": "llama-tiny", "shard_id": 1,
+                                     "shard_path": str(paths[1])})
+    h = worker.get("/health").get_json()
+    assert sorted(s["shard_id"] for s in h["loaded_shards"]) == [0, 1]
+    body = {"model_name": "llama-tiny", "prompt": "abc", "max_length": 16, "temperature": 0}
+    sharded = worker.post("/inference", json={**body, "shard_ids": [0, 1]}).get_json()
+    full = worker.post("/inference", json=body).get_json()
+    assert sharded["status"] == "success"
+    assert sharded["result"] == full["result"]       # same weights: exported == random init
+
+
+# ----------------------------------------------------------------------------- master API
+@pytest.fixture()
+def master(tmp_path):
+    app = create_master_app(settings(tmp_path), start_background=True, dispatch_workers=2,
+                            health_interval=0.5)
+    yield app
+    app.extensions["dli"].shutdown()
+
+
+def test_master_pages_and_validation(master):
+    c = master.test_client()
+    for p in ("/", "/nodes/", "/inference/", "/admin/"):
+        assert c.get(p).status_code == 200
+    r = c.post("/api/nodes/add/", data={"hostname": "x"})
+    assert r.status_code == 400 and set(r.get_json()["errors"]) == {"ip_address", "port"}
+    r = c.post("/api/nodes/add/", data={"hostname": "x", "ip_address": "127.0.0.1", "port": 1})
+    assert r.status_code == 400 and "Could not connect to node" in r.get_json()["message"]
+    r = c.post("/api/inference/submit/", data={"model_name": "gpt2"})
+    assert r.status_code == 400 and "prompt" in r.get_json()["errors"]
+    assert c.get("/api/inference/status/999/").status_code == 500
+    assert c.post("/api/nodes/remove/999/").status_code == 500
+    assert c.get("/api/inference/recent/").get_json() == {"requests": []}
+
+
+def test_end_to_end_dispatch_over_http(tmp_path, master):
+    """submit -> queue -> dispatcher -> worker /load_model + /inference -> completed."""
+    w = Server(create_worker_app(settings(tmp_path), device="cpu", engine_kwargs=SMALL))
+    try:
+        c = master.test_client()
+        r = c.post("/api/nodes/add/", data={"hostname": "cpu0", "ip_address": "127.0.0.1",
+                                            "port": w.port}).get_json()
+        assert r["status"] == "success"
+        nodes = c.get("/api/nodes/status/").get_json()["nodes"]
+        assert nodes[0]["is_active"] and nodes[0]["resources"]["device"] == "cpu"
+        rid = c.post("/api/inference/submit/", data={"model_name": "gpt2-tiny",
+                                                     "prompt": "Hello"}).get_json()["request_id"]
+        for _ in range(300):
+            st = c.get(f"/api/inference/status/{rid}/").get_json()
+            if st["status"] in ("completed", "failed"):
+                break
+            time.sleep(0.1)
+        assert st["status"] == "completed", st
+        assert st["result"].startswith("Hello") and st["completed_at"]
+        recent = c.get("/api/inference/recent/").get_json()["requests"]
+        assert recent[0]["id"] == rid
+        m = c.get("/metrics").get_json()
+        assert m["requests"]["completed"] == 1
+    finally:
+        w.close()
+
+
+def test_failover_and_no_nodes(tmp_path, master):
+    c = master.test_client()
+    rid = c.post("/api/inference/submit/", data={"model_name": "gpt2-tiny",
+                                                 "prompt": "x"}).get_json()["request_id"]
+    for _ in range(100):
+        st = c.get(f"/api/inference/status/{rid}/").get_json()
+        if st["status"] == "failed":
+            break
+        time.sleep(0.05)
+    assert st["error"] == "No active worker nodes available"
+    # a dead node plus a live one: the request must land on the live one
+    w = Server(create_worker_app(settings(tmp_path), device="cpu", engine_kwargs=SMALL))
+    try:
+        store = master.extensions["dli"].store
+        dead = store.add_node("dead", "127.0.0.1", 1, True)
+        c.post("/api/nodes/add/", data={"hostname": "live", "ip_address": "127.0.0.1",
+                                        "port": w.port})
+        rids = [c.post("/api/inference/submit/", data={"model_name": "gpt2-tiny",
+                                                       "prompt": f"p{i}"}).get_json()["request_id"]
+                for i in range(3)]
+        for rid in rids:
+            for _ in range(300):
+                st = c.get(f"/api/inference/status/{rid}/").get_json()
+                if st["status"] in ("completed", "failed"):
+                    break
+                time.sleep(0.1)
+            assert st["status"] == "completed", st
+        # the health monitor eventually marks the dead node inactive
+        for _ in range(50):
+            if not store.get_node(dead)["is_active"]:
+                break
+            time.sleep(0.1)
+        assert not store.get_node(dead)["is_active"]
+    finally:
+        w.close()
+
+
+def test_remove_node_unloads(tmp_path, master):
+    w = Server(create_worker_app(settings(tmp_path), device="cpu", engine_kwargs=SMALL))
+    try:
+        c = master.test_client()
+        nid = c.post("/api/nodes/add/", data={"hostname": "w", "ip_address": "127.0.0.1",
+                                              "port": w.port}).get_json()["node_id"]
+        requests.post(f"{w.url}/load_model", json={"model_name": "gpt2-tiny"}, timeout=60)
+        c.post("/api/shards/register/", data={"node_id": nid, "model_name": "gpt2-tiny",
+                                              "shard_id": 0})
+        r = c.post(f"/api/nodes/remove/{nid}/").get_json()
+        assert r["status"] == "success" and r["warnings"] is None
+        assert requests.get(f"{w.url}/health", timeout=10).json()["loaded_models"] == []
+    finally:
+        w.close()
