@@ -89,6 +89,13 @@ def run_single(args):
 
 
 def run_pipeline(args, world, rank):
+    from distributed_llm_inferencing_amd.models import get_config
+    mode = args.mode
+    if mode == "auto":
+        mode = "ep" if get_config(args.model).is_moe else "pp"
+    if mode == "ep":      # Mixtral: DP attention + experts sharded over ranks (all-to-all)
+        from distributed_llm_inferencing_amd.parallel.expert import bench_expert_parallel
+        return bench_expert_parallel(args, world, rank, make_prompts)
     from distributed_llm_inferencing_amd.parallel.pipeline import bench_pipeline
     return bench_pipeline(args, world, rank, make_prompts)
 
@@ -103,6 +110,8 @@ def main():
     ap.add_argument("--prompt-len", type=int, default=32)
     ap.add_argument("--max-length", type=int, default=100)
     ap.add_argument("--max-model-len", type=int, default=512)
+    ap.add_argument("--mode", default="auto", choices=["auto", "pp", "ep"],
+                    help="N>1: pp = layer-sharded pipeline (dense), ep = expert parallel (MoE)")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

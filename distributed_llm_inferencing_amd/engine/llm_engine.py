@@ -66,13 +66,16 @@ class LLMEngine:
                  block_size: int = 16, num_blocks: Optional[int] = None,
                  kv_fraction: float = 0.85, seed: int = 0, use_graphs: Optional[bool] = None,
                  params: Optional[Dict[str, torch.Tensor]] = None, tokenizer_path=None,
-                 max_prefill_tokens: int = 16384, num_layers: Optional[int] = None):
+                 max_prefill_tokens: int = 16384, num_layers: Optional[int] = None,
+                 lm: Optional[TransformerLM] = None):
         self.cfg = get_config(model, num_layers) if isinstance(model, str) else model
         self.device = torch.device(device)
         if self.device.type == "cuda" and self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
         cfg = self.cfg
-        if params is None:
+        if lm is not None:
+            self.model = lm
+        elif params is None:
             self.model = TransformerLM.random(cfg, device=self.device, dtype=dtype, seed=seed)
         else:
             self.model = TransformerLM(cfg, {k: v.to(self.device) for k, v in params.items()},

@@ -102,3 +102,43 @@ def test_gloo_ring_matches_single_stage(world):
                     num_blocks=64)
     assert res[2] == [o.all_ids for o in eng.generate(PROMPTS[:2], SamplingParams(
         max_length=12, do_sample=False, ignore_eos=True))]
+
+
+def _ep_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    import torch.distributed as dist
+    from distributed_llm_inferencing_amd.parallel.expert import ExpertParallelEngine
+    eng = ExpertParallelEngine("mixtral-tiny", "cpu", max_batch=8, max_model_len=64,
+                               num_blocks=64, dtype=torch.float32)
+    # ranks serve DIFFERENT requests (DP attention) and unequal amounts (idle-step path)
+    mine = PROMPTS[rank::world] if rank == 0 else PROMPTS[rank::world][:1]
+    sp = SamplingParams(max_length=18, do_sample=False, ignore_eos=True)
+    out = [o.all_ids for o in eng.generate(mine, sp)]
+    q.put((rank, mine, out, eng.moe.exchanges))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_expert_parallel_gloo_matches_dense():
+    """DP attention + EP experts over 2 gloo ranks == single process with all experts."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ep_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    eng = LLMEngine("mixtral-tiny", device="cpu", dtype=torch.float32, max_batch=8,
+                    max_model_len=64, num_blocks=64)
+    sp = SamplingParams(max_length=18, do_sample=False, ignore_eos=True)
+    for rank, mine, out, exch in res:
+        assert out == [o.all_ids for o in eng.generate(mine, sp)], rank
+        assert exch > 0
+    # lockstep: both ranks ran the same number of MoE exchanges
+    assert res[0][3] == res[1][3]
