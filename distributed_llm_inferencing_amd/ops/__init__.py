@@ -95,7 +95,13 @@ def _gemm_native(x, w, epi: str, bias=None, out=None, plan: Optional[G.GemmPlan]
     M, K = x.shape
     Nn = w.shape[-2]
     if plan is None:
-        plan = G.plan(M if group_off is None else rows_per_group, Nn, K, epi)
+        if group_off is None:
+            plan = G.plan(M, Nn, K, epi)
+        else:
+            # grouped (MoE): size the tile to the EXPECTED rows per expert, not the bound
+            exp_rows = max(1, (2 * rows_per_group) // max(1, groups))
+            p = G._heuristic(min(exp_rows, 512), Nn, K, epi)
+            plan = G.GemmPlan("dli", p.tile, 1)
     out_n = Nn // 2 if epi == "silu_mul" else Nn
     if out is None:
         dt = torch.float32 if epi == "f32" else x.dtype
