@@ -61,20 +61,43 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
   for (int i = 0; i < DB; ++i) o_acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   for (int t0 = s_begin + wid * DEC_TILE; t0 < s_end; t0 += DEC_WAVES * DEC_TILE) {
-    f32x4 s_acc[2];
+    // ---- issue every global load of the tile up front (K fragments AND V fragments) so the
+    // tile pays one HBM round trip instead of two (V used to wait for the softmax)
+    uint4 kreg[2][KK];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       int tok = t0 + 16 * s + col;
       tok = tok < s_end ? tok : s_end - 1;                     // clamp: always-written rows
       const int blk = bt[tok / block_size], off = tok % block_size;
       const u16* kp = k_cache + ((long)blk * hkv + kvh) * kv_head_stride + (long)off * HD;
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk)
+        kreg[s][kk] = *reinterpret_cast<const uint4*>(kp + kk * 32 + grp * 8);
+    }
+    // V rows: tokens t0 + pi(grp, j), pi(grp, j) = 16(j>>2) + 4grp + (j&3), from V^T [d][tok]
+    const int tokA = min(t0 + 4 * grp, s_end - 1) & ~3;         // 4-aligned, in-range rows
+    const int tokB = min(t0 + 16 + 4 * grp, s_end - 1) & ~3;
+    const int blkA = bt[tokA / block_size], offA = tokA % block_size;
+    const int blkB = bt[tokB / block_size], offB = tokB % block_size;
+    const u16* vA = v_cache + ((long)blkA * hkv + kvh) * kv_head_stride + offA;
+    const u16* vB = v_cache + ((long)blkB * hkv + kvh) * kv_head_stride + offB;
+    uint4 vreg[DB];
+#pragma unroll
+    for (int i = 0; i < DB; ++i) {
+      const long drow = (long)(16 * i + col) * block_size;
+      const uint2 a = *reinterpret_cast<const uint2*>(vA + drow);
+      const uint2 c = *reinterpret_cast<const uint2*>(vB + drow);
+      vreg[i] = make_uint4(a.x, a.y, c.x, c.y);
+    }
+    // ---- S^T = K . Q^T for the two 16-token subtiles
+    f32x4 s_acc[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
       s_acc[s] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int kk = 0; kk < KK; ++kk) {
-        uint4 kv = *reinterpret_cast<const uint4*>(kp + kk * 32 + grp * 8);
-        s_acc[s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<bf16x8*>(&kv),
-                                                          qf[kk], s_acc[s], 0, 0, 0);
-      }
+      for (int kk = 0; kk < KK; ++kk)
+        s_acc[s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            *reinterpret_cast<bf16x8*>(&kreg[s][kk]), qf[kk], s_acc[s], 0, 0, 0);
     }
     // lane holds S^T[tok = t0 + 16s + 4grp + r][head = col]
     float p[8];
@@ -104,26 +127,14 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
 #pragma unroll
       for (int i = 0; i < DB; ++i) o_acc[i][r] *= a;
     }
-    // A operand: P[head=col][k = 8grp + j] with token order pi(grp, j) = 16(j>>2) + 4grp + (j&3)
+    // A operand: P[head=col][k = 8grp + j] in the permuted token order pi(grp, j)
     bf16x8 pa;
 #pragma unroll
     for (int j = 0; j < 8; ++j) pa[j] = (__bf16)p[j];
-    // B operand: V[tok = t0 + pi(grp, j)][d = 16 db + col] from V^T [d][tok] rows
-    const int tokA = min(t0 + 4 * grp, s_end - 1) & ~3;         // 4-aligned, in-range rows
-    const int tokB = min(t0 + 16 + 4 * grp, s_end - 1) & ~3;
-    const int blkA = bt[tokA / block_size], offA = tokA % block_size;
-    const int blkB = bt[tokB / block_size], offB = tokB % block_size;
-    const u16* vA = v_cache + ((long)blkA * hkv + kvh) * kv_head_stride + offA;
-    const u16* vB = v_cache + ((long)blkB * hkv + kvh) * kv_head_stride + offB;
 #pragma unroll
-    for (int i = 0; i < DB; ++i) {
-      const long drow = (long)(16 * i + col) * block_size;
-      uint2 a = *reinterpret_cast<const uint2*>(vA + drow);
-      uint2 c = *reinterpret_cast<const uint2*>(vB + drow);
-      uint4 w = make_uint4(a.x, a.y, c.x, c.y);
-      o_acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, *reinterpret_cast<bf16x8*>(&w),
+    for (int i = 0; i < DB; ++i)
+      o_acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, *reinterpret_cast<bf16x8*>(&vreg[i]),
                                                         o_acc[i], 0, 0, 0);
-    }
   }
   // total denominator for head `col`
   float l_tot = l_part + __shfl_xor(l_part, 16, 64);

@@ -83,8 +83,10 @@ __global__ void __launch_bounds__(SMP_THREADS) sample_kernel(
     const float* __restrict__ temperature, const int* __restrict__ top_k,
     const float* __restrict__ top_p, const long long* __restrict__ seeds) {
   __shared__ uint32_t hist[256];
-  __shared__ uint32_t ckey[SMP_CAP];
-  __shared__ int cidx[SMP_CAP];
+  __shared__ uint32_t ckey[2 * SMP_CAP];      // fast path: 512 threads x top-8 candidates
+  __shared__ int cidx[2 * SMP_CAP];
+  __shared__ uint32_t skey[512];
+  __shared__ int sidx[512];
   __shared__ float cprob[SMP_CAP];
   __shared__ float sv[16];
   __shared__ int si[16];
@@ -126,6 +128,78 @@ __global__ void __launch_bounds__(SMP_THREADS) sample_kernel(
   int Keff = (K <= 0 || K > SMP_CAP) ? SMP_CAP : K;
   if (Keff > V) Keff = V;
 
+  int n = 0;
+  bool fast_ok = false;
+  // ---- fast path: one pass over the row, each thread keeps its top-8 (key, index) in
+  // registers (static-index insertion network); the Keff-th largest of the 4096 candidates
+  // (tau) is exact iff no thread dropped an element >= tau, i.e. every thread's 8th kept key
+  // is < tau — checked with one block-wide OR. Otherwise fall back to the full radix select.
+  if (Keff <= 256) {
+    uint32_t tk[8];
+    int ti[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { tk[j] = 0u; ti[j] = 0x7fffffff; }
+    for (int i = tid; i < V; i += blockDim.x) {
+      uint32_t k = f2key(x[i]);
+      if (k > tk[7]) {
+        int id = i;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (k > tk[j]) {
+            const uint32_t t = tk[j]; tk[j] = k; k = t;
+            const int u = ti[j]; ti[j] = id; id = u;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { ckey[tid * 8 + j] = tk[j]; cidx[tid * 8 + j] = ti[j]; }
+    __syncthreads();
+    uint32_t prefix = 0, pmask = 0, k_rem = (uint32_t)Keff;
+    for (int pass = 0; pass < 4; ++pass) {
+      const int shift = 24 - 8 * pass;
+      for (int i = tid; i < 256; i += blockDim.x) hist[i] = 0;
+      __syncthreads();
+      for (int e = tid; e < 8 * SMP_THREADS; e += blockDim.x) {
+        const uint32_t k = ckey[e];
+        if ((k & pmask) == prefix) atomicAdd(&hist[(k >> shift) & 255u], 1u);
+      }
+      __syncthreads();
+      if (tid == 0) {
+        uint32_t cum = 0, d = 0;
+        for (int bb = 255; bb >= 0; --bb) {
+          if (cum + hist[bb] >= k_rem) { d = (uint32_t)bb; break; }
+          cum += hist[bb];
+        }
+        s_digit = d; s_above = cum;
+      }
+      __syncthreads();
+      k_rem -= s_above;
+      prefix |= s_digit << shift;
+      pmask |= 255u << shift;
+    }
+    const uint32_t tau = prefix;                  // key of the Keff-th largest candidate
+    fast_ok = !__syncthreads_or(tk[7] >= tau ? 1 : 0);
+    if (fast_ok) {
+      if (tid == 0) s_cnt = 0;
+      __syncthreads();
+      for (int e = tid; e < 8 * SMP_THREADS; e += blockDim.x) {
+        if (ckey[e] >= tau) {
+          const uint32_t pos = atomicAdd(&s_cnt, 1u);
+          if (pos < 512) { skey[pos] = ckey[e]; sidx[pos] = cidx[e]; }
+        }
+      }
+      __syncthreads();
+      if (s_cnt > 512) {
+        fast_ok = false;                          // absurd tie count: take the slow path
+      } else {
+        n = (int)s_cnt;
+        for (int e = tid; e < n; e += blockDim.x) { ckey[e] = skey[e]; cidx[e] = sidx[e]; }
+      }
+      __syncthreads();
+    }
+  }
+  if (!fast_ok) {
   // ---- radix select on order-preserving keys (largest first), 8-bit digits
   uint32_t prefix = 0, pmask = 0, k_rem = (uint32_t)Keff, above_total = 0;
   for (int pass = 0; pass < 4; ++pass) {
@@ -163,7 +237,8 @@ __global__ void __launch_bounds__(SMP_THREADS) sample_kernel(
     }
   }
   __syncthreads();
-  const int n = (int)min(s_cnt, (uint32_t)SMP_CAP);
+  n = (int)min(s_cnt, (uint32_t)SMP_CAP);
+  }
   int npow = 1;
   while (npow < n) npow <<= 1;
   for (int i = n + tid; i < npow; i += blockDim.x) { ckey[i] = 0u; cidx[i] = 0x7fffffff; }

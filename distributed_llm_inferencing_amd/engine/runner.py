@@ -136,10 +136,41 @@ class StageRunner:
         hidden = self.hidden_in[:b] if self.hidden_in is not None else None
         return self.model.forward(db, self.kv_layers, hidden=hidden)
 
+    def gemm_shapes(self, M: int):
+        """(shapes, weights) of every projection GEMM a decode step of M rows runs here."""
+        m = self.model
+        shapes, weights = [], {}
+        lp = m.layers[0] if m.layers else {}
+
+        def add(w, epi, rows=M):
+            if w is None or w.dim() != 2:
+                return
+            shapes.append((rows, w.shape[0], w.shape[1], epi))
+            weights[(w.shape[0], w.shape[1])] = w
+        if m.cfg.arch == "gpt2":
+            add(lp.get("wqkv"), "bias"), add(lp.get("wo"), "bias")
+            add(lp.get("w_fc"), "bias_gelu"), add(lp.get("w_proj"), "bias")
+        else:
+            add(lp.get("wqkv"), "none"), add(lp.get("wo"), "none")
+            if not m.cfg.is_moe:
+                add(lp.get("w_gu"), "silu_mul"), add(lp.get("w_down"), "none")
+        if m.is_last:
+            head = m.params["embed"] if m.cfg.tie_embeddings else m.params.get("lm_head")
+            add(head, "f32")
+        return shapes, weights
+
+    def autotune(self, buckets=None):
+        from ..ops import gemm as G
+        for b in (buckets or self.buckets):
+            shapes, weights = self.gemm_shapes(b)
+            G.autotune(shapes, weights, self.device)
+
     def capture(self, buckets=None):
         """Warm up and capture decode graphs for the given buckets (default: all)."""
         if not self.use_graphs:
             return
+        if os.environ.get("DLI_GEMM_AUTOTUNE", "1") == "1":
+            self.autotune(buckets)
         for b in (buckets or self.buckets):
             if b in self.graphs:
                 continue

@@ -103,6 +103,41 @@ def clear_plans() -> None:
     _plan_cache.clear()
 
 
+def autotune(shapes, weights: dict, device, iters: int = 8, log=None) -> dict:
+    """Measure every candidate plan for each (M, N, K, epi) and pin the fastest
+    ("measure, don't guess"). ``weights[(N, K)]`` is a real [N, K] weight of that shape.
+    Returns {shape: (plan, ms)}."""
+    from .. import ops  # local import: ops imports this module
+    out = {}
+    for (M, N, K, epi) in shapes:
+        key = (_bucket(M), N, K, epi)
+        if key in _tuned:
+            continue
+        w = weights[(N, K)]
+        x = (torch.randn(M, K, device=device) * 0.5).to(w.dtype)
+        best = None
+        for p in candidate_plans(M, N, K, epi):
+            if p.backend == "hipblaslt" and epi != "none":
+                continue
+            try:
+                ms = ops.benchmark(lambda p=p: ops._gemm_native(x, w, epi, plan=p),
+                                   iters=iters, warmup=2)
+            except Exception:  # noqa: BLE001 — an invalid candidate is skipped
+                continue
+            if best is None or ms < best[1]:
+                best = (p, ms)
+        if best is not None:
+            _plan_cache[key] = best[0]
+            _tuned.add(key)
+            out[(M, N, K, epi)] = best
+            if log:
+                log(f"[gemm autotune] M={M} N={N} K={K} {epi}: {best[0]} {best[1]*1e3:.1f} us")
+    return out
+
+
+_tuned: set = set()
+
+
 def candidate_plans(M: int, N: int, K: int, epi: str):
     out = []
     for tile, (bm, bn) in TILES.items():

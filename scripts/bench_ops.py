@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Per-op timings at the bench's decode shapes (Llama-3-8B, B=256, ctx 32..100)."""
+import math
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+from distributed_llm_inferencing_amd import ops  # noqa: E402
+from distributed_llm_inferencing_amd.ops import reference as R  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda")
+    B, hq, hkv, hd, bs, D, V = 256, 32, 8, 128, 16, 4096, 128256
+    torch.manual_seed(0)
+    lens = torch.randint(33, 100, (B,)).tolist()
+    nblk = sum(-(-n // bs) for n in lens) + 16
+    kc = (torch.randn(nblk, hkv, bs, hd, device=dev) * 0.5).to(torch.bfloat16)
+    vc = (torch.randn(nblk, hkv, hd, bs, device=dev) * 0.5).to(torch.bfloat16)
+    perm = torch.randperm(nblk).tolist()
+    W = 32
+    tables, o = [], 0
+    for n in lens:
+        nb = -(-n // bs)
+        tables.append(perm[o:o + nb] + [0] * (W - nb))
+        o += nb
+    tables = torch.tensor(tables, device=dev, dtype=torch.int32)
+    ctx = torch.tensor(lens, device=dev, dtype=torch.int32)
+    qkv = torch.randn(B, (hq + 2 * hkv) * hd, device=dev).to(torch.bfloat16)
+    res = {}
+    kv_bytes = sum(lens) * hkv * hd * 2 * 2
+    ms = ops.benchmark(lambda: ops.decode_attention(qkv, kc, vc, tables, ctx, 512, hq, hkv, hd,
+                                                    1 / math.sqrt(hd)), iters=50)
+    res["decode_attention"] = (ms * 1e3, kv_bytes / ms / 1e9)
+    logits = torch.randn(B, V, device=dev) * 1.3
+    t = torch.full((B,), 0.8, device=dev)
+    k = torch.full((B,), 50, device=dev, dtype=torch.int32)
+    p = torch.full((B,), 0.95, device=dev)
+    s = torch.arange(B, device=dev, dtype=torch.int64)
+    ms = ops.benchmark(lambda: ops.sample(logits, t, k, p, s), iters=30)
+    res["sample_topk_topp"] = (ms * 1e3, B * V * 4 / ms / 1e9)
+    x = torch.randn(B, D, device=dev).to(torch.bfloat16)
+    r = torch.randn(B, D, device=dev).to(torch.bfloat16)
+    w = torch.ones(D, device=dev, dtype=torch.bfloat16)
+    ms = ops.benchmark(lambda: ops.add_rmsnorm(x, r, w, 1e-5), iters=50)
+    res["add_rmsnorm"] = (ms * 1e3, 4 * B * D * 2 / ms / 1e9)
+    pos = ctx - 1
+    slots = torch.arange(B, device=dev, dtype=torch.int32)
+    cs = R.rope_cos_sin(2048, hd, 5e5, device=dev)
+    ms = ops.benchmark(lambda: ops.rope_and_cache(qkv, pos, slots, cs, kc, vc, hq, hkv, hd),
+                       iters=50)
+    res["rope_cache"] = (ms * 1e3, qkv.numel() * 2 * 2 / ms / 1e9)
+    for kname, (us, gbs) in res.items():
+        print(f"{kname:20s} {us:8.1f} us  {gbs:8.1f} GB/s")
+
+
+if __name__ == "__main__":
+    main()

@@ -252,3 +252,21 @@ def test_moe_route_and_mlp(gpu, T, E, k):
         out2 = ops.moe_mlp(x, wgu[2:4].contiguous(), wd[2:4].contiguous(), rw, rids, 2)
         ref2 = R.moe_mlp(x, wgu[2:4], wd[2:4], rw, rids, 2)
         close(out2, ref2, rtol=3e-2, atol=3e-2)
+
+
+def test_sampling_fallback_path_adversarial(gpu):
+    """Top-k values concentrated in ONE thread's strided slice force the exact radix-select
+    fallback (the register top-8 fast path cannot prove completeness)."""
+    torch.manual_seed(9)
+    B, V = 4, 128256
+    logits = torch.randn(B, V, device=gpu)
+    logits[:, 0::512][:, :60] += 20.0            # 60 huge values all owned by thread 0
+    temp = torch.full((B,), 0.8, device=gpu)
+    topk = torch.full((B,), 50, device=gpu, dtype=torch.int32)
+    topp = torch.full((B,), 0.95, device=gpu)
+    filt = R.topk_topp_filter(logits, temp, topk, topp)
+    for rep in range(8):
+        tok = ops.sample(logits, temp, topk, topp,
+                         torch.arange(B, device=gpu, dtype=torch.int64) + 1000 * rep)
+        assert torch.isfinite(filt.gather(1, tok.long()[:, None])).all()
+        assert (tok % 512 == 0).all()
