@@ -1,0 +1,152 @@
+// Split-K partial-sum reductions fused with the elementwise op that follows the GEMM, so a
+// decode layer runs 2 fewer kernels and never re-reads the bf16 GEMM output:
+//
+//  dli_splitk_add_rmsnorm : out = rmsnorm(residual += sum_s P_s) * w     (O-proj, down-proj)
+//                           (w == null: residual += sum_s P_s only, for a stage's last layer)
+//  dli_splitk_rope_cache  : qkv = bf16(sum_s P_s); RoPE on q,k in place; k,v -> paged cache
+//
+// P_s are the fp32 [M, N] slabs written by gemm_bf16_kernel when called with C == nullptr.
+// Numerics equal the unfused path: the GEMM result is rounded to bf16 before the residual add
+// / rotation, exactly as the bf16 GEMM output would be.
+#include "common.h"
+
+template <int VPT>
+__global__ void __launch_bounds__(256) splitk_add_rmsnorm_kernel(
+    u16* __restrict__ out, u16* __restrict__ residual, const float* __restrict__ ws, int splits,
+    int M, int N, const u16* __restrict__ w, float eps) {
+  __shared__ float red[16];
+  const int row = blockIdx.x;
+  const int nvec = N >> 3;
+  float v[VPT][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int vi = threadIdx.x + i * blockDim.x;
+    if (vi < nvec) {
+      float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int s = 0; s < splits; ++s) {
+        const float4* p = reinterpret_cast<const float4*>(ws + ((long)s * M + row) * N + vi * 8);
+        const float4 a = p[0], b = p[1];
+        acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
+        acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
+      }
+      float r[8];
+      u16* rp = residual + (long)row * N + vi * 8;
+      load8(rp, r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = bf2f(f2bf(r[j] + bf2f(f2bf(acc[j]))));
+      store8(rp, v[i]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[i][j] * v[i][j];
+    }
+  }
+  if (w == nullptr) return;
+  const float rstd = rsqrtf(block_sum(ss, red) / N + eps);
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int vi = threadIdx.x + i * blockDim.x;
+    if (vi < nvec) {
+      float wv[8], o[8];
+      load8(w + vi * 8, wv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = v[i][j] * rstd * wv[j];
+      store8(out + (long)row * N + vi * 8, o);
+    }
+  }
+}
+
+extern "C" int dli_splitk_add_rmsnorm(void* out, void* residual, const float* ws, int splits,
+                                      int M, int N, const void* w, float eps, hipStream_t st) {
+  if (M <= 0) return 0;
+  if (N % 8) return (int)hipErrorInvalidValue;
+  const int nvec = N / 8;
+  int threads = ((nvec + 63) / 64) * 64;
+  if (threads > 256) threads = 256;
+  const int vpt = (nvec + threads - 1) / threads;
+  auto o = (u16*)out; auto r = (u16*)residual; auto wp = (const u16*)w;
+  switch (vpt) {
+    case 1: splitk_add_rmsnorm_kernel<1><<<M, threads, 0, st>>>(o, r, ws, splits, M, N, wp, eps); break;
+    case 2: splitk_add_rmsnorm_kernel<2><<<M, threads, 0, st>>>(o, r, ws, splits, M, N, wp, eps); break;
+    case 3: case 4: splitk_add_rmsnorm_kernel<4><<<M, threads, 0, st>>>(o, r, ws, splits, M, N, wp, eps); break;
+    case 5: case 6: case 7: case 8:
+      splitk_add_rmsnorm_kernel<8><<<M, threads, 0, st>>>(o, r, ws, splits, M, N, wp, eps); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  DLI_RETURN_LAUNCH();
+}
+
+// one lane: 8 dims of the first half of a head + the matching 8 of the second half
+__global__ void __launch_bounds__(256) splitk_rope_cache_kernel(
+    u16* __restrict__ qkv, const float* __restrict__ ws, int splits, int T, int N,
+    const int* __restrict__ positions, const int* __restrict__ slot_mapping,
+    const float* __restrict__ cos_sin, u16* __restrict__ k_cache, u16* __restrict__ v_cache,
+    int hq, int hkv, int hd, int block_size, int use_rope) {
+  const int lanes_per_head = hd >> 4;
+  const int heads = hq + 2 * hkv;
+  const long total = (long)T * heads * lanes_per_head;
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= total) return;
+  const int c = (int)(gid % lanes_per_head);
+  const long th = gid / lanes_per_head;
+  const int h = (int)(th % heads);
+  const int t = (int)(th / heads);
+  const int half = hd >> 1, d0 = c * 8;
+  const long col1 = (long)h * hd + d0, col2 = col1 + half;
+  float x1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, x2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int s = 0; s < splits; ++s) {
+    const float* base = ws + ((long)s * T + t) * N;
+    const float4* p1 = reinterpret_cast<const float4*>(base + col1);
+    const float4* p2 = reinterpret_cast<const float4*>(base + col2);
+    const float4 a = p1[0], b = p1[1], e = p2[0], f = p2[1];
+    x1[0] += a.x; x1[1] += a.y; x1[2] += a.z; x1[3] += a.w;
+    x1[4] += b.x; x1[5] += b.y; x1[6] += b.z; x1[7] += b.w;
+    x2[0] += e.x; x2[1] += e.y; x2[2] += e.z; x2[3] += e.w;
+    x2[4] += f.x; x2[5] += f.y; x2[6] += f.z; x2[7] += f.w;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { x1[j] = bf2f(f2bf(x1[j])); x2[j] = bf2f(f2bf(x2[j])); }
+  const bool is_q = h < hq, is_k = !is_q && h < hq + hkv;
+  if (use_rope && (is_q || is_k)) {
+    const float* cs = cos_sin + (long)positions[t] * hd;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float co = cs[d0 + j], si = cs[half + d0 + j];
+      const float o1 = x1[j] * co - x2[j] * si, o2 = x2[j] * co + x1[j] * si;
+      x1[j] = bf2f(f2bf(o1));
+      x2[j] = bf2f(f2bf(o2));
+    }
+  }
+  u16* row = qkv + (long)t * N;
+  store8(row + col1, x1);
+  store8(row + col2, x2);
+  if (is_q || k_cache == nullptr) return;
+  const int slot = slot_mapping[t];
+  if (slot < 0) return;
+  const int blk = slot / block_size, off = slot - blk * block_size;
+  if (is_k) {
+    u16* dst = k_cache + (((long)blk * hkv + (h - hq)) * block_size + off) * hd;
+    store8(dst + d0, x1);
+    store8(dst + half + d0, x2);
+  } else {
+    u16* dst = v_cache + ((long)blk * hkv + (h - hq - hkv)) * hd * block_size + off;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      dst[(long)(d0 + j) * block_size] = f2bf(x1[j]);
+      dst[(long)(half + d0 + j) * block_size] = f2bf(x2[j]);
+    }
+  }
+}
+
+extern "C" int dli_splitk_rope_cache(void* qkv, const float* ws, int splits, int T, int N,
+                                     const int* positions, const int* slot_mapping,
+                                     const float* cos_sin, void* k_cache, void* v_cache, int hq,
+                                     int hkv, int hd, int block_size, int use_rope,
+                                     hipStream_t st) {
+  if (T <= 0) return 0;
+  if (hd % 16 || N != (hq + 2 * hkv) * hd) return (int)hipErrorInvalidValue;
+  const long total = (long)T * (hq + 2 * hkv) * (hd / 16);
+  splitk_rope_cache_kernel<<<(int)((total + 255) / 256), 256, 0, st>>>(
+      (u16*)qkv, ws, splits, T, N, positions, slot_mapping, cos_sin, (u16*)k_cache,
+      (u16*)v_cache, hq, hkv, hd, block_size, use_rope);
+  DLI_RETURN_LAUNCH();
+}

@@ -248,8 +248,8 @@ static int launch_cfg(const void* A, int lda, const void* W, int ldw, void* C, i
   gemm_bf16_kernel<BM, BN, EPI><<<grid, GEMM_THREADS, lds, st>>>(
       (const u16*)A, lda, (const u16*)W, ldw, C, ldc, M, N, K, ksl, (const u16*)bias,
       (float*)ws, group_off);
-  if (splits > 1) {
-    const int outN = (EPI == EPI_SILU) ? N / 2 : N;
+  if (splits > 1 && C != nullptr) {       // C == nullptr: leave the fp32 partial slabs for a
+    const int outN = (EPI == EPI_SILU) ? N / 2 : N;   // fused consumer (fused_reduce.hip)
     const long total = (long)M * outN;
     splitk_reduce_kernel<EPI><<<(int)((total + 255) / 256), 256, 0, st>>>(
         C, ldc, (const float*)ws, M, N, splits, (const u16*)bias);

@@ -78,6 +78,33 @@ __device__ float block_scan(float v, float* tmp) {
   return v + add;
 }
 
+// Visit every element of a row with 16-B loads, 4 loads in flight per thread (the sampler is
+// one workgroup per row, so memory-level parallelism per CU comes from ILP, not occupancy).
+template <typename F>
+__device__ __forceinline__ void row_scan(const float* __restrict__ x, int V, F&& f) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  int done = 0;
+  if ((reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+    const int V4 = V >> 2;
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+    int i = tid;
+    for (; i + 3 * nt < V4; i += 4 * nt) {
+      const float4 a = x4[i], b = x4[i + nt], c = x4[i + 2 * nt], d = x4[i + 3 * nt];
+      f(a.x, 4 * i); f(a.y, 4 * i + 1); f(a.z, 4 * i + 2); f(a.w, 4 * i + 3);
+      const int ib = 4 * (i + nt), ic = 4 * (i + 2 * nt), id = 4 * (i + 3 * nt);
+      f(b.x, ib); f(b.y, ib + 1); f(b.z, ib + 2); f(b.w, ib + 3);
+      f(c.x, ic); f(c.y, ic + 1); f(c.z, ic + 2); f(c.w, ic + 3);
+      f(d.x, id); f(d.y, id + 1); f(d.z, id + 2); f(d.w, id + 3);
+    }
+    for (; i < V4; i += nt) {
+      const float4 a = x4[i];
+      f(a.x, 4 * i); f(a.y, 4 * i + 1); f(a.z, 4 * i + 2); f(a.w, 4 * i + 3);
+    }
+    done = V4 * 4;
+  }
+  for (int j = done + tid; j < V; j += nt) f(x[j], j);
+}
+
 __global__ void __launch_bounds__(SMP_THREADS) sample_kernel(
     int* __restrict__ out_tokens, const float* __restrict__ logits, long row_stride, int V,
     const float* __restrict__ temperature, const int* __restrict__ top_k,
@@ -101,7 +128,7 @@ __global__ void __launch_bounds__(SMP_THREADS) sample_kernel(
 
   if (T <= 0.f || K == 1) {                                  // greedy
     ArgMax a{-INFINITY, 0x7fffffff};
-    for (int i = tid; i < V; i += blockDim.x) a = amax(a, ArgMax{x[i], i});
+    row_scan(x, V, [&](float v, int i) { a = amax(a, ArgMax{v, i}); });
     a = block_argmax(a, sv, si);
     if (tid == 0) out_tokens[row] = a.i < V ? a.i : 0;
     return;
@@ -139,8 +166,8 @@ __global__ void __launch_bounds__(SMP_THREADS) sample_kernel(
     int ti[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) { tk[j] = 0u; ti[j] = 0x7fffffff; }
-    for (int i = tid; i < V; i += blockDim.x) {
-      uint32_t k = f2key(x[i]);
+    row_scan(x, V, [&](float v, int i) {
+      uint32_t k = f2key(v);
       if (k > tk[7]) {
         int id = i;
 #pragma unroll
@@ -151,7 +178,7 @@ __global__ void __launch_bounds__(SMP_THREADS) sample_kernel(
           }
         }
       }
-    }
+    });
 #pragma unroll
     for (int j = 0; j < 8; ++j) { ckey[tid * 8 + j] = tk[j]; cidx[tid * 8 + j] = ti[j]; }
     __syncthreads();
@@ -206,10 +233,10 @@ __global__ void __launch_bounds__(SMP_THREADS) sample_kernel(
     const int shift = 24 - 8 * pass;
     for (int i = tid; i < 256; i += blockDim.x) hist[i] = 0;
     __syncthreads();
-    for (int i = tid; i < V; i += blockDim.x) {
-      const uint32_t k = f2key(x[i]);
+    row_scan(x, V, [&](float v, int) {
+      const uint32_t k = f2key(v);
       if ((k & pmask) == prefix) atomicAdd(&hist[(k >> shift) & 255u], 1u);
-    }
+    });
     __syncthreads();
     if (tid == 0) {
       uint32_t cum = 0, d = 0;
@@ -229,13 +256,13 @@ __global__ void __launch_bounds__(SMP_THREADS) sample_kernel(
   // ---- gather everything at or above the boundary bin
   if (tid == 0) s_cnt = 0;
   __syncthreads();
-  for (int i = tid; i < V; i += blockDim.x) {
-    const uint32_t k = f2key(x[i]);
+  row_scan(x, V, [&](float v, int i) {
+    const uint32_t k = f2key(v);
     if ((k & pmask) >= prefix) {
       const uint32_t pos = atomicAdd(&s_cnt, 1u);
       if (pos < SMP_CAP) { ckey[pos] = k; cidx[pos] = i; }
     }
-  }
+  });
   __syncthreads();
   n = (int)min(s_cnt, (uint32_t)SMP_CAP);
   }

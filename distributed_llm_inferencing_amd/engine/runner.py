@@ -150,10 +150,10 @@ class StageRunner:
         if m.cfg.arch == "gpt2":
             add(lp.get("wqkv"), "bias"), add(lp.get("wo"), "bias")
             add(lp.get("w_fc"), "bias_gelu"), add(lp.get("w_proj"), "bias")
-        else:
-            add(lp.get("wqkv"), "none"), add(lp.get("wo"), "none")
+        else:   # llama family: these feed the fused split-K reduces (ops.linear_*)
+            add(lp.get("wqkv"), "splitk"), add(lp.get("wo"), "splitk")
             if not m.cfg.is_moe:
-                add(lp.get("w_gu"), "silu_mul"), add(lp.get("w_down"), "none")
+                add(lp.get("w_gu"), "silu_mul"), add(lp.get("w_down"), "splitk")
         if m.is_last:
             head = m.params["embed"] if m.cfg.tie_embeddings else m.params.get("lm_head")
             add(head, "f32")

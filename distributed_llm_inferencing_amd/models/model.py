@@ -86,6 +86,8 @@ class TransformerLM:
                        kv_caches: List[Tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:
         """Runs this stage's layers; returns the hidden state with the residual folded in."""
         cfg = self.cfg
+        if cfg.arch != "gpt2":
+            return self._llama_layers(x, b, kv_caches)
         residual = torch.empty_like(x)
         pending = None             # output of the previous sub-block awaiting its residual add
         for li, lp in enumerate(self.layers):
@@ -118,6 +120,45 @@ class TransformerLM:
             return x
         residual.add_(pending)
         return residual
+
+    def _llama_layers(self, x: torch.Tensor, b: DeviceBatch, kv_caches) -> torch.Tensor:
+        """Llama / Mixtral layers with the split-K reduces fused into their consumers:
+        QKV GEMM -> (reduce + RoPE + KV write), O GEMM -> (reduce + residual add + RMSNorm),
+        down GEMM -> (reduce + residual add + NEXT layer's input RMSNorm)."""
+        cfg = self.cfg
+        eps = cfg.norm_eps
+        residual = torch.empty_like(x)
+        n = len(self.layers)
+        if n == 0:
+            return x
+        h = ops.rmsnorm(x, self.layers[0]["attn_norm"], eps, residual_copy=residual)
+        pending = None
+        for li, lp in enumerate(self.layers):
+            kc, vc = kv_caches[li] if kv_caches else (None, None)
+            if pending is not None:          # MoE output of the previous layer
+                h = ops.add_rmsnorm(pending, residual, lp["attn_norm"], eps)
+                pending = None
+            qkv = ops.linear_rope_cache(h, lp["wqkv"], b.positions, b.slot_mapping, self.cos_sin,
+                                        kc, vc, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim)
+            attn = self._attend(qkv, b, kc, vc)
+            h = ops.linear_add_rmsnorm(attn, lp["wo"], residual, lp["mlp_norm"], eps)
+            if cfg.is_moe:
+                pending = self.moe_fn(h, lp, self.layer_start + li)
+                continue
+            act = ops.linear(h, lp["w_gu"], epi="silu_mul")
+            nxt = self.layers[li + 1]["attn_norm"] if li + 1 < n else None
+            h = ops.linear_add_rmsnorm(act, lp["w_down"], residual, nxt, eps)
+        if pending is not None:
+            residual.add_(pending)
+        return residual
+
+    def _attend(self, qkv, b: DeviceBatch, kc, vc) -> torch.Tensor:
+        cfg = self.cfg
+        if b.is_prefill:
+            return ops.prefill_attention(qkv, b.cu_seqlens, b.max_seqlen, cfg.num_heads,
+                                         cfg.num_kv_heads, cfg.head_dim, self.scale)
+        return ops.decode_attention(qkv, kc, vc, b.block_tables, b.context_lens, b.max_context,
+                                    cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, self.scale)
 
     def _attention(self, qkv, b: DeviceBatch, kc, vc) -> torch.Tensor:
         cfg = self.cfg

@@ -18,6 +18,7 @@ from . import reference as R
 
 _native_call = N.call
 _p = N.ptr
+_FUSED_OFF = __import__("os").environ.get("DLI_NO_FUSED_REDUCE", "0") == "1"   # A/B switch
 
 
 def _use_native(t: torch.Tensor) -> bool:
@@ -154,6 +155,61 @@ def linear(x, w, bias=None, epi: str = "none", out=None):
     if x.stride(-1) != 1 or w.stride(-1) != 1:
         raise ValueError("linear: inner dims must be contiguous")
     return _gemm_native(x, w, epi, bias=bias, out=out)
+
+
+def _splitk_plan(x, w):
+    """A split-K plan for a GEMM whose partial sums feed a fused reduce, or None."""
+    if not _use_native(x) or x.stride(-1) != 1 or w.stride(-1) != 1:
+        return None
+    if _FUSED_OFF:
+        return None
+    M, K = x.shape
+    p = G.plan(M, w.shape[0], K, "splitk")
+    return p if (p.backend == "dli" and p.splits > 1) else None
+
+
+def linear_add_rmsnorm(x, w, residual, norm_w, eps):
+    """residual += x @ w.T (bf16-rounded, in place); returns rmsnorm(residual) * norm_w
+    (None when norm_w is None). Split-K GEMMs reduce their partial slabs inside the norm
+    kernel (fused_reduce.hip), so the bf16 GEMM output is never materialised."""
+    p = _splitk_plan(x, w)
+    if p is None:
+        y = linear(x, w)
+        if norm_w is None:
+            residual.add_(y)             # bf16 add computes in fp32 and rounds once
+            return None
+        return add_rmsnorm(y, residual, norm_w, eps)
+    M, K = x.shape
+    Nn = w.shape[0]
+    ws = G.workspace(x.device, p.splits * M * Nn * 4)
+    _native_call("dli_gemm", _p(x), x.stride(0), _p(w), w.stride(-2), None, Nn, M, Nn, K,
+                 0, p.tile, p.splits, None, _p(ws), None, 1, _st())
+    out = torch.empty_like(residual) if norm_w is not None else None
+    _native_call("dli_splitk_add_rmsnorm", _p(out), _p(residual), _p(ws), p.splits, M, Nn,
+                 _p(norm_w), eps, _st())
+    return out
+
+
+def linear_rope_cache(x, w, positions, slot_mapping, cos_sin, k_cache, v_cache, hq, hkv, hd,
+                      use_rope: bool = True):
+    """qkv = x @ w.T with RoPE applied in place to q,k and k,v written to the paged cache."""
+    p = _splitk_plan(x, w)
+    if p is None:
+        qkv = linear(x, w)
+        rope_and_cache(qkv, positions, slot_mapping, cos_sin, k_cache, v_cache, hq, hkv, hd,
+                       use_rope)
+        return qkv
+    M, K = x.shape
+    Nn = w.shape[0]
+    ws = G.workspace(x.device, p.splits * M * Nn * 4)
+    _native_call("dli_gemm", _p(x), x.stride(0), _p(w), w.stride(-2), None, Nn, M, Nn, K,
+                 0, p.tile, p.splits, None, _p(ws), None, 1, _st())
+    qkv = torch.empty(M, Nn, dtype=x.dtype, device=x.device)
+    bs = k_cache.shape[2] if k_cache is not None else 16
+    _native_call("dli_splitk_rope_cache", _p(qkv), _p(ws), p.splits, M, Nn, _p(positions),
+                 _p(slot_mapping), _p(cos_sin), _p(k_cache), _p(v_cache), hq, hkv, hd, bs,
+                 int(use_rope), _st())
+    return qkv
 
 
 def silu_mul(gu):

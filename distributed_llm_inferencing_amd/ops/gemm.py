@@ -22,7 +22,9 @@ from dataclasses import dataclass
 import torch
 
 TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256), 4: (256, 128)}
-EPI = {"none": 0, "f32": 1, "silu_mul": 2, "bias_gelu": 3, "bias": 4}
+# "splitk": a plain GEMM whose fp32 partial slabs feed a fused reduce (ops.linear_add_rmsnorm,
+# ops.linear_rope_cache); planned/tuned separately, only split-K >= 2 candidates qualify.
+EPI = {"none": 0, "f32": 1, "silu_mul": 2, "bias_gelu": 3, "bias": 4, "splitk": 0}
 NUM_CUS = int(os.environ.get("DLI_NUM_CUS", "256"))
 
 
@@ -72,6 +74,8 @@ def _heuristic(M: int, N: int, K: int, epi: str) -> GemmPlan:
     while (tiles * splits * 2 <= 3 * NUM_CUS and K % (64 * splits * 2) == 0
            and K // (splits * 2) >= 512 and splits < 8):
         splits *= 2
+    if epi == "splitk" and splits == 1 and K % 128 == 0 and K >= 1024:
+        splits = 2            # the fused reduce consumes partial slabs: need >= 2 slices
     return GemmPlan("dli", tile, splits)
 
 
@@ -147,6 +151,8 @@ def candidate_plans(M: int, N: int, K: int, epi: str):
             continue
         for splits in (1, 2, 4, 8):
             if K % (64 * splits) or K // splits < 256:
+                continue
+            if epi == "splitk" and splits == 1:
                 continue
             tiles = -(-M // bm) * -(-N // bn)
             if splits > 1 and tiles * splits > 4 * NUM_CUS:

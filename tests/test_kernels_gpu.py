@@ -109,6 +109,45 @@ def test_gemm_epilogues(gpu, epi, M, N, K):
                 assert out.dtype == torch.float32
 
 
+@pytest.mark.parametrize("M,N,K", [(3, 512, 1024), (256, 4096, 4096), (77, 4096, 14336)])
+def test_fused_splitk_add_rmsnorm(gpu, M, N, K):
+    torch.manual_seed(11)
+    x, w = rnd(M, K, dev=gpu), rnd(N, K, dev=gpu, scale=0.02)
+    r0, nw = rnd(M, N, dev=gpu), rnd(N, dev=gpu)
+    y = R.linear(x, w)                                    # bf16-rounded GEMM output
+    ref_out, ref_res = R.fused_add_rmsnorm(y, r0, nw, 1e-5)
+    for splits in (2, 4):
+        G.set_plan(M, N, K, "splitk", G.GemmPlan("dli", 0, splits))
+        res = r0.clone()
+        out = ops.linear_add_rmsnorm(x, w, res, nw, 1e-5)
+        close(out, ref_out, rtol=2e-2, atol=3e-2)
+        close(res, ref_res, rtol=1e-2, atol=2e-2)
+        res2 = r0.clone()
+        assert ops.linear_add_rmsnorm(x, w, res2, None, 1e-5) is None
+        assert torch.equal(res2, res)                     # add-only mode: same residual
+    G.clear_plans()
+
+
+@pytest.mark.parametrize("hq,hkv,hd", [(32, 8, 128), (4, 2, 64)])
+def test_fused_splitk_rope_cache(gpu, hq, hkv, hd):
+    lens = [5, 17, 1, 40]
+    T = sum(lens)
+    _, pos, slots, kc, vc, _ = _paged_setup(gpu, lens, hq, hkv, hd, 16)
+    K = 1024
+    N = (hq + 2 * hkv) * hd
+    x, w = rnd(T, K, dev=gpu), rnd(N, K, dev=gpu, scale=0.05)
+    cs = R.rope_cos_sin(256, hd, 500000.0, device=gpu)
+    ref = R.linear(x, w)
+    kc1, vc1 = kc.clone(), vc.clone()
+    R.rope_and_cache(ref, pos, slots, cs, kc1, vc1, hq, hkv, hd)
+    G.set_plan(T, N, K, "splitk", G.GemmPlan("dli", 0, 4))
+    out = ops.linear_rope_cache(x, w, pos, slots, cs, kc, vc, hq, hkv, hd)
+    G.clear_plans()
+    close(out, ref, rtol=2e-2, atol=2e-2)
+    close(kc, kc1, rtol=2e-2, atol=2e-2)
+    close(vc, vc1, rtol=2e-2, atol=2e-2)
+
+
 def test_silu_mul_and_bias_act(gpu):
     gu = rnd(9, 2 * 512, dev=gpu)
     close(ops.silu_mul(gu), R.silu_mul(gu))
