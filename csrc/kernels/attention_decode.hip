@@ -1,7 +1,7 @@
 // Paged decode attention (one query token per sequence, GQA) on MFMA — SURVEY.md §2.4 K8.
 //
-// Work decomposition: workgroup = (kv head, sequence, KV split); 4 waves; each wave walks
-// 32-token tiles of the split round-robin. Per tile, with the GQA group of G <= 16 query
+// Work decomposition: one wave per (sequence, kv head, KV split) item, 4 independent items per
+// workgroup; the wave walks the split's 32-token tiles. Per tile, with the GQA group of G <= 16 query
 // heads padded to 16 MFMA columns:
 //   S^T[tok, head] = K[tok, :] . Q[head, :]^T   (mfma_f32_16x16x32_bf16, K rows as the A
 //                                                operand straight from the cache: 16-B loads)
@@ -10,8 +10,7 @@
 //                                                permuted token order, so P never leaves
 //                                                registers; V^T is stored token-contiguous in
 //                                                the cache so the B operand is two 8-B loads)
-// The 4 waves' (m, l, O) are merged through LDS; with >1 split the partials go to a
-// workspace reduced by a second kernel.
+// With >1 split the per-split (m, l, O) go to a workspace merged by a second kernel.
 //
 // Layouts: q rows of stride q_stride (the fused QKV buffer), k_cache [nblk,Hkv,bs,hd],
 // v_cache [nblk,Hkv,hd,bs], block_tables [B, max_blocks], out [B, Hq, hd].
@@ -25,20 +24,23 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
     u16* __restrict__ out, const u16* __restrict__ q, int q_stride,
     const u16* __restrict__ k_cache, const u16* __restrict__ v_cache,
     const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ context_lens,
-    int hq, int hkv, int block_size, float scale_log2, int num_splits, int split_tokens,
+    int B, int hq, int hkv, int block_size, float scale_log2, int num_splits, int split_tokens,
     float* __restrict__ ws_o, float* __restrict__ ws_ml) {
   constexpr int KK = HD / 32;     // MFMA k-steps over head_dim
   constexpr int DB = HD / 16;     // 16-wide output column blocks
-  const int kvh = blockIdx.x, b = blockIdx.y, split = blockIdx.z;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  // one WAVE per work item (sequence, kv head, KV split): no LDS, no barriers, so every
+  // resident wave of the chip streams a different (seq, head) pair concurrently
+  const int item = blockIdx.x * DEC_WAVES + (threadIdx.x >> 6);
+  if (item >= B * hkv * num_splits) return;                    // wave-uniform exit
+  const int split = item % num_splits;
+  const int bh = item / num_splits;
+  const int kvh = bh % hkv, b = bh / hkv;
   const int col = lane & 15, grp = lane >> 4;
   const int G = hq / hkv;
   const int ctx = context_lens[b];
   const int s_begin = split * split_tokens;
   const int s_end = min(ctx, s_begin + split_tokens);
-
-  __shared__ float sh_o[DEC_WAVES][16][HD];
-  __shared__ float sh_m[DEC_WAVES][16], sh_l[DEC_WAVES][16];
 
   // Q^T fragments (B operand): head = col, dims 32kk + 8grp .. +7
   bf16x8 qf[KK];
@@ -60,9 +62,8 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
 #pragma unroll
   for (int i = 0; i < DB; ++i) o_acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int t0 = s_begin + wid * DEC_TILE; t0 < s_end; t0 += DEC_WAVES * DEC_TILE) {
-    // ---- issue every global load of the tile up front (K fragments AND V fragments) so the
-    // tile pays one HBM round trip instead of two (V used to wait for the softmax)
+  for (int t0 = s_begin; t0 < s_end; t0 += DEC_TILE) {
+    // ---- issue every global load of the tile up front (K fragments AND V fragments)
     uint4 kreg[2][KK];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -136,48 +137,29 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
       o_acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, *reinterpret_cast<bf16x8*>(&vreg[i]),
                                                         o_acc[i], 0, 0, 0);
   }
-  // total denominator for head `col`
+  // ---- finalize: denominator of head `col`, then rows 4grp + r of O
   float l_tot = l_part + __shfl_xor(l_part, 16, 64);
   l_tot += __shfl_xor(l_tot, 32, 64);
-  if (grp == 0) { sh_m[wid][col] = m_run; sh_l[wid][col] = l_tot; }
 #pragma unroll
-  for (int i = 0; i < DB; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) sh_o[wid][4 * grp + r][16 * i + col] = o_acc[i][r];
-  __syncthreads();
-
-  // merge the 4 waves: each thread produces 8 consecutive output dims of one head
-  const int per_head = HD / 8;
-  for (int idx = threadIdx.x; idx < G * per_head; idx += blockDim.x) {
-    const int h = idx / per_head, d0 = (idx % per_head) * 8;
-    float M = -INFINITY;
-#pragma unroll
-    for (int w = 0; w < DEC_WAVES; ++w) M = fmaxf(M, sh_m[w][h]);
-    float den = 0.f, acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (M != -INFINITY) {
-#pragma unroll
-      for (int w = 0; w < DEC_WAVES; ++w) {
-        const float f = exp2f(sh_m[w][h] - M);
-        den += f * sh_l[w][h];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] += f * sh_o[w][h][d0 + j];
-      }
-    }
-    const float inv = den > 0.f ? 1.f / den : 0.f;
+  for (int r = 0; r < 4; ++r) {
+    const int h = 4 * grp + r;
+    const float lr = __shfl(l_tot, h, 64);
+    const float mr = __shfl(m_run, h, 64);
+    if (h >= G) continue;
     const int qh = kvh * G + h;
+    const float inv = lr > 0.f ? 1.f / lr : 0.f;
     if (num_splits == 1) {
-      float o8[8];
+      u16* op = out + ((long)b * hq + qh) * HD;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o8[j] = acc[j] * inv;
-      store8(out + ((long)b * hq + qh) * HD + d0, o8);
+      for (int i = 0; i < DB; ++i) op[16 * i + col] = f2bf(o_acc[i][r] * inv);
     } else {
-      float* wo = ws_o + (((long)b * hq + qh) * num_splits + split) * HD + d0;
+      const long base = ((long)b * hq + qh) * num_splits + split;
+      float* wo = ws_o + base * HD;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) wo[j] = acc[j] * inv;
-      if (d0 == 0) {
-        float* ml = ws_ml + (((long)b * hq + qh) * num_splits + split) * 2;
-        ml[0] = M;
-        ml[1] = den;
+      for (int i = 0; i < DB; ++i) wo[16 * i + col] = o_acc[i][r] * inv;
+      if (col == 0) {
+        ws_ml[base * 2] = lr > 0.f ? mr : -INFINITY;
+        ws_ml[base * 2 + 1] = lr;
       }
     }
   }
@@ -229,16 +211,17 @@ extern "C" int dli_decode_attention(void* out, const void* q, int q_stride, cons
   float* ws_o = (float*)workspace;
   float* ws_ml = ws_o ? ws_o + (long)B * hq * num_splits * hd : nullptr;
   const float scale_log2 = scale * 1.4426950408889634f;
-  dim3 grid(hkv, B, num_splits);
+  const long items = (long)B * hkv * num_splits;
+  dim3 grid((int)((items + DEC_WAVES - 1) / DEC_WAVES));
   if (hd == 128)
-    decode_attn_kernel<128><<<grid, 256, 0, st>>>(
+    decode_attn_kernel<128><<<grid, 64 * DEC_WAVES, 0, st>>>(
         (u16*)out, (const u16*)q, q_stride, (const u16*)k_cache, (const u16*)v_cache,
-        block_tables, max_blocks, context_lens, hq, hkv, block_size, scale_log2, num_splits,
+        block_tables, max_blocks, context_lens, B, hq, hkv, block_size, scale_log2, num_splits,
         split_tokens, ws_o, ws_ml);
   else
-    decode_attn_kernel<64><<<grid, 256, 0, st>>>(
+    decode_attn_kernel<64><<<grid, 64 * DEC_WAVES, 0, st>>>(
         (u16*)out, (const u16*)q, q_stride, (const u16*)k_cache, (const u16*)v_cache,
-        block_tables, max_blocks, context_lens, hq, hkv, block_size, scale_log2, num_splits,
+        block_tables, max_blocks, context_lens, B, hq, hkv, block_size, scale_log2, num_splits,
         split_tokens, ws_o, ws_ml);
   if (num_splits > 1) {
     const long total = (long)B * hq * (hd / 8);

@@ -267,10 +267,11 @@ def prefill_attention(qkv, cu_seqlens, max_seqlen: int, hq, hkv, hd, scale, out=
 
 
 def decode_num_splits(B: int, hkv: int, max_context: int) -> int:
-    """KV splits so that B*Hkv*splits workgroups cover the chip for long contexts."""
-    wgs = B * hkv
+    """KV splits so that the B*Hkv*splits work items (one wave each) fill the chip's ~2048
+    resident waves for long contexts, keeping >= 128 tokens per split."""
+    items = B * hkv
     splits = 1
-    while wgs * splits < 512 and max_context // (splits * 2) >= 256:
+    while items * splits < 2048 and max_context // (splits * 2) >= 128 and splits < 64:
         splits *= 2
     return splits
 
