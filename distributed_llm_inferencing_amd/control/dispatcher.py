@@ -25,6 +25,8 @@ from typing import Callable, Dict, List, Optional
 
 import requests
 
+from ..utils import faults
+
 log = logging.getLogger("dli.dispatcher")
 
 MAX_LENGTH = 100            # views.py:351,417
@@ -149,6 +151,7 @@ class Dispatcher:
         (False, msg) on a connection failure (retry elsewhere)."""
         t0 = time.perf_counter()
         try:
+            faults.check("dispatch.post")
             if shard_ids is None:
                 r = self._post(node, "/load_model", {"model_name": model}, HTTP_LOAD_TIMEOUT)
                 if r.status_code != 200:
@@ -159,7 +162,7 @@ class Dispatcher:
             if shard_ids is not None:
                 payload["shard_ids"] = sorted(shard_ids)
             r = self._post(node, "/inference", payload, HTTP_INFER_TIMEOUT)
-        except requests.RequestException as e:
+        except (requests.RequestException, faults.InjectedFault) as e:
             return False, f"Connection error: {e}"
         if r.status_code == 200:
             data = r.json()

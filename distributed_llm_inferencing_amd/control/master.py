@@ -328,7 +328,8 @@ def main(argv=None):
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--port", type=int, default=8000)
     a = ap.parse_args(argv)
-    logging.basicConfig(level=logging.INFO)
+    from ..utils.log import setup_logging
+    setup_logging("master")
     app = create_master_app()
     app.run(host=a.host, port=a.port, threaded=True)
 

@@ -23,6 +23,7 @@ from .kv_cache import KVCache, auto_num_blocks
 from .runner import StageRunner
 from .scheduler import Scheduler
 from .sequence import RequestOutput, SamplingParams, Sequence
+from ..utils.tracing import SpanLog, StepTimer, trace_range
 
 
 @dataclass
@@ -94,6 +95,8 @@ class LLMEngine:
                                   use_graphs=use_graphs)
         self.tokenizer = load_tokenizer(cfg, tokenizer_path)
         self.stats = EngineStats()
+        self.timer = StepTimer()
+        self.spans = SpanLog()
         self._ids = itertools.count()
         self.max_batch = max_batch
         self.max_model_len = max_model_len
@@ -117,12 +120,17 @@ class LLMEngine:
         self.runner.capture(buckets)
 
     def step(self) -> List[RequestOutput]:
-        meta = self.scheduler.schedule(0)
+        with self.timer.phase("schedule"):
+            meta = self.scheduler.schedule(0)
         if meta is not None:
             t0 = time.perf_counter()
-            tokens = self.runner.run(meta)
-            tok = tokens.cpu().numpy() if tokens.is_cuda else tokens.numpy()
-            self.scheduler.update(meta, tok)
+            kind = "prefill" if meta.kind == 1 else "decode"
+            with trace_range(f"engine.{kind}[{meta.num_seqs}]"), self.timer.phase(f"run_{kind}"):
+                tokens = self.runner.run(meta)
+            with self.timer.phase("sync"):
+                tok = tokens.cpu().numpy() if tokens.is_cuda else tokens.numpy()
+            with self.timer.phase("update"):
+                self.scheduler.update(meta, tok)
             self.stats.busy_s += time.perf_counter() - t0
             self.stats.steps += 1
             self.stats.tokens_out += meta.num_seqs
@@ -136,6 +144,7 @@ class LLMEngine:
             o = seq_to_output(seq, self.tokenizer)
             self.stats.finished += 1
             self.stats.latencies.append(o.latency_s)
+            self.spans.record(o)
             outs.append(o)
         return outs
 

@@ -27,6 +27,8 @@ import torch
 import torch.distributed as dist
 
 from ..engine.batch import HEADER_LEN
+from ..utils import faults
+from ..utils.tracing import trace_range
 
 HDR32 = 2 * HEADER_LEN
 CTRL_MAX = int(os.environ.get("DLI_CTRL_MAX_WORDS", str(24 * 1024)))
@@ -91,6 +93,12 @@ class TorchDistTransport(Transport):
             r.wait()
 
     def exchange(self, send: Optional[Message], recv: bool) -> Optional[Message]:
+        if send is not None and faults.active():
+            faults.check("transport.exchange", tick=int(send.header[H_TICK]))
+        with trace_range("pp.exchange"):
+            return self._exchange(send, recv)
+
+    def _exchange(self, send: Optional[Message], recv: bool) -> Optional[Message]:
         nxt, prv = self._peer(self.next), self._peer(self.prev)
         # ---- phase 1: control words
         ops = []

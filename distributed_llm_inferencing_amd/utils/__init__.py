@@ -1,1 +1,1 @@
-
+"""Cross-cutting utilities: tracing (roctx, request spans), fault injection, logging."""

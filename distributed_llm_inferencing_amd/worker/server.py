@@ -40,6 +40,8 @@ from ..config import Settings, get_settings
 from ..engine.sequence import SamplingParams
 from ..models.configs import get_config
 from ..shard.writer import load_shard, read_metadata, stage_plan_from_metadata
+from ..utils import faults
+from ..utils.log import setup_logging
 from .service import EngineService
 
 log = logging.getLogger("dli.worker")
@@ -184,6 +186,10 @@ def create_worker_app(settings: Optional[Settings] = None, device: Optional[str]
     @app.get("/health")
     @require_auth
     def health():
+        try:
+            faults.check("worker.health")
+        except faults.InjectedFault as e:
+            return jsonify({"status": "error", "message": str(e)}), 503
         shard_info = [{"model_name": m, "shard_id": sid, "path": r["path"],
                        "metadata": r["metadata"]}
                       for m, sh in st.shards.items() for sid, r in sh.items()]
@@ -258,6 +264,7 @@ def create_worker_app(settings: Optional[Settings] = None, device: Optional[str]
             if k in data:
                 setattr(params, k, data[k])
         try:
+            faults.check("worker.inference")
             if shard_ids:
                 svc = getattr(st, "pipeline_service", None)
                 if svc is not None and name == getattr(st, "pipeline_model", None):
@@ -339,7 +346,7 @@ def main(argv=None):
     ap.add_argument("--preload", default="", help="comma-separated models to load at start")
     ap.add_argument("--max-batch", type=int, default=None)
     a = ap.parse_args(argv)
-    logging.basicConfig(level=logging.INFO)
+    setup_logging(f"worker{a.port}")
     s = get_settings()
     dev = None
     if a.gpu is not None:
