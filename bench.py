@@ -96,6 +96,9 @@ def run_pipeline(args, world, rank):
     if mode == "ep":      # Mixtral: DP attention + experts sharded over ranks (all-to-all)
         from distributed_llm_inferencing_amd.parallel.expert import bench_expert_parallel
         return bench_expert_parallel(args, world, rank, make_prompts)
+    if mode == "tp":      # ablation: Megatron-style head/FFN sharding, 2 all-reduces/layer
+        from distributed_llm_inferencing_amd.parallel.tensor import bench_tensor_parallel
+        return bench_tensor_parallel(args, world, rank, make_prompts)
     from distributed_llm_inferencing_amd.parallel.pipeline import bench_pipeline
     return bench_pipeline(args, world, rank, make_prompts)
 
@@ -110,8 +113,9 @@ def main():
     ap.add_argument("--prompt-len", type=int, default=32)
     ap.add_argument("--max-length", type=int, default=100)
     ap.add_argument("--max-model-len", type=int, default=512)
-    ap.add_argument("--mode", default="auto", choices=["auto", "pp", "ep"],
-                    help="N>1: pp = layer-sharded pipeline (dense), ep = expert parallel (MoE)")
+    ap.add_argument("--mode", default="auto", choices=["auto", "pp", "ep", "tp"],
+                    help="N>1: pp = layer-sharded pipeline (dense), ep = expert parallel (MoE),"
+                         " tp = tensor-parallel ablation (dense)")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

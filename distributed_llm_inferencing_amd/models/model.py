@@ -46,6 +46,9 @@ class TransformerLM:
             self.cos_sin = R.rope_cos_sin(cfg.max_position, cfg.head_dim, cfg.rope_theta,
                                           device=self.device)
         self.moe_fn: Callable = self._moe_local
+        # tensor-parallel mode (parallel/tensor.py): all-reduce(sum) of the row-parallel
+        # O / down projections before their residual add
+        self.tp_reduce: Optional[Callable] = None
         self.layers = [self._layer_params(i) for i in range(self.layer_start, self.layer_end)]
 
     # ------------------------------------------------------------------ construction
@@ -141,16 +144,25 @@ class TransformerLM:
             qkv = ops.linear_rope_cache(h, lp["wqkv"], b.positions, b.slot_mapping, self.cos_sin,
                                         kc, vc, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim)
             attn = self._attend(qkv, b, kc, vc)
-            h = ops.linear_add_rmsnorm(attn, lp["wo"], residual, lp["mlp_norm"], eps)
+            h = self._proj_add_norm(attn, lp["wo"], residual, lp["mlp_norm"], eps)
             if cfg.is_moe:
                 pending = self.moe_fn(h, lp, self.layer_start + li)
                 continue
             act = ops.linear(h, lp["w_gu"], epi="silu_mul")
             nxt = self.layers[li + 1]["attn_norm"] if li + 1 < n else None
-            h = ops.linear_add_rmsnorm(act, lp["w_down"], residual, nxt, eps)
+            h = self._proj_add_norm(act, lp["w_down"], residual, nxt, eps)
         if pending is not None:
             residual.add_(pending)
         return residual
+
+    def _proj_add_norm(self, x, w, residual, norm_w, eps):
+        if self.tp_reduce is None:
+            return ops.linear_add_rmsnorm(x, w, residual, norm_w, eps)
+        y = self.tp_reduce(ops.linear(x, w))
+        if norm_w is None:
+            residual.add_(y)
+            return None
+        return ops.add_rmsnorm(y, residual, norm_w, eps)
 
     def _attend(self, qkv, b: DeviceBatch, kc, vc) -> torch.Tensor:
         cfg = self.cfg

@@ -142,3 +142,42 @@ def test_expert_parallel_gloo_matches_dense():
         assert exch > 0
     # lockstep: both ranks ran the same number of MoE exchanges
     assert res[0][3] == res[1][3]
+
+
+def _tp_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    import torch.distributed as dist
+    from distributed_llm_inferencing_amd.parallel.tensor import TensorParallelEngine
+    eng = TensorParallelEngine("llama-tiny", "cpu", max_batch=8, max_model_len=64,
+                               num_blocks=64, dtype=torch.float32)
+    greedy = SamplingParams(max_length=16, do_sample=False, ignore_eos=True)
+    sampled = SamplingParams(max_length=16, seed=5, ignore_eos=True)
+    out = ([o.all_ids for o in eng.generate(PROMPTS[:3], greedy)],
+           [o.all_ids for o in eng.generate(PROMPTS[:3], sampled)])
+    q.put((rank, out, eng.reduce.calls, eng.engine.cfg.num_kv_heads))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_tensor_parallel_gloo_matches_dense():
+    """Head/FFN-sharded layers + all-reduce over 2 gloo ranks == the unsharded model."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tp_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    eng = LLMEngine("llama-tiny", device="cpu", dtype=torch.float32, max_batch=8,
+                    max_model_len=64, num_blocks=64)
+    greedy = [o.all_ids for o in eng.generate(PROMPTS[:3], SamplingParams(
+        max_length=16, do_sample=False, ignore_eos=True))]
+    assert res[0][1][0] == greedy and res[1][1][0] == greedy
+    assert res[0][1][1] == res[1][1][1]            # ranks agree on sampled tokens
+    assert res[0][2] > 0 and res[0][3] == 1        # 2 kv heads split over 2 ranks
