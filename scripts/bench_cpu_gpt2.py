@@ -42,7 +42,11 @@ def main(n_ref=3, n_ours=16):
     dt = time.perf_counter() - t0
     ours = {"tok_s": sum(len(o.output_ids) for o in outs) / dt,
             "p50_s": statistics.median(o.latency_s for o in outs), "concurrent": n_ours}
+    # same serial batch-1 strategy as the reference, for a like-for-like latency
+    lat1 = [eng.generate([p], sp)[0].latency_s for p in prompts[:n_ref]]
+    ours_b1 = {"tok_s": 68 * n_ref / sum(lat1), "p50_s": statistics.median(lat1)}
     res = {"config": "gpt2, 1 CPU worker", "reference_strategy": ref, "ours": ours,
+           "ours_batch1_serial": ours_b1,
            "threads": torch.get_num_threads()}
     print(json.dumps(res))
     Path("profiles").mkdir(exist_ok=True)
