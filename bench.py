@@ -11,7 +11,7 @@ tokens (fixed work per step).
 One "step" = one wave of requests served end to end (submit -> last token): --batch
 requests per GPU-worker, so per-GPU work is fixed as N grows (weak scaling). N = 1 runs
 the single-GPU engine; N > 1 splits the 32 layers into N contiguous stages (one per GPU,
-``parallel/pipeline.py``) with N microbatches of --batch requests in flight.
+``parallel/pipeline.py``) with N + 1 microbatches of --batch requests in flight.
 
     python bench.py                               # N=1 defaults
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8
@@ -109,7 +109,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--model", default="llama3-8b")
-    ap.add_argument("--batch", type=int, default=256, help="requests per GPU-worker per wave")
+    ap.add_argument("--batch", type=int, default=512, help="requests per microbatch (per GPU-worker) per wave")
     ap.add_argument("--prompt-len", type=int, default=32)
     ap.add_argument("--max-length", type=int, default=100)
     ap.add_argument("--max-model-len", type=int, default=512)

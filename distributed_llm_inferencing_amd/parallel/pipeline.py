@@ -9,10 +9,13 @@ shards) — made real:
 * rank 0 (the head) owns the scheduler, the C++ block allocator and the tokenizer; every
   step's packed metadata rides with the activations through the ring, so the other stages
   hold no scheduling state at all;
-* M = N microbatches circulate: while microbatch m is in stage r, stage r-1 runs m+1, so
-  all N GPUs are busy in steady state; the tail samples on device and returns int32 tokens
-  to the head (C3), which schedules that microbatch's next step one ring later;
-* sessions: the head drives the ring while it has work, then sends STOP; other ranks
+* M = N + 1 microbatches circulate: while microbatch m is in stage r, stage r-1 runs the
+  next one, so all N GPUs are busy in steady state; the tail samples on device and returns
+  int32 tokens to the head (C3), which schedules that microbatch's next step a tick after
+  they arrived (the extra microbatch keeps the head's host off the critical path);
+* control plane (gloo, host) / data plane (RCCL, stream-ordered): see ``transport.py`` —
+  non-head ranks never synchronise their host with their GPU;
+* sessions: the head drives ticks while it has work, then broadcasts STOP; other ranks
   block waiting for the next session; SHUTDOWN ends them.
 
 ``LocalPipeline`` runs the same partitioned stages and tick schedule in ONE process (all
@@ -40,29 +43,29 @@ from ..models.model import TransformerLM
 from ..runtime import BlockManager
 from ..shard.planner import StagePlan, plan_stages
 from ..tokenizer import load_tokenizer
-from .transport import (DATA_HIDDEN, DATA_NONE, DATA_TOKENS, H_DATA_COLS, H_DATA_KIND,
-                        H_DATA_ROWS, H_TICK, Message, TorchDistTransport, init_distributed)
+from .transport import H_TICK, PipeChannel, init_distributed
 
 SHUTDOWN = 4
 
 
-def _control(kind: int, tick: int) -> Message:
-    h = np.zeros(HEADER_LEN, dtype=np.int64)
-    h[0] = kind
-    h[H_TICK] = tick
-    return Message(header=h, payload=np.zeros(0, dtype=np.int32), data=None)
-
-
-def _msg_from(meta: StepMeta, data: Optional[torch.Tensor], tick: int, tokens: bool) -> Message:
-    h, payload = meta.pack()
-    h[H_TICK] = tick
-    if data is None:
-        h[H_DATA_KIND] = DATA_NONE
-    elif tokens:
-        h[H_DATA_KIND], h[H_DATA_ROWS] = DATA_TOKENS, data.shape[0]
+def _ctrl(kind: int, tick: int, meta: Optional[StepMeta] = None):
+    if meta is None:
+        h = np.zeros(HEADER_LEN, dtype=np.int64)
+        h[0] = kind
+        p = np.zeros(0, dtype=np.int32)
     else:
-        h[H_DATA_KIND], h[H_DATA_ROWS], h[H_DATA_COLS] = DATA_HIDDEN, data.shape[0], data.shape[1]
-    return Message(header=h, payload=payload, data=data)
+        h, p = meta.pack()
+    h[H_TICK] = tick
+    return h, p
+
+
+def num_microbatches(world: int) -> int:
+    """M = N + 1 microbatches in flight: the head schedules microbatch m one full tick after
+    the tail returned its tokens, so no stage ever waits on the head's host (M = N would
+    put the head's token sync + scheduling on the critical path of every tick)."""
+    if world <= 1:
+        return 1
+    return int(os.environ.get("DLI_PP_MICROBATCHES", str(world + 1)))
 
 
 class StageWorker:
@@ -99,56 +102,56 @@ def _stage_capacity_blocks(cfg, plan, block_size, device, kv_fraction, cap_token
 
 
 class PipelineHead:
-    """Rank-0 driver: scheduler + ring ticks (M = N microbatches)."""
+    """Rank-0 driver: scheduler + tick loop over M = N + 1 microbatches.
 
-    def __init__(self, stage: StageWorker, transport, scheduler: Scheduler, tokenizer):
-        self.stage, self.tp, self.sched, self.tok = stage, transport, scheduler, tokenizer
-        self.N = transport.world
+    Tick k: take microbatch (k mod M)'s tokens of tick k - M (returned by the tail a tick
+    ago), update the scheduler, schedule its next step, broadcast that step's metadata on
+    the control plane, replay stage 0 and send the hidden state to stage 1, then post the
+    receive of this tick's tokens from the tail on a side stream."""
+
+    def __init__(self, stage: StageWorker, channel, scheduler: Scheduler, tokenizer,
+                 microbatches: Optional[int] = None):
+        self.stage, self.ch, self.sched, self.tok = stage, channel, scheduler, tokenizer
+        self.N = channel.world
+        self.M = microbatches or num_microbatches(self.N)
         self.stats = EngineStats()
 
     def run_session(self) -> List[RequestOutput]:
-        N, k = self.N, 0
-        inflight: Dict[int, Optional[StepMeta]] = {}
-        results: Dict[int, np.ndarray] = {}
+        N, M, k = self.N, self.M, 0
+        pending: Dict[int, tuple] = {}             # tick -> (meta, token handle)
         while True:
-            j = k - N
-            if j >= 0:
-                m = inflight.pop(j, None)
-                if m is not None:
-                    self.sched.update(m, results.pop(j))
-                    self.stats.tokens_out += m.num_seqs
-                else:
-                    results.pop(j, None)
-            live = any(v is not None for v in inflight.values())
-            meta = self.sched.schedule(k % N) if self.sched.has_work() else None
-            if meta is None and not live and not self.sched.has_work():
-                self.tp.exchange(_control(STOP, k), recv=(k - N + 1) >= 0)
-                break
-            t0 = time.perf_counter()
+            j = k - M
+            if j in pending:
+                m, h = pending.pop(j)
+                toks = h if isinstance(h, np.ndarray) else self.ch.tokens_to_host(h)
+                self.sched.update(m, toks)
+                self.stats.tokens_out += m.num_seqs
+            meta = self.sched.schedule(k % M) if self.sched.has_work() else None
             if meta is None:
-                msg = _control(EMPTY, k)
+                if not pending and not self.sched.has_work():
+                    break
+                k += 1
+                continue
+            t0 = time.perf_counter()
+            if N > 1:
+                self.ch.broadcast_ctrl(*_ctrl(meta.kind, k, meta))
+            out = self.stage.compute(meta, None)
+            if N == 1:
+                pending[k] = (meta, out.cpu().numpy())
             else:
-                hidden = self.stage.compute(meta, None)
-                msg = _msg_from(meta, hidden, k, tokens=False)
-                self.stats.steps += 1
-                if meta.kind == PREFILL:
-                    self.stats.prefill_steps += 1
-                    self.stats.prompt_tokens += meta.num_tokens
-                else:
-                    self.stats.decode_steps += 1
-            inflight[k] = meta
-            got = self.tp.exchange(msg, recv=(k - N + 1) >= 0)
-            if got is not None:
-                tick = int(got.header[H_TICK])
-                results[tick] = (got.data.cpu().numpy() if got.data is not None
-                                 else np.zeros(0, np.int32))
+                self.ch.send(out)
+                pending[k] = (meta, self.ch.irecv_tokens(meta.num_seqs))
+            self.stats.steps += 1
+            if meta.kind == PREFILL:
+                self.stats.prefill_steps += 1
+                self.stats.prompt_tokens += meta.num_tokens
+            else:
+                self.stats.decode_steps += 1
             self.stats.busy_s += time.perf_counter() - t0
             k += 1
-        # drain the ring until our STOP comes back from the tail
-        while True:
-            got = self.tp.exchange(None, recv=True)
-            if int(got.header[0]) == STOP:
-                break
+        if N > 1:
+            self.ch.broadcast_ctrl(*_ctrl(STOP, k))
+            self.ch.flush()
         outs = []
         for seq in self.sched.pop_finished():
             o = seq_to_output(seq, self.tok)
@@ -158,34 +161,32 @@ class PipelineHead:
         return outs
 
     def shutdown(self):
-        self.tp.exchange(_control(SHUTDOWN, -1), recv=False)
-        got = self.tp.exchange(None, recv=True)          # SHUTDOWN returns from the tail
-        assert int(got.header[0]) == SHUTDOWN
+        if self.N > 1:
+            self.ch.broadcast_ctrl(*_ctrl(SHUTDOWN, -1))
+            self.ch.flush()
 
 
-def run_stage_loop(stage: StageWorker, transport) -> None:
-    """Non-head ranks: serve sessions until SHUTDOWN."""
+def serve_session(stage: StageWorker, channel) -> int:
+    """Non-head rank: run every tick of one head session; returns STOP or SHUTDOWN.
+    The host never waits on this GPU: receive, replay and send are all stream-ordered."""
     while True:
-        msg = transport.exchange(None, recv=True)
-        while True:
-            kind = int(msg.header[0])
-            if kind in (STOP, SHUTDOWN):
-                transport.exchange(_control(kind, int(msg.header[H_TICK])), recv=False)
-                break
-            meta = StepMeta.unpack(msg.header, msg.payload)
-            out = stage.compute(meta, msg.data)
-            if stage.is_last:
-                # tail -> head: only the tokens (+ tick); the head still holds the metadata
-                tmeta = StepMeta(kind=meta.kind, seq_ids=[], microbatch=meta.microbatch,
-                                 step_id=meta.step_id)
-                send = _msg_from(tmeta, out, int(msg.header[H_TICK]), tokens=True)
-            elif out is None:
-                send = _msg_from(meta, None, int(msg.header[H_TICK]), tokens=False)
-            else:
-                send = _msg_from(meta, out, int(msg.header[H_TICK]), tokens=False)
-            msg = transport.exchange(send, recv=True)
-        if kind == SHUTDOWN:
-            return
+        h, p = channel.recv_ctrl()
+        kind = int(h[0])
+        if kind in (STOP, SHUTDOWN):
+            channel.flush()
+            return kind
+        if kind not in (PREFILL, DECODE):
+            continue
+        meta = StepMeta.unpack(h, p)
+        x = channel.recv_hidden(meta.num_tokens, stage.cfg.hidden_size)
+        out = stage.compute(meta, x)
+        channel.send(out)
+
+
+def run_stage_loop(stage: StageWorker, channel) -> None:
+    """Non-head ranks: serve sessions until SHUTDOWN."""
+    while serve_session(stage, channel) != SHUTDOWN:
+        pass
 
 
 # ------------------------------------------------------------------------------ builders
@@ -198,7 +199,7 @@ def build_stage(cfg: ModelConfig, rank: int, world: int, device, max_batch: int,
     table_width = -(-max_model_len // block_size)
     if num_blocks is None:
         cap = _stage_capacity_blocks(cfg, plan, block_size, device, kv_fraction,
-                                     cap_tokens=max(world * max_batch * max_model_len, 1 << 16))
+                                     cap_tokens=max((world + 1) * max_batch * max_model_len, 1 << 16))
         t = torch.tensor([cap], dtype=torch.int64,
                          device=device if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MIN)     # block ids are global: same pool size
@@ -222,15 +223,17 @@ class DistributedPipelineEngine:
         self.stage, self.plans, nb, tw = build_stage(
             self.cfg, self.rank, self.world, self.device, max_batch, max_model_len, block_size,
             policy=policy, seed=seed, use_graphs=use_graphs, num_blocks=num_blocks, dtype=dtype)
-        self.transport = TorchDistTransport(self.device, self.cfg.hidden_size, dtype=dtype)
+        self.channel = PipeChannel(self.device, dtype=dtype)
+        self.microbatches = num_microbatches(self.world)
         self.head = None
         if self.rank == 0:
             bm = BlockManager(nb, block_size)
             sched = Scheduler(bm, max_seqs_per_mb=max_batch, max_prefill_tokens=max_prefill_tokens,
-                              num_microbatches=self.world, eos_token_id=self.cfg.eos_token_id,
+                              num_microbatches=self.microbatches,
+                              eos_token_id=self.cfg.eos_token_id,
                               max_model_len=max_model_len, table_width=tw)
-            self.head = PipelineHead(self.stage, self.transport, sched,
-                                     load_tokenizer(self.cfg))
+            self.head = PipelineHead(self.stage, self.channel, sched, load_tokenizer(self.cfg),
+                                     self.microbatches)
         self._ids = 0
 
     def warmup(self):
@@ -251,7 +254,7 @@ class DistributedPipelineEngine:
 
     def serve(self):
         """Non-head ranks: block serving sessions until the head shuts the ring down."""
-        run_stage_loop(self.stage, self.transport)
+        run_stage_loop(self.stage, self.channel)
 
     def shutdown(self):
         if self.head is not None:
@@ -343,7 +346,7 @@ def bench_pipeline(args, world: int, rank: int, make_prompts):
     eng.warmup()
     sp = SamplingParams(max_length=args.max_length, temperature=0.8, top_k=50, top_p=0.95,
                         ignore_eos=True)
-    per_wave = args.batch * world                  # N microbatches of --batch requests
+    per_wave = args.batch * eng.microbatches       # M = N + 1 microbatches of --batch requests
 
     def wave(seed):
         if rank == 0:
@@ -382,19 +385,4 @@ def bench_pipeline(args, world: int, rank: int, make_prompts):
 
 def run_one_session(eng: DistributedPipelineEngine):
     """Serve exactly one head session on a non-head rank (bench lockstep)."""
-    tp, stage = eng.transport, eng.stage
-    msg = tp.exchange(None, recv=True)
-    while True:
-        kind = int(msg.header[0])
-        if kind in (STOP, SHUTDOWN):
-            tp.exchange(_control(kind, int(msg.header[H_TICK])), recv=False)
-            return
-        meta = StepMeta.unpack(msg.header, msg.payload)
-        out = stage.compute(meta, msg.data)
-        if stage.is_last:
-            tmeta = StepMeta(kind=meta.kind, seq_ids=[], microbatch=meta.microbatch,
-                             step_id=meta.step_id)
-            send = _msg_from(tmeta, out, int(msg.header[H_TICK]), tokens=True)
-        else:
-            send = _msg_from(meta, out, int(msg.header[H_TICK]), tokens=False)
-        msg = tp.exchange(send, recv=True)
+    serve_session(eng.stage, eng.channel)

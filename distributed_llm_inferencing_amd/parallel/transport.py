@@ -1,26 +1,27 @@
 """Inter-stage transport for the layer-sharded pipeline.
 
 The reference has NO inter-shard data plane (its "sharded" path runs shard 0 alone,
-``worker/app.py:334-336``). Here activations move between pipeline stages by RCCL
-point-to-point over xGMI (``torch.distributed`` backend "nccl" == RCCL on ROCm), or gloo
-on CPU for tests.
+``worker/app.py:334-336``). Here a pipeline step moves over two planes:
 
-Ring protocol. Every rank exchanges once per tick with a grouped
-``batch_isend_irecv({send msg_k -> next, recv msg_{k+1} <- prev})`` (two phases: a fixed
-size control message, then the data tensor whose shape the control message announced).
-With M = N microbatches in flight, rank r's exchange at tick k pairs only with exchanges
-on the same anti-diagonal r + k (including the tail -> head token return edge), so the
-schedule is deadlock-free by construction regardless of how the backend progresses sends.
+* control plane (host): the head's packed ``StepMeta`` for every tick goes to every other
+  stage over a separate **gloo** process group (TCP loopback, CPU tensors) the moment the
+  head schedules it, so a stage's host can stage the metadata upload and enqueue its graph
+  replay long before the activations arrive — no stage ever waits on its GPU to learn what
+  to do next;
+* data plane (device): hidden states stage r -> r+1 and sampled token ids tail -> head go by
+  RCCL point-to-point over xGMI (``torch.distributed`` backend "nccl" == RCCL on ROCm),
+  ordered on the GPU streams: the receive is a stream dependency of the consumer's graph
+  replay, never a host wait. On CPU (tests) the data plane is gloo as well.
 
-Message = (ctrl int32[CTRL_WORDS], data tensor). ctrl = 16 int64 header words (as 32
-int32) + the packed StepMeta payload inline (up to CTRL_MAX words; larger payloads ride in
-phase 2 ahead of the data).
+Every stage learns the activation shape of tick k from tick k's metadata (rows = tokens of
+the step, cols = hidden size), so the data plane carries no headers at all. Sends and
+receives between a pair of ranks are posted in the same (tick) order on both sides.
 """
 from __future__ import annotations
 
 import os
-from dataclasses import dataclass
-from typing import List, Optional
+from collections import deque
+from typing import Optional, Tuple
 
 import numpy as np
 import torch
@@ -30,25 +31,34 @@ from ..engine.batch import HEADER_LEN
 from ..utils import faults
 from ..utils.tracing import trace_range
 
-HDR32 = 2 * HEADER_LEN
-CTRL_MAX = int(os.environ.get("DLI_CTRL_MAX_WORDS", str(24 * 1024)))
-CTRL_WORDS = HDR32 + CTRL_MAX
-
 # header word indices (int64 units) beyond StepMeta's own first 8
-H_DATA_KIND, H_DATA_ROWS, H_DATA_COLS, H_INLINE, H_TICK = 8, 9, 10, 11, 12
-DATA_NONE, DATA_HIDDEN, DATA_TOKENS = 0, 1, 2
+H_TICK = 12
 
 
-@dataclass
-class Message:
-    header: np.ndarray                 # int64[HEADER_LEN]
-    payload: np.ndarray                # int32[n]
-    data: Optional[torch.Tensor]       # bf16 [rows, D] or int32 [S]
+class PipeChannel:
+    """Control + data planes of one pipeline rank (default process group = the stages)."""
 
-
-class Transport:
-    rank: int
-    world: int
+    def __init__(self, device: torch.device, dtype=torch.bfloat16, max_pending: int = 8):
+        self.rank = dist.get_rank()
+        self.world = dist.get_world_size()
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.nccl = dist.get_backend() == "nccl"
+        # collective over all ranks, same order everywhere (called once per engine)
+        self.ctrl_group = dist.new_group(backend="gloo")
+        # one communicator per data edge (r -> r+1, and tail -> head): RCCL serialises the
+        # operations of one communicator on one stream, so sharing a communicator would
+        # queue the head's next send behind its wait for the tail's tokens
+        edges = [dist.new_group([r, r + 1]) for r in range(self.world - 1)]
+        ret = dist.new_group([0, self.world - 1]) if self.world > 1 else None
+        self.out_group = (edges[self.rank] if self.rank < self.world - 1 else ret)
+        self.in_group = edges[self.rank - 1] if self.rank > 0 else ret
+        self.data_device = self.device if self.nccl else torch.device("cpu")
+        self._sends = deque()
+        self._ctrl_sends = deque()
+        self.max_pending = max_pending
+        self.recv_stream = (torch.cuda.Stream(self.device)
+                            if self.nccl and self.device.type == "cuda" else None)
 
     @property
     def next(self) -> int:
@@ -58,106 +68,78 @@ class Transport:
     def prev(self) -> int:
         return (self.rank - 1) % self.world
 
-    def exchange(self, send: Optional[Message], recv: bool) -> Optional[Message]:
-        raise NotImplementedError
+    # ------------------------------------------------------------------ control plane
+    def broadcast_ctrl(self, header: np.ndarray, payload: np.ndarray) -> None:
+        """Head -> every other stage (asynchronous; buffers kept until delivered)."""
+        if faults.active():
+            faults.check("transport.exchange", tick=int(header[H_TICK]))
+        h = torch.from_numpy(np.ascontiguousarray(header, dtype=np.int64).copy())
+        h[4] = int(payload.shape[0])
+        p = torch.from_numpy(np.ascontiguousarray(payload, dtype=np.int32).copy())
+        with trace_range("pp.ctrl"):
+            for r in range(1, self.world):
+                self._ctrl_sends.append((dist.isend(h, r, group=self.ctrl_group), h))
+                if p.numel():
+                    self._ctrl_sends.append((dist.isend(p, r, group=self.ctrl_group), p))
+        while len(self._ctrl_sends) > 4 * self.world * 2:
+            w, _ = self._ctrl_sends.popleft()
+            w.wait()
 
-    def barrier(self):
-        pass
+    def recv_ctrl(self) -> Tuple[np.ndarray, np.ndarray]:
+        h = torch.empty(HEADER_LEN, dtype=torch.int64)
+        dist.recv(h, 0, group=self.ctrl_group)
+        n = int(h[4])
+        p = torch.empty(n, dtype=torch.int32)
+        if n:
+            dist.recv(p, 0, group=self.ctrl_group)
+        return h.numpy(), p.numpy()
 
+    # ------------------------------------------------------------------ data plane
+    def send(self, t: torch.Tensor) -> None:
+        """Asynchronous send of a snapshot of ``t`` (graph outputs are static buffers) to
+        the next stage, or from the tail back to the head."""
+        with trace_range("pp.send"):
+            snap = t.clone() if self.nccl else t.to("cpu")
+            w = dist.isend(snap.contiguous(), self.next, group=self.out_group)
+            self._sends.append((w, snap))
+        while len(self._sends) > self.max_pending:
+            w, _ = self._sends.popleft()
+            w.wait()
 
-class TorchDistTransport(Transport):
-    """Ring transport over an initialised torch.distributed process group."""
+    def recv_hidden(self, rows: int, cols: int) -> torch.Tensor:
+        """Receive stage input from the previous stage; on RCCL the wait is a stream
+        dependency of the replay that consumes it, not a host wait."""
+        with trace_range("pp.recv"):
+            buf = torch.empty(rows, cols, dtype=self.dtype, device=self.data_device)
+            dist.irecv(buf, self.prev, group=self.in_group).wait()
+        return buf if buf.device == self.device else buf.to(self.device)
 
-    def __init__(self, device: torch.device, hidden_size: int, dtype=torch.bfloat16,
-                 group=None):
-        self.rank = dist.get_rank(group)
-        self.world = dist.get_world_size(group)
-        self.group = group
-        self.device = device
-        self.hidden = hidden_size
-        self.dtype = dtype
-        self.comm_device = device if dist.get_backend(group) == "nccl" else torch.device("cpu")
-        self._ctrl_send = torch.zeros(CTRL_WORDS, dtype=torch.int32, device=self.comm_device)
-        self._ctrl_recv = torch.zeros(CTRL_WORDS, dtype=torch.int32, device=self.comm_device)
-        self._ctrl_host = torch.zeros(CTRL_WORDS, dtype=torch.int32).pin_memory() \
-            if self.comm_device.type == "cuda" else None
+    def irecv_tokens(self, n: int):
+        """Post the head's receive of a tick's sampled ids from the tail, on a side stream
+        so the next replay does not depend on it (returns a handle)."""
+        if self.recv_stream is not None:
+            with torch.cuda.stream(self.recv_stream):
+                buf = torch.empty(n, dtype=torch.int32, device=self.device)
+                dist.irecv(buf, self.prev, group=self.in_group).wait()
+            return buf, None
+        buf = torch.empty(n, dtype=torch.int32)
+        return buf, dist.irecv(buf, self.prev, group=self.in_group)
 
-    def _peer(self, r):
-        return dist.get_global_rank(self.group, r) if self.group is not None else r
+    def tokens_to_host(self, handle) -> np.ndarray:
+        buf, work = handle
+        if self.recv_stream is not None:
+            with torch.cuda.stream(self.recv_stream):
+                return buf.cpu().numpy()
+        work.wait()
+        return buf.numpy()
 
-    def _run(self, ops):
-        if not ops:
-            return
-        reqs = dist.batch_isend_irecv(ops)
-        for r in reqs:
-            r.wait()
-
-    def exchange(self, send: Optional[Message], recv: bool) -> Optional[Message]:
-        if send is not None and faults.active():
-            faults.check("transport.exchange", tick=int(send.header[H_TICK]))
-        with trace_range("pp.exchange"):
-            return self._exchange(send, recv)
-
-    def _exchange(self, send: Optional[Message], recv: bool) -> Optional[Message]:
-        nxt, prv = self._peer(self.next), self._peer(self.prev)
-        # ---- phase 1: control words
-        ops = []
-        if send is not None:
-            hdr = send.header.copy()
-            inline = send.payload.shape[0] <= CTRL_MAX
-            hdr[H_INLINE] = 1 if inline else 0
-            words = np.zeros(CTRL_WORDS, dtype=np.int32)
-            words[:HDR32] = hdr.view(np.int32)
-            if inline:
-                words[HDR32:HDR32 + send.payload.shape[0]] = send.payload
-            self._ctrl_send.copy_(torch.from_numpy(words))
-            ops.append(dist.P2POp(dist.isend, self._ctrl_send, nxt, self.group))
-        if recv:
-            ops.append(dist.P2POp(dist.irecv, self._ctrl_recv, prv, self.group))
-        self._run(ops)
-        got = None
-        if recv:
-            if self._ctrl_host is not None:
-                self._ctrl_host.copy_(self._ctrl_recv)
-                words = self._ctrl_host.numpy().copy()
-            else:
-                words = self._ctrl_recv.numpy().copy()
-            rh = words[:HDR32].view(np.int64).copy()
-            got = rh
-        # ---- phase 2: overflow payload + data
-        ops = []
-        if send is not None:
-            if send.payload.shape[0] > CTRL_MAX:
-                pl = torch.from_numpy(send.payload).to(self.comm_device)
-                ops.append(dist.P2POp(dist.isend, pl, nxt, self.group))
-            if send.data is not None and send.data.numel() > 0:
-                d = send.data if send.data.device == self.comm_device else send.data.to(self.comm_device)
-                ops.append(dist.P2POp(dist.isend, d.contiguous(), nxt, self.group))
-        rpl = rdata = None
-        if recv:
-            n_pl = int(got[4])
-            if not got[H_INLINE]:
-                rpl = torch.empty(n_pl, dtype=torch.int32, device=self.comm_device)
-                ops.append(dist.P2POp(dist.irecv, rpl, prv, self.group))
-            kind, rows, cols = int(got[H_DATA_KIND]), int(got[H_DATA_ROWS]), int(got[H_DATA_COLS])
-            if kind == DATA_HIDDEN and rows > 0:
-                rdata = torch.empty(rows, cols, dtype=self.dtype, device=self.comm_device)
-            elif kind == DATA_TOKENS and rows > 0:
-                rdata = torch.empty(rows, dtype=torch.int32, device=self.comm_device)
-            if rdata is not None:
-                ops.append(dist.P2POp(dist.irecv, rdata, prv, self.group))
-        self._run(ops)
-        if not recv:
-            return None
-        n_pl = int(got[4])
-        payload = (words[HDR32:HDR32 + n_pl].copy() if got[H_INLINE]
-                   else rpl.cpu().numpy())
-        if rdata is not None and rdata.device != self.device:
-            rdata = rdata.to(self.device)
-        return Message(header=got, payload=payload, data=rdata)
-
-    def barrier(self):
-        dist.barrier(self.group)
+    def flush(self) -> None:
+        while self._sends:
+            w, _ = self._sends.popleft()
+            w.wait()
+        while self._ctrl_sends:
+            w, _ = self._ctrl_sends.popleft()
+            w.wait()
 
 
 def init_distributed(backend: Optional[str] = None, device: Optional[torch.device] = None):

@@ -36,5 +36,11 @@ for s in "$@"; do
     ep2) step ep2 900 env DLI_DIST_BACKEND=gloo DLI_SAME_DEVICE=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29535 bench.py --model mixtral-8x7b --gpus 2 --steps 1 --warmup 1 --batch 32 ;;
     llama70) step llama70 1100 python bench.py --model llama3-70b --steps 1 --warmup 1 --batch 64 ;;
     bench_small) step bench_small 600 python bench.py --steps 2 --warmup 1 --batch 64 ;;
+    sweep) for b in 128 384 512 768; do
+             step sweep_b$b 600 python bench.py --steps 2 --warmup 1 --batch $b
+           done ;;
+    llama70b) for b in 128 256; do
+             step llama70_b$b 900 python bench.py --model llama3-70b --steps 1 --warmup 1 --batch $b
+           done ;;
   esac
 done
