@@ -161,9 +161,13 @@ class StageRunner:
 
     def autotune(self, buckets=None):
         from ..ops import gemm as G
+        log = None
+        if os.environ.get("DLI_GEMM_AUTOTUNE_LOG", "0") == "1":
+            import sys
+            log = lambda m: print(m, file=sys.stderr, flush=True)  # noqa: E731
         for b in (buckets or self.buckets):
             shapes, weights = self.gemm_shapes(b)
-            G.autotune(shapes, weights, self.device)
+            G.autotune(shapes, weights, self.device, log=log)
 
     def capture(self, buckets=None):
         """Warm up and capture decode graphs for the given buckets (default: all)."""

@@ -110,7 +110,7 @@ def _gemm_native(x, w, epi: str, bias=None, out=None, plan: Optional[G.GemmPlan]
         out = torch.empty(M, out_n, dtype=dt, device=x.device)
     if plan.backend == "hipblaslt" and group_off is None:
         # plain library GEMM (hipBLASLt) + our epilogue kernel as a separate pass
-        if epi == "none":
+        if epi in ("none", "splitk"):
             torch.matmul(x, w.t(), out=out)
             return out
         y = torch.matmul(x, w.t())

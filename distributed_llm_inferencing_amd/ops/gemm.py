@@ -107,9 +107,16 @@ def clear_plans() -> None:
     _plan_cache.clear()
 
 
-def autotune(shapes, weights: dict, device, iters: int = 8, log=None) -> dict:
+def autotune(shapes, weights: dict, device, iters: int = 6, log=None,
+             cold_bytes: int = 1 << 30) -> dict:
     """Measure every candidate plan for each (M, N, K, epi) and pin the fastest
     ("measure, don't guess"). ``weights[(N, K)]`` is a real [N, K] weight of that shape.
+
+    Measured the way a decode step sees it: the weight is COLD (each call reads a different
+    copy; the copies together exceed the 256 MB Infinity Cache — timing one warm weight
+    picked plans that ran 12 % slower in the model), and split-K plans pay their slab
+    reduction (a "splitk" GEMM feeds a fused reduce that reads every slab). A non-split
+    winner for a "splitk" shape also becomes that shape's plain plan (unfused path).
     Returns {shape: (plan, ms)}."""
     from .. import ops  # local import: ops imports this module
     out = {}
@@ -117,22 +124,31 @@ def autotune(shapes, weights: dict, device, iters: int = 8, log=None) -> dict:
         key = (_bucket(M), N, K, epi)
         if key in _tuned:
             continue
-        w = weights[(N, K)]
-        x = (torch.randn(M, K, device=device) * 0.5).to(w.dtype)
+        w0 = weights[(N, K)]
+        n_copies = max(2, min(16, -(-cold_bytes // (w0.numel() * w0.element_size()))))
+        ws_ = [w0] + [w0.clone() for _ in range(n_copies - 1)]
+        x = (torch.randn(M, K, device=device) * 0.5).to(w0.dtype)
         best = None
         for p in candidate_plans(M, N, K, epi):
-            if p.backend == "hipblaslt" and epi != "none":
+            if p.backend == "hipblaslt" and epi not in ("none", "splitk"):
                 continue
+
+            def run(p=p):
+                for w in ws_:
+                    ops._gemm_native(x, w, epi, plan=p)
             try:
-                ms = ops.benchmark(lambda p=p: ops._gemm_native(x, w, epi, plan=p),
-                                   iters=iters, warmup=2)
+                ms = ops.benchmark(run, iters=iters, warmup=1) / len(ws_)
             except Exception:  # noqa: BLE001 — an invalid candidate is skipped
                 continue
             if best is None or ms < best[1]:
                 best = (p, ms)
+        del ws_
         if best is not None:
             _plan_cache[key] = best[0]
             _tuned.add(key)
+            if epi == "splitk" and (best[0].splits == 1 or best[0].backend != "dli"):
+                _plan_cache[(_bucket(M), N, K, "none")] = best[0]
+                _tuned.add((_bucket(M), N, K, "none"))
             out[(M, N, K, epi)] = best
             if log:
                 log(f"[gemm autotune] M={M} N={N} K={K} {epi}: {best[0]} {best[1]*1e3:.1f} us")
@@ -152,12 +168,10 @@ def candidate_plans(M: int, N: int, K: int, epi: str):
         for splits in (1, 2, 4, 8):
             if K % (64 * splits) or K // splits < 256:
                 continue
-            if epi == "splitk" and splits == 1:
-                continue
             tiles = -(-M // bm) * -(-N // bn)
             if splits > 1 and tiles * splits > 4 * NUM_CUS:
                 continue
             out.append(GemmPlan("dli", tile, splits))
-    if epi == "none":
+    if epi in ("none", "splitk"):
         out.append(GemmPlan("hipblaslt", 0, 1))
     return out

@@ -36,6 +36,9 @@ for s in "$@"; do
     ep2) step ep2 900 env DLI_DIST_BACKEND=gloo DLI_SAME_DEVICE=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29535 bench.py --model mixtral-8x7b --gpus 2 --steps 1 --warmup 1 --batch 32 ;;
     llama70) step llama70 1100 python bench.py --model llama3-70b --steps 1 --warmup 1 --batch 64 ;;
     bench_small) step bench_small 600 python bench.py --steps 2 --warmup 1 --batch 64 ;;
+    tune) step tune_off 600 python bench.py --steps 2 --warmup 1
+          step tune_on 900 env DLI_GEMM_AUTOTUNE=1 DLI_GEMM_AUTOTUNE_LOG=1 python bench.py --steps 2 --warmup 1
+          step tune_on256 900 env DLI_GEMM_AUTOTUNE=1 python bench.py --steps 2 --warmup 1 --batch 256 ;;
     sweep) for b in 128 384 512 768; do
              step sweep_b$b 600 python bench.py --steps 2 --warmup 1 --batch $b
            done ;;
