@@ -80,6 +80,11 @@ def _heuristic(M: int, N: int, K: int, epi: str) -> GemmPlan:
 
 
 def _bucket(M: int) -> int:
+    """Plan-cache key for M: exact up to 1024 rows (decode graph buckets are a fixed small
+    set and their best plans differ: one plan per power of two let M=320's plan run M=512),
+    power-of-two above (prefill)."""
+    if M <= 1024:
+        return M
     b = 1
     while b < M:
         b <<= 1
