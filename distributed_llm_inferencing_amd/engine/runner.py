@@ -173,10 +173,10 @@ class StageRunner:
         """Warm up and capture decode graphs for the given buckets (default: all)."""
         if not self.use_graphs:
             return
-        # Off by default: measured in-situ on MI355X, plans picked by isolated microbenchmarks
-        # ran the full 8B decode 12 % SLOWER than the fitted heuristic (warm-L2 / clock bias of
-        # back-to-back timing); kept as an opt-in tool for new shapes.
-        if os.environ.get("DLI_GEMM_AUTOTUNE", "0") == "1":
+        # Measured in-situ on MI355X (Llama-3-8B decode): cold-weight autotune at capture is
+        # +2.6 % at batch 512 and +12 % at batch 256 over the fitted heuristic, for ~5 s of
+        # startup (profiles/r1_final/autotune_ab.txt). DLI_GEMM_AUTOTUNE=0 turns it off.
+        if os.environ.get("DLI_GEMM_AUTOTUNE", "1") == "1":
             self.autotune(buckets)
         for b in (buckets or self.buckets):
             if b in self.graphs:

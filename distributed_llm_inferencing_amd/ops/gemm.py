@@ -8,7 +8,8 @@ The projection GEMMs of a decode step are skinny (M = batch) and of a prefill st
   GEMM at M = 256': choose SPLITK so that tiles * SPLITK ~ 0.5-1x the CU count),
 * the backend. Fused epilogues (SiLU*mul, bias+GELU, fp32 logits) always run on our kernel.
   Plain bf16 GEMMs may run on hipBLASLt (torch.matmul) if the autotuner measured it
-  faster on this shape (``DLI_GEMM_AUTOTUNE=1``), or if forced with ``DLI_GEMM_BACKEND``.
+  faster on this shape (autotune at graph capture, on by default; ``DLI_GEMM_AUTOTUNE=0``
+  disables it), or if forced with ``DLI_GEMM_BACKEND``.
 
 Split-K partial slabs live in a grow-only per-device workspace; engines warm every shape
 up before hipGraph capture so no allocation happens inside a capture.

@@ -29,7 +29,10 @@ def test_gpu_logits_close_to_hf_fp32(gpu, name):
 
 
 @pytest.mark.parametrize("name", ["llama-tiny", "gpt2-tiny", "mixtral-tiny"])
-def test_graph_decode_equals_eager(gpu, name):
+def test_graph_decode_equals_eager(gpu, name, monkeypatch):
+    # same GEMM plans on both sides (capture would otherwise autotune between the runs and
+    # change split-K summation order)
+    monkeypatch.setenv("DLI_GEMM_AUTOTUNE", "0")
     prompts = [IDS[:5], IDS[:9], IDS[3:14], IDS[:2]]
     sp = SamplingParams(max_length=40, temperature=0.8, top_k=50, top_p=0.95, seed=123,
                         ignore_eos=True)
