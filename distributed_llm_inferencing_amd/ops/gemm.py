@@ -24,7 +24,7 @@ import torch
 
 TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256), 4: (256, 128)}
 # "splitk": a plain GEMM whose fp32 partial slabs feed a fused reduce (ops.linear_add_rmsnorm,
-# ops.linear_rope_cache); planned/tuned separately, only split-K >= 2 candidates qualify.
+# ops.linear_rope_cache); planned/tuned separately (a non-split winner runs unfused).
 EPI = {"none": 0, "f32": 1, "silu_mul": 2, "bias_gelu": 3, "bias": 4, "splitk": 0}
 NUM_CUS = int(os.environ.get("DLI_NUM_CUS", "256"))
 
@@ -136,7 +136,7 @@ def autotune(shapes, weights: dict, device, iters: int = 6, log=None,
         x = (torch.randn(M, K, device=device) * 0.5).to(w0.dtype)
         best = None
         for p in candidate_plans(M, N, K, epi):
-            if p.backend == "hipblaslt" and epi not in ("none", "splitk"):
+            if p.backend == "hipblaslt" and epi not in ("none", "splitk", "silu_mul"):
                 continue
 
             def run(p=p):
@@ -178,6 +178,6 @@ def candidate_plans(M: int, N: int, K: int, epi: str):
             if splits > 1 and tiles * splits > 4 * NUM_CUS:
                 continue
             out.append(GemmPlan("dli", tile, splits))
-    if epi in ("none", "splitk"):
+    if epi in ("none", "splitk", "silu_mul"):     # silu_mul: + our SiLU*up pass
         out.append(GemmPlan("hipblaslt", 0, 1))
     return out
