@@ -113,14 +113,15 @@ def _gemm_native(x, w, epi: str, bias=None, out=None, plan: Optional[G.GemmPlan]
         if epi in ("none", "splitk"):
             torch.matmul(x, w.t(), out=out)
             return out
+        if epi == "f32":           # hipBLASLt bf16 x bf16 -> fp32 output (LM head logits)
+            torch.mm(x, w.t(), out_dtype=torch.float32, out=out)
+            return out
         y = torch.matmul(x, w.t())
         if epi == "silu_mul":
             _native_call("dli_silu_mul", _p(out), _p(y), M, out_n, _st())
         elif epi in ("bias", "bias_gelu"):
             _native_call("dli_bias_act", _p(y), _p(bias), M, Nn, 1 if epi == "bias_gelu" else 0,
                          _st())
-            out.copy_(y)
-        else:  # f32
             out.copy_(y)
         return out
     splits = plan.splits if group_off is None else 1

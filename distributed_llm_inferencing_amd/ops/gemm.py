@@ -136,7 +136,7 @@ def autotune(shapes, weights: dict, device, iters: int = 6, log=None,
         x = (torch.randn(M, K, device=device) * 0.5).to(w0.dtype)
         best = None
         for p in candidate_plans(M, N, K, epi):
-            if p.backend == "hipblaslt" and epi not in ("none", "splitk", "silu_mul"):
+            if p.backend == "hipblaslt" and epi not in ("none", "splitk", "silu_mul", "f32"):
                 continue
 
             def run(p=p):
@@ -178,6 +178,6 @@ def candidate_plans(M: int, N: int, K: int, epi: str):
             if splits > 1 and tiles * splits > 4 * NUM_CUS:
                 continue
             out.append(GemmPlan("dli", tile, splits))
-    if epi in ("none", "splitk", "silu_mul"):     # silu_mul: + our SiLU*up pass
+    if epi in ("none", "splitk", "silu_mul", "f32"):   # silu_mul: + our SiLU*up pass
         out.append(GemmPlan("hipblaslt", 0, 1))
     return out

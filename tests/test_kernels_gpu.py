@@ -107,6 +107,11 @@ def test_gemm_epilogues(gpu, epi, M, N, K):
             close(out, ref, rtol=2e-2, atol=2e-2)
             if epi == "f32":
                 assert out.dtype == torch.float32
+    # hipBLASLt plan (autotune candidate) + our epilogue pass
+    out = ops._gemm_native(x, w, epi, bias=b if "bias" in epi else None,
+                           plan=G.GemmPlan("hipblaslt", 0, 1))
+    close(out, ref, rtol=2e-2, atol=2e-2)
+    assert out.dtype == (torch.float32 if epi == "f32" else BF)
 
 
 @pytest.mark.parametrize("M,N,K", [(3, 512, 1024), (256, 4096, 4096), (77, 4096, 14336)])
