@@ -45,7 +45,14 @@ __device__ __forceinline__ void store_pair_or_one(void* C, int ldc, int row, int
   }
 }
 
-template <int BM, int BN, int EPI>
+// s_waitcnt vmcnt(N) with expcnt/lgkmcnt left at their maxima (gfx9 encoding)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+template <int BM, int BN, int EPI, int NS>
 __global__ void __launch_bounds__(GEMM_THREADS) gemm_bf16_kernel(
     const u16* __restrict__ A, int lda, const u16* __restrict__ W, int ldw,
     void* __restrict__ C, int ldc, int M, int N, int K, int k_split_len,
@@ -122,13 +129,8 @@ __global__ void __launch_bounds__(GEMM_THREADS) gemm_bf16_kernel(
 #pragma unroll
   for (int j = 0; j < NI; ++j) w_row[j] = wn * (BN / 2) + j * 16 + fr;
 
-  if (nk > 0) stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
-    const char* abuf = smem + cur * BUF;
+  auto compute = [&](int buf) {
+    const char* abuf = smem + buf * BUF;
     const char* wbuf = abuf + A_BYTES;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -150,8 +152,39 @@ __global__ void __launch_bounds__(GEMM_THREADS) gemm_bf16_kernel(
         for (int j = 0; j < NI; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
+  };
+
+  if (NS == 2) {
+    // 2 LDS buffers: the next tile's DMA overlaps this tile's MFMAs; drained every K-step
+    if (nk > 0) stage(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
+      compute(cur);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  } else {
+    // 3 LDS buffers, one tile kept in flight ACROSS the barrier (cdna_hip_programming.md §5
+    // 'Pipelining across barriers'): counted vmcnt retires tile kt only, then a raw
+    // s_barrier (a __syncthreads() would emit vmcnt(0) and drain the DMA); the restaged
+    // buffer (kt+2)%3 was last read in iteration kt-1, which every wave has finished.
+    constexpr int INSTR = A_INSTR + W_INSTR;
+    if (nk > 0) stage(0, 0);
+    if (nk > 1) stage(1, 1);
+    int cur = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) wait_vmcnt<INSTR>();
+      else wait_vmcnt<0>();
+      __builtin_amdgcn_s_waitcnt(0xC07F);          // lgkmcnt(0)
+      __builtin_amdgcn_s_barrier();
+      if (kt + 2 < nk) stage(cur == 0 ? 2 : cur - 1, kt + 2);
+      compute(cur);
+      cur = (cur == 2) ? 0 : cur + 1;
+    }
+    wait_vmcnt<0>();
   }
 
   // ---- epilogue. acc[i][j][r] = C[m0 + wm*BM/2 + 16i + 4fq + r][n0 + wn*BN/2 + 16j + fr]
@@ -229,7 +262,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(void* __restrict__ C
   }
 }
 
-template <int BM, int BN, int EPI>
+template <int BM, int BN, int EPI, int NS>
 static int launch_cfg(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M,
                       int N, int K, int splits, const void* bias, void* ws,
                       const int* group_off, int groups, hipStream_t st) {
@@ -237,15 +270,15 @@ static int launch_cfg(const void* A, int lda, const void* W, int ldw, void* C, i
   int ksl = K / splits;
   ksl = (ksl / BK) * BK;
   if (ksl * splits != K) return (int)hipErrorInvalidValue;
-  const size_t lds = 2 * (size_t)(BM + BN) * BK * 2;
+  const size_t lds = NS * (size_t)(BM + BN) * BK * 2;
   static bool attr_done = false;                   // > 64 KiB dynamic LDS needs the opt-in
   if (!attr_done) {
-    hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, EPI>,
+    hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, EPI, NS>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_done = true;
   }
   dim3 grid(tiles, splits, groups);
-  gemm_bf16_kernel<BM, BN, EPI><<<grid, GEMM_THREADS, lds, st>>>(
+  gemm_bf16_kernel<BM, BN, EPI, NS><<<grid, GEMM_THREADS, lds, st>>>(
       (const u16*)A, lda, (const u16*)W, ldw, C, ldc, M, N, K, ksl, (const u16*)bias,
       (float*)ws, group_off);
   if (splits > 1 && C != nullptr) {       // C == nullptr: leave the fp32 partial slabs for a
@@ -262,16 +295,20 @@ static int dispatch_tile(int tile_cfg, const void* A, int lda, const void* W, in
                          int ldc, int M, int N, int K, int splits, const void* bias, void* ws,
                          const int* go, int groups, hipStream_t st) {
   switch (tile_cfg) {
-    case 0: return launch_cfg<64, 64, EPI>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
-    case 1: return launch_cfg<64, 128, EPI>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
-    case 2: return launch_cfg<128, 128, EPI>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
-    case 3: return launch_cfg<128, 256, EPI>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
-    case 4: return launch_cfg<256, 128, EPI>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
+#define DLI_CFG(id, bm, bn, ns) \
+    case id: return launch_cfg<bm, bn, EPI, ns>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
+    DLI_CFG(0, 64, 64, 2) DLI_CFG(1, 64, 128, 2) DLI_CFG(2, 128, 128, 2) DLI_CFG(3, 128, 256, 2)
+    DLI_CFG(4, 256, 128, 2)
+    DLI_CFG(5, 64, 64, 3) DLI_CFG(6, 64, 128, 3) DLI_CFG(7, 128, 128, 3) DLI_CFG(8, 128, 256, 3)
+    DLI_CFG(9, 256, 128, 3)
+#undef DLI_CFG
     default: return (int)hipErrorInvalidValue;
   }
 }
 
-// tile_cfg: 0=64x64 1=64x128 2=128x128 3=128x256 4=256x128. ws: fp32 [splits, M, N] when splits>1.
+// tile_cfg: 0=64x64 1=64x128 2=128x128 3=128x256 4=256x128 (2 LDS stages); 5..9 = the same
+// tiles with 3 LDS stages (one tile in flight across the barrier). ws: fp32 [splits, M, N]
+// when splits>1.
 // group_off (nullable): int[groups+1] row offsets; M is then the max rows of any group.
 extern "C" int dli_gemm(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M,
                         int N, int K, int epi, int tile_cfg, int splits, const void* bias,

@@ -22,7 +22,10 @@ from dataclasses import dataclass
 
 import torch
 
-TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256), 4: (256, 128)}
+# tile id -> (BM, BN); 0-4 stage K through 2 LDS buffers, 5-9 are the same tiles with 3
+# buffers and one tile kept in flight across the K-step barrier (gemm.hip)
+TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256), 4: (256, 128),
+         5: (64, 64), 6: (64, 128), 7: (128, 128), 8: (128, 256), 9: (256, 128)}
 # "splitk": a plain GEMM whose fp32 partial slabs feed a fused reduce (ops.linear_add_rmsnorm,
 # ops.linear_rope_cache); planned/tuned separately (a non-split winner runs unfused).
 EPI = {"none": 0, "f32": 1, "silu_mul": 2, "bias_gelu": 3, "bias": 4, "splitk": 0}
