@@ -1,23 +1,48 @@
 #!/usr/bin/env python3
-"""Summarise a rocprofv3 --kernel-trace --stats CSV directory: top kernels + GPU busy time."""
+"""Summarise a rocprofv3 --kernel-trace --stats CSV directory: top kernels + GPU busy time.
+
+    prof_summary.py <dir> [top_n] [--tail-ms T]
+
+--tail-ms T restricts everything to kernels that started in the last T ms of the trace
+(e.g. the timed wave of bench.py, excluding autotune and graph-capture warmup), computed
+from the kernel trace instead of the stats file."""
+import argparse
 import csv
-import sys
+from collections import defaultdict
 from pathlib import Path
 
-d = Path(sys.argv[1])
-stats = next(d.glob("*kernel_stats.csv"))
-rows = list(csv.DictReader(open(stats)))
+ap = argparse.ArgumentParser()
+ap.add_argument("dir")
+ap.add_argument("top", nargs="?", type=int, default=25)
+ap.add_argument("--tail-ms", type=float, default=None)
+a = ap.parse_args()
+d = Path(a.dir)
+tr = list(d.glob("*kernel_trace.csv"))
+ev = []
+if tr:
+    ev = sorted((int(x["Start_Timestamp"]), int(x["End_Timestamp"]), x["Kernel_Name"])
+                for x in csv.DictReader(open(tr[0])))
+if a.tail_ms is not None and ev:
+    t_end = ev[-1][1]
+    ev = [e for e in ev if e[0] >= t_end - a.tail_ms * 1e6]
+    agg = defaultdict(lambda: [0, 0])
+    for s, e, n in ev:
+        agg[n][0] += e - s
+        agg[n][1] += 1
+    rows = [{"Name": n, "TotalDurationNs": v[0], "Calls": v[1], "AverageNs": v[0] / v[1]}
+            for n, v in agg.items()]
+else:
+    stats = next(d.glob("*kernel_stats.csv"))
+    rows = list(csv.DictReader(open(stats)))
 tot = sum(float(r["TotalDurationNs"]) for r in rows)
 print(f"{'ms':>9} {'%':>5} {'calls':>7} {'avg_us':>8}  kernel")
-for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:int(sys.argv[2]) if len(sys.argv) > 2 else 25]:
+for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:a.top]:
     print(f"{float(r['TotalDurationNs'])/1e6:9.2f} {100*float(r['TotalDurationNs'])/tot:5.1f} "
           f"{r['Calls']:>7} {float(r['AverageNs'])/1e3:8.1f}  {r['Name'][:100]}")
 print(f"total kernel ms {tot/1e6:.1f}")
-tr = list(d.glob("*kernel_trace.csv"))
-if tr:
-    ev = sorted((int(x["Start_Timestamp"]), int(x["End_Timestamp"])) for x in csv.DictReader(open(tr[0])))
+if ev:
     busy, cur_s, cur_e = 0, None, None
-    for s, e in ev:
+    for s, e, _ in ev:
         if cur_e is None or s > cur_e:
             if cur_e is not None:
                 busy += cur_e - cur_s
