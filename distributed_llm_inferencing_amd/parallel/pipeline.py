@@ -104,49 +104,61 @@ def _stage_capacity_blocks(cfg, plan, block_size, device, kv_fraction, cap_token
 class PipelineHead:
     """Rank-0 driver: scheduler + tick loop over M = N + 1 microbatches.
 
-    Tick k: take microbatch (k mod M)'s tokens of tick k - M (returned by the tail a tick
-    ago), update the scheduler, schedule its next step, broadcast that step's metadata on
-    the control plane, replay stage 0 and send the hidden state to stage 1, then post the
-    receive of this tick's tokens from the tail on a side stream."""
+    Tick k: consume the tokens of the microbatch started at tick k - M (they arrived in the
+    exchange of tick k - 1), schedule that microbatch's next step, broadcast its metadata
+    on the control plane, post this tick's exchange {hidden of tick k-1 -> stage 1, ids of
+    the microbatch started at k - N <- tail}, then replay stage 0 for tick k."""
 
     def __init__(self, stage: StageWorker, channel, scheduler: Scheduler, tokenizer,
                  microbatches: Optional[int] = None):
         self.stage, self.ch, self.sched, self.tok = stage, channel, scheduler, tokenizer
         self.N = channel.world
         self.M = microbatches or num_microbatches(self.N)
+        assert self.N == 1 or self.M > self.N, "need M > N microbatches"
         self.stats = EngineStats()
+
+    def _account(self, meta: StepMeta):
+        self.stats.steps += 1
+        if meta.kind == PREFILL:
+            self.stats.prefill_steps += 1
+            self.stats.prompt_tokens += meta.num_tokens
+        else:
+            self.stats.decode_steps += 1
 
     def run_session(self) -> List[RequestOutput]:
         N, M, k = self.N, self.M, 0
-        pending: Dict[int, tuple] = {}             # tick -> (meta, token handle)
+        started: Dict[int, StepMeta] = {}          # start tick -> meta awaiting its tokens
+        tokens: Dict[int, object] = {}             # start tick -> exchange handle / host ids
+        prev_out = None
         while True:
-            j = k - M
-            if j in pending:
-                m, h = pending.pop(j)
-                toks = h if isinstance(h, np.ndarray) else self.ch.tokens_to_host(h)
-                self.sched.update(m, toks)
+            t0 = time.perf_counter()
+            s = k - M
+            if s in started:
+                m = started.pop(s)
+                h = tokens.pop(s)
+                self.sched.update(m, h if isinstance(h, np.ndarray) else self.ch.to_host(h))
                 self.stats.tokens_out += m.num_seqs
             meta = self.sched.schedule(k % M) if self.sched.has_work() else None
-            if meta is None:
-                if not pending and not self.sched.has_work():
-                    break
+            if meta is None and not started and not self.sched.has_work():
+                break
+            if N == 1:
+                if meta is not None:
+                    out = self.stage.compute(meta, None)
+                    started[k], tokens[k] = meta, out.cpu().numpy()
+                    self._account(meta)
                 k += 1
                 continue
-            t0 = time.perf_counter()
-            if N > 1:
-                self.ch.broadcast_ctrl(*_ctrl(meta.kind, k, meta))
-            out = self.stage.compute(meta, None)
-            if N == 1:
-                pending[k] = (meta, out.cpu().numpy())
-            else:
-                self.ch.send(out)
-                pending[k] = (meta, self.ch.irecv_tokens(meta.num_seqs))
-            self.stats.steps += 1
-            if meta.kind == PREFILL:
-                self.stats.prefill_steps += 1
-                self.stats.prompt_tokens += meta.num_tokens
-            else:
-                self.stats.decode_steps += 1
+            self.ch.broadcast_ctrl(*_ctrl(EMPTY if meta is None else meta.kind, k, meta))
+            ret = started.get(k - N)
+            h = self.ch.exchange(prev_out, None if ret is None else (ret.num_seqs,),
+                                 torch.int32)
+            if ret is not None:
+                tokens[k - N] = h
+            prev_out = None
+            if meta is not None:
+                prev_out = self.stage.compute(meta, None)
+                started[k] = meta
+                self._account(meta)
             self.stats.busy_s += time.perf_counter() - t0
             k += 1
         if N > 1:
@@ -167,20 +179,27 @@ class PipelineHead:
 
 
 def serve_session(stage: StageWorker, channel) -> int:
-    """Non-head rank: run every tick of one head session; returns STOP or SHUTDOWN.
-    The host never waits on this GPU: receive, replay and send are all stream-ordered."""
+    """Non-head rank r: every tick of one head session; returns STOP or SHUTDOWN.
+    At tick k it runs the microbatch the head started at tick k - r (control message k - r,
+    received in order). The host never waits on this GPU: receive, replay and send are all
+    stream-ordered."""
+    r, k, prev_out = channel.rank, 0, None
     while True:
-        h, p = channel.recv_ctrl()
-        kind = int(h[0])
-        if kind in (STOP, SHUTDOWN):
-            channel.flush()
-            return kind
-        if kind not in (PREFILL, DECODE):
-            continue
-        meta = StepMeta.unpack(h, p)
-        x = channel.recv_hidden(meta.num_tokens, stage.cfg.hidden_size)
-        out = stage.compute(meta, x)
-        channel.send(out)
+        meta = None
+        if k >= r:
+            h, p = channel.recv_ctrl()
+            kind = int(h[0])
+            if kind in (STOP, SHUTDOWN):
+                channel.flush()
+                return kind
+            if kind in (PREFILL, DECODE):
+                meta = StepMeta.unpack(h, p)
+        rshape = None if meta is None else (meta.num_tokens, stage.cfg.hidden_size)
+        hd = channel.exchange(prev_out, rshape)
+        prev_out = None
+        if meta is not None:
+            prev_out = stage.compute(meta, channel.wait(hd))
+        k += 1
 
 
 def run_stage_loop(stage: StageWorker, channel) -> None:

@@ -9,18 +9,19 @@ The reference has NO inter-shard data plane (its "sharded" path runs shard 0 alo
   replay long before the activations arrive — no stage ever waits on its GPU to learn what
   to do next;
 * data plane (device): hidden states stage r -> r+1 and sampled token ids tail -> head go by
-  RCCL point-to-point over xGMI (``torch.distributed`` backend "nccl" == RCCL on ROCm),
-  ordered on the GPU streams: the receive is a stream dependency of the consumer's graph
-  replay, never a host wait. On CPU (tests) the data plane is gloo as well.
+  RCCL point-to-point over xGMI (``torch.distributed`` backend "nccl" == RCCL on ROCm), one
+  grouped send/recv per rank per tick, ordered on the GPU streams: the receive is a stream
+  dependency of the consumer's graph replay, never a host wait. On CPU (tests) the data
+  plane is gloo as well.
 
 Every stage learns the activation shape of tick k from tick k's metadata (rows = tokens of
-the step, cols = hidden size), so the data plane carries no headers at all. Sends and
-receives between a pair of ranks are posted in the same (tick) order on both sides.
+the step, cols = hidden size), so the data plane carries no headers at all.
 """
 from __future__ import annotations
 
 import os
 from collections import deque
+from datetime import timedelta
 from typing import Optional, Tuple
 
 import numpy as np
@@ -36,7 +37,16 @@ H_TICK = 12
 
 
 class PipeChannel:
-    """Control + data planes of one pipeline rank (default process group = the stages)."""
+    """Control + data planes of one pipeline rank (default process group = the stages).
+
+    Data plane: ONE grouped ``batch_isend_irecv`` per rank per tick on the default
+    communicator — {send my output of tick k-1 -> next, receive my input of tick k <- prev}
+    (the tail's output is the sampled ids, sent to the head). Rank r's group at tick k pairs
+    with rank r+1's and rank r-1's groups of the same tick (anti-diagonal schedule), so all
+    ranks exchange together and nothing can wait on a later tick: deadlock-free. One
+    communicator = one RCCL stream per rank: separate per-edge communicators would add
+    streams that HIP may alias onto the same hardware queue (GPU_MAX_HW_QUEUES=4), putting
+    a spinning receive in front of a send."""
 
     def __init__(self, device: torch.device, dtype=torch.bfloat16, max_pending: int = 8):
         self.rank = dist.get_rank()
@@ -44,20 +54,14 @@ class PipeChannel:
         self.device = torch.device(device)
         self.dtype = dtype
         self.nccl = dist.get_backend() == "nccl"
-        # collective over all ranks, same order everywhere (called once per engine)
-        self.ctrl_group = dist.new_group(backend="gloo")
-        # one communicator per data edge (r -> r+1, and tail -> head): RCCL serialises the
-        # operations of one communicator on one stream, so sharing a communicator would
-        # queue the head's next send behind its wait for the tail's tokens
-        edges = [dist.new_group([r, r + 1]) for r in range(self.world - 1)]
-        ret = dist.new_group([0, self.world - 1]) if self.world > 1 else None
-        self.out_group = (edges[self.rank] if self.rank < self.world - 1 else ret)
-        self.in_group = edges[self.rank - 1] if self.rank > 0 else ret
+        # collective over all ranks (called once per engine). Idle serving ranks block on
+        # the control plane between sessions: no timeout that could fire while idle.
+        self.ctrl_group = dist.new_group(backend="gloo", timeout=timedelta(days=365))
         self.data_device = self.device if self.nccl else torch.device("cpu")
-        self._sends = deque()
+        self._inflight = deque()
         self._ctrl_sends = deque()
         self.max_pending = max_pending
-        self.recv_stream = (torch.cuda.Stream(self.device)
+        self.side_stream = (torch.cuda.Stream(self.device)
                             if self.nccl and self.device.type == "cuda" else None)
 
     @property
@@ -81,7 +85,7 @@ class PipeChannel:
                 self._ctrl_sends.append((dist.isend(h, r, group=self.ctrl_group), h))
                 if p.numel():
                     self._ctrl_sends.append((dist.isend(p, r, group=self.ctrl_group), p))
-        while len(self._ctrl_sends) > 4 * self.world * 2:
+        while len(self._ctrl_sends) > 8 * self.world:
             w, _ = self._ctrl_sends.popleft()
             w.wait()
 
@@ -95,48 +99,58 @@ class PipeChannel:
         return h.numpy(), p.numpy()
 
     # ------------------------------------------------------------------ data plane
-    def send(self, t: torch.Tensor) -> None:
-        """Asynchronous send of a snapshot of ``t`` (graph outputs are static buffers) to
-        the next stage, or from the tail back to the head."""
-        with trace_range("pp.send"):
-            snap = t.clone() if self.nccl else t.to("cpu")
-            w = dist.isend(snap.contiguous(), self.next, group=self.out_group)
-            self._sends.append((w, snap))
-        while len(self._sends) > self.max_pending:
-            w, _ = self._sends.popleft()
-            w.wait()
+    def exchange(self, send: Optional[torch.Tensor], recv_shape: Optional[tuple],
+                 recv_dtype=None):
+        """Post this tick's grouped send/recv. ``send`` is snapshotted (graph outputs are
+        static buffers). Returns a handle for ``wait`` / ``to_host``, or None."""
+        ops, keep, buf = [], [], None
+        with trace_range("pp.exchange"):
+            if send is not None and send.numel() > 0:
+                snap = send.clone() if self.nccl else send.to("cpu")
+                keep.append(snap)
+                ops.append(dist.P2POp(dist.isend, snap.contiguous(), self.next))
+            if recv_shape is not None:
+                buf = torch.empty(recv_shape, dtype=recv_dtype or self.dtype,
+                                  device=self.data_device)
+                ops.append(dist.P2POp(dist.irecv, buf, self.prev))
+            if not ops:
+                return None
+            works = dist.batch_isend_irecv(ops)
+        rec = [works, keep, False]        # [works, snapshots, waited]
+        self._inflight.append(rec)
+        while len(self._inflight) > self.max_pending:
+            self._finish(self._inflight.popleft())
+        return buf, rec
 
-    def recv_hidden(self, rows: int, cols: int) -> torch.Tensor:
-        """Receive stage input from the previous stage; on RCCL the wait is a stream
-        dependency of the replay that consumes it, not a host wait."""
-        with trace_range("pp.recv"):
-            buf = torch.empty(rows, cols, dtype=self.dtype, device=self.data_device)
-            dist.irecv(buf, self.prev, group=self.in_group).wait()
+    def _finish(self, rec) -> None:
+        # a gloo Work must be waited exactly once (a second wait on a completed receive
+        # blocks forever); an RCCL wait is a dependency of the CURRENT stream and idempotent,
+        # so it is always issued (the caller's stream may not have waited yet)
+        if self.nccl or not rec[2]:
+            for w in rec[0]:
+                w.wait()
+            rec[2] = True
+
+    def wait(self, handle) -> torch.Tensor:
+        """Input of this tick: on RCCL a stream dependency of the replay, not a host wait."""
+        buf, rec = handle
+        self._finish(rec)
         return buf if buf.device == self.device else buf.to(self.device)
 
-    def irecv_tokens(self, n: int):
-        """Post the head's receive of a tick's sampled ids from the tail, on a side stream
-        so the next replay does not depend on it (returns a handle)."""
-        if self.recv_stream is not None:
-            with torch.cuda.stream(self.recv_stream):
-                buf = torch.empty(n, dtype=torch.int32, device=self.device)
-                dist.irecv(buf, self.prev, group=self.in_group).wait()
-            return buf, None
-        buf = torch.empty(n, dtype=torch.int32)
-        return buf, dist.irecv(buf, self.prev, group=self.in_group)
-
-    def tokens_to_host(self, handle) -> np.ndarray:
-        buf, work = handle
-        if self.recv_stream is not None:
-            with torch.cuda.stream(self.recv_stream):
+    def to_host(self, handle) -> np.ndarray:
+        """Head: the tail's sampled ids on the host, synchronised on a side stream so the
+        compute stream (already running the next replay) is never blocked."""
+        buf, rec = handle
+        if self.side_stream is not None:
+            with torch.cuda.stream(self.side_stream):
+                self._finish(rec)
                 return buf.cpu().numpy()
-        work.wait()
+        self._finish(rec)
         return buf.numpy()
 
     def flush(self) -> None:
-        while self._sends:
-            w, _ = self._sends.popleft()
-            w.wait()
+        while self._inflight:
+            self._finish(self._inflight.popleft())
         while self._ctrl_sends:
             w, _ = self._ctrl_sends.popleft()
             w.wait()
