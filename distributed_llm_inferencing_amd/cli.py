@@ -9,8 +9,12 @@ launcher for an 8-GPU MI355X box.
     serve-node      --gpus N [--base-port 5000] [--master URL]
                     one worker process per GPU (HIP_VISIBLE_DEVICES=i, port base+i), each
                     registered with the master as a node
-    serve-pipeline  --model M --gpus N [--port 5000]    N-rank layer-sharded pipeline; rank 0
-                    serves the worker API and reports the stages as loaded shards
+    serve-pipeline  --model M [--port 5000]             (under torchrun) N-rank layer-sharded
+                    pipeline; rank 0 serves the worker API and reports the stages as shards
+    serve-cluster   --model M --gpus 8 --dp K [--base-port 5000] [--master URL]
+                    K data-parallel replicas, each a pipeline of gpus/K stages (SURVEY.md
+                    §2.5 "DP replicas"); every replica head registers as a node and the
+                    master's dispatcher load-balances across them (least in flight)
     shard-model     --model_name M --num_shards N [--output_dir D] [--policy even|hbm|balanced]
     bench           ... (bench.py)
 """
@@ -70,6 +74,8 @@ def _serve_pipeline(argv):
     ap.add_argument("--max-batch", type=int, default=256)
     ap.add_argument("--max-model-len", type=int, default=2048)
     ap.add_argument("--policy", default="balanced")
+    ap.add_argument("--no-shard-report", action="store_true",
+                    help="DP replica: serve the model as a plain node (no shard rows)")
     a = ap.parse_args(argv)
     import torch
     from .config import get_settings
@@ -93,12 +99,64 @@ def _serve_pipeline(argv):
     st.pipeline_model = a.model
     st.pipeline_service = PipelineService(eng, name=a.model)
     st.tokenizers[a.model] = eng.head.tok
-    st.pipeline_shards = [
+    st.pipeline_shards = [] if a.no_shard_report else [
         {"model_name": a.model, "shard_id": p.shard_id, "path": f"rank{p.shard_id}",
          "metadata": p.to_metadata(a.model, len(eng.plans), eng.cfg.num_layers)}
         for p in eng.plans]
     app = create_worker_app(s, state=st)
     app.run(host="0.0.0.0", port=a.port, threaded=True)
+
+
+def cluster_plan(gpus: int, dp: int, base_port: int = 5000, rdzv_base: int = 29600):
+    """[(replica, visible_devices, http_port, rendezvous_port)] for K pipelines of gpus/K."""
+    if dp < 1 or gpus % dp:
+        raise ValueError(f"--gpus {gpus} is not divisible into {dp} replicas")
+    g = gpus // dp
+    return [(j, ",".join(str(j * g + i) for i in range(g)), base_port + j, rdzv_base + j)
+            for j in range(dp)]
+
+
+def _serve_cluster(argv):
+    import argparse
+
+    import requests
+    ap = argparse.ArgumentParser("dli serve-cluster")
+    ap.add_argument("--model", required=True)
+    ap.add_argument("--gpus", type=int, default=8)
+    ap.add_argument("--dp", type=int, default=1)
+    ap.add_argument("--base-port", type=int, default=5000)
+    ap.add_argument("--master", default=None)
+    ap.add_argument("--max-batch", type=int, default=256)
+    a, extra = ap.parse_known_args(argv)
+    procs = []
+    plan = cluster_plan(a.gpus, a.dp, a.base_port)
+    for j, devs, port, rdzv in plan:
+        env = dict(os.environ, HIP_VISIBLE_DEVICES=devs, USE_GPU="1",
+                   HSA_ENABLE_IPC_MODE_LEGACY="0")
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               f"--nproc-per-node={len(devs.split(','))}", "--master-addr", "127.0.0.1",
+               "--master-port", str(rdzv), "-m", "distributed_llm_inferencing_amd.cli",
+               "serve-pipeline", "--model", a.model, "--port", str(port),
+               "--max-batch", str(a.max_batch), "--no-shard-report", *extra]
+        procs.append(subprocess.Popen(cmd, env=env))
+    if a.master:
+        for j, _devs, port, _ in plan:
+            for _ in range(600):
+                try:
+                    r = requests.post(f"{a.master}/api/nodes/add/",
+                                      data={"hostname": f"replica{j}", "ip_address": "127.0.0.1",
+                                            "port": port}, timeout=10)
+                    if r.status_code == 200:
+                        break
+                except requests.RequestException:
+                    pass
+                time.sleep(1)
+    try:
+        for p in procs:
+            p.wait()
+    except KeyboardInterrupt:
+        for p in procs:
+            p.terminate()
 
 
 def main(argv=None):
@@ -117,6 +175,8 @@ def main(argv=None):
         return _serve_node(rest)
     if cmd == "serve-pipeline":
         return _serve_pipeline(rest)
+    if cmd == "serve-cluster":
+        return _serve_cluster(rest)
     if cmd == "shard-model":
         from .shard.writer import main as m
         return m(rest)

@@ -73,8 +73,8 @@ class WorkerState:
     def load_model(self, name: str):
         from ..engine.llm_engine import LLMEngine
         with self.lock:
-            if name in self.services:
-                return False
+            if name in self.services or name == getattr(self, "pipeline_model", None):
+                return False            # a pipeline head serves its model across all stages
             cfg = get_config(name)
             eng = LLMEngine(cfg, device=str(self.device), **self.engine_kwargs)
             self.services[name] = EngineService(eng, name=name.replace("/", "_"))
@@ -265,14 +265,15 @@ def create_worker_app(settings: Optional[Settings] = None, device: Optional[str]
                 setattr(params, k, data[k])
         try:
             faults.check("worker.inference")
-            if shard_ids:
-                svc = getattr(st, "pipeline_service", None)
-                if svc is not None and name == getattr(st, "pipeline_model", None):
-                    out = svc.generate(prompt, params, timeout=timeout + 30)
-                else:
-                    pipe = st.shard_pipeline(name, [int(s) for s in shard_ids])
-                    with st.lock:
-                        out = pipe.generate([prompt], params)[0]
+            svc = getattr(st, "pipeline_service", None)
+            if svc is not None and name == getattr(st, "pipeline_model", None):
+                # pipeline head (serve-pipeline / one DP replica of serve-cluster): every
+                # stage of this model runs on this rank's pipeline, with or without shard_ids
+                out = svc.generate(prompt, params, timeout=timeout + 30)
+            elif shard_ids:
+                pipe = st.shard_pipeline(name, [int(s) for s in shard_ids])
+                with st.lock:
+                    out = pipe.generate([prompt], params)[0]
             else:
                 if name not in st.services:
                     try:

@@ -269,3 +269,38 @@ def test_remove_node_unloads(tmp_path, master):
         assert requests.get(f"{w.url}/health", timeout=10).json()["loaded_models"] == []
     finally:
         w.close()
+
+
+def test_dp_replica_plan_and_pipeline_head_routing(tmp_path):
+    """serve-cluster: K pipelines of gpus/K ranks; a replica head serves its model as a plain
+    node (load_model = already loaded; /inference with or without shard_ids -> pipeline)."""
+    from distributed_llm_inferencing_amd.cli import cluster_plan
+    from distributed_llm_inferencing_amd.engine.sequence import RequestOutput
+    from distributed_llm_inferencing_amd.worker.server import WorkerState
+    assert cluster_plan(8, 2) == [(0, "0,1,2,3", 5000, 29600), (1, "4,5,6,7", 5001, 29601)]
+    assert [p[1] for p in cluster_plan(8, 8)] == [str(i) for i in range(8)]
+    with pytest.raises(ValueError):
+        cluster_plan(8, 3)
+
+    class FakePipe:
+        calls = 0
+
+        def generate(self, prompt, params=None, timeout=None):
+            FakePipe.calls += 1
+            return RequestOutput(request_id="x", prompt_ids=[1], output_ids=[2, 3],
+                                 finish_reason="length", latency_s=0.1, ttft_s=None,
+                                 text=f"{prompt}!")
+
+        def stats(self):
+            return {}
+
+    s = settings(tmp_path)
+    st = WorkerState(s, "cpu")
+    st.pipeline_model, st.pipeline_service, st.pipeline_shards = "llama3-8b", FakePipe(), []
+    c = create_worker_app(s, state=st).test_client()
+    r = c.post("/load_model", json={"model_name": "llama3-8b"})
+    assert r.status_code == 200 and "already loaded" in r.get_json()["message"]
+    for extra in ({}, {"shard_ids": [0, 1]}):
+        r = c.post("/inference", json={"model_name": "llama3-8b", "prompt": "hi", **extra})
+        assert r.status_code == 200 and r.get_json()["result"] == "hi!"
+    assert FakePipe.calls == 2 and "llama3-8b" not in st.services
