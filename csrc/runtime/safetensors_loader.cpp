@@ -55,12 +55,19 @@ struct Json {
     ++p;
     return true;
   }
-  bool num(long long& v) {
+  bool num(long long& v) {  // bounded: the header is not NUL-terminated
     ws();
-    char* endp = nullptr;
-    v = strtoll(p, &endp, 10);
-    if (endp == p) return false;
-    p = endp;
+    const char* q = p;
+    bool neg = false;
+    if (q < e && *q == '-') { neg = true; ++q; }
+    if (q >= e || *q < '0' || *q > '9') return false;
+    unsigned long long acc = 0;
+    for (; q < e && *q >= '0' && *q <= '9'; ++q) {
+      if (acc > (1ull << 62)) return false;       // absurd value: reject, never overflow
+      acc = acc * 10 + (unsigned)(*q - '0');
+    }
+    v = neg ? -(long long)acc : (long long)acc;
+    p = q;
     return true;
   }
   bool skip() {  // skip any value
@@ -162,10 +169,16 @@ void* dli_st_open(const char* path) {
   f->map = (const uint8_t*)m;
   uint64_t hlen = 0;
   std::memcpy(&hlen, f->map, 8);
-  if (8 + hlen > f->size || !parse_header(*f, (const char*)f->map + 8, hlen)) {
+  bool ok = hlen <= f->size - 8 && parse_header(*f, (const char*)f->map + 8, hlen);
+  if (ok) {
+    f->data_off = 8 + hlen;
+    const long long avail = (long long)(f->size - f->data_off);
+    for (const auto& t : f->tensors)            // every tensor must lie inside the file
+      if (t.begin < 0 || t.end < t.begin || t.end > avail) { ok = false; break; }
+  }
+  if (!ok) {
     munmap((void*)f->map, f->size); close(f->fd); delete f; return nullptr;
   }
-  f->data_off = 8 + hlen;
   return f;
 }
 

@@ -113,11 +113,36 @@ def build(force: bool = False, jobs: int = 0, verbose: bool = True) -> dict:
     return out
 
 
+def build_asan_selftest(verbose: bool = True) -> Path:
+    """Host-AddressSanitizer build of the C++ runtime + its self-test driver
+    (csrc/runtime/tests/runtime_selftest.cpp). Sanitizer flags are host-only
+    (``-Xarch_host``): GPU ASan is not available on the target pool."""
+    srcs = sorted((CSRC / "runtime").glob("*.cpp")) + [CSRC / "runtime" / "tests" /
+                                                        "runtime_selftest.cpp"]
+    out = REPO / "build" / "runtime_selftest_asan"
+    out.parent.mkdir(parents=True, exist_ok=True)
+    newest = max(p.stat().st_mtime for p in srcs)
+    if not out.exists() or out.stat().st_mtime < newest:
+        cmd = [_hipcc(), "-O1", "-g", "-std=c++17", "-Xarch_host", "-fsanitize=address",
+               "-Xarch_host", "-fno-omit-frame-pointer", *map(str, srcs), "-o", str(out),
+               "-lpthread"]
+        if verbose:
+            print("[dli.build]", " ".join(cmd))
+        subprocess.run(cmd, check=True)
+    return out
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", type=int, default=0)
+    ap.add_argument("--asan-selftest", action="store_true",
+                    help="build + run the host-ASan runtime self-test")
     a = ap.parse_args(argv)
+    if a.asan_selftest:
+        exe = build_asan_selftest()
+        env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1")
+        return subprocess.run([str(exe)], env=env).returncode
     build(force=a.force, jobs=a.j)
 
 

@@ -34,7 +34,8 @@ class StageRunner:
         self.max_batch = max_batch
         self.W = table_width
         if use_graphs is None:
-            use_graphs = self.device.type == "cuda" and os.environ.get("DLI_NO_GRAPHS", "0") != "1"
+            use_graphs = (self.device.type == "cuda" and os.environ.get("DLI_NO_GRAPHS", "0") != "1"
+                          and os.environ.get("DLI_DEBUG_SYNC", "0") != "1")
         self.use_graphs = use_graphs
         self.buckets = sorted({b for b in buckets if b < max_batch} | {max_batch})
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}

@@ -99,11 +99,24 @@ def ptr(t) -> int | None:
     return None if t is None else t.data_ptr()
 
 
+# DLI_DEBUG_SYNC=1: synchronise after every native launch and name the op whose kernel
+# faulted (SURVEY.md §5.2 debug mode; pair with AMD_SERIALIZE_KERNEL=3 set before HIP init,
+# which utils.debug.enable_debug_sync() does). Not usable inside hipGraph capture.
+_DEBUG_SYNC = os.environ.get("DLI_DEBUG_SYNC", "0") == "1"
+
+
 def call(name: str, *args) -> None:
     lib = require_native()
     rc = getattr(lib, name)(*args)
     if rc != 0:
         raise RuntimeError(f"{name} failed with hipError {rc}")
+    if _DEBUG_SYNC:
+        import torch
+        if not torch.cuda.is_current_stream_capturing():
+            try:
+                torch.cuda.synchronize()
+            except RuntimeError as e:
+                raise RuntimeError(f"{name}: kernel fault detected after launch: {e}") from e
 
 
 def loaded_path() -> str | None:

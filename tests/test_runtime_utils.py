@@ -126,3 +126,18 @@ def test_preemption_under_kv_pressure_keeps_outputs():
     small = small_eng.generate(prompts, sp)
     assert [o.all_ids for o in small] == [o.all_ids for o in big]
     assert small_eng.bm.num_free == 8
+
+
+def test_runtime_host_asan_selftest():
+    """The C++ runtime under host AddressSanitizer: allocator stress + safetensors parser
+    fuzz (truncated headers, bad lengths, out-of-range offsets)."""
+    import shutil
+    import subprocess
+    from distributed_llm_inferencing_amd import build
+    if shutil.which("hipcc") is None and not os.path.exists("/opt/rocm/bin/hipcc"):
+        pytest.skip("hipcc not available")
+    exe = build.build_asan_selftest(verbose=False)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1")
+    r = subprocess.run([str(exe)], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "runtime_selftest: OK" in r.stdout
