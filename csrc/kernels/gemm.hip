@@ -301,14 +301,15 @@ static int dispatch_tile(int tile_cfg, const void* A, int lda, const void* W, in
     DLI_CFG(4, 256, 128, 2)
     DLI_CFG(5, 64, 64, 3) DLI_CFG(6, 64, 128, 3) DLI_CFG(7, 128, 128, 3) DLI_CFG(8, 128, 256, 3)
     DLI_CFG(9, 256, 128, 3)
+    DLI_CFG(10, 192, 128, 2) DLI_CFG(11, 192, 128, 3) DLI_CFG(12, 160, 128, 2)
 #undef DLI_CFG
     default: return (int)hipErrorInvalidValue;
   }
 }
 
 // tile_cfg: 0=64x64 1=64x128 2=128x128 3=128x256 4=256x128 (2 LDS stages); 5..9 = the same
-// tiles with 3 LDS stages (one tile in flight across the barrier). ws: fp32 [splits, M, N]
-// when splits>1.
+// tiles with 3 LDS stages (one tile in flight across the barrier); 10/11 = 192x128 with 2/3
+// stages, 12 = 160x128 (MoE experts of ~130-190 rows in one pass). ws: fp32 [splits, M, N] when splits>1.
 // group_off (nullable): int[groups+1] row offsets; M is then the max rows of any group.
 extern "C" int dli_gemm(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M,
                         int N, int K, int epi, int tile_cfg, int splits, const void* bias,

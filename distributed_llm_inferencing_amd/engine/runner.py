@@ -166,9 +166,17 @@ class StageRunner:
         if os.environ.get("DLI_GEMM_AUTOTUNE_LOG", "0") == "1":
             import sys
             log = lambda m: print(m, file=sys.stderr, flush=True)  # noqa: E731
+        m = self.model
+        moe = (m.cfg.is_moe and m.layers and m.layers[0].get("w_gu") is not None
+               and m.layers[0]["w_gu"].dim() == 3)
         for b in (buckets or self.buckets):
             shapes, weights = self.gemm_shapes(b)
             G.autotune(shapes, weights, self.device, log=log)
+            if moe:      # grouped expert GEMMs: rows = b tokens x top-k (uniform routing)
+                lp = m.layers[0]
+                rows = b * m.cfg.top_k_experts
+                G.autotune_grouped(rows, lp["w_gu"], "silu_mul", log=log)
+                G.autotune_grouped(rows, lp["w_down"], "none", log=log)
 
     def capture(self, buckets=None):
         """Warm up and capture decode graphs for the given buckets (default: all)."""

@@ -99,11 +99,7 @@ def _gemm_native(x, w, epi: str, bias=None, out=None, plan: Optional[G.GemmPlan]
         if group_off is None:
             plan = G.plan(M, Nn, K, epi)
         else:
-            # grouped (MoE): a tile tall enough that one workgroup covers an expert's rows
-            # reads each expert weight tile once (measured: sizing by the mean rows per
-            # expert re-reads weights and ran 14 % slower on Mixtral)
-            p = G._heuristic(min(rows_per_group, 512), Nn, K, epi)
-            plan = G.GemmPlan("dli", p.tile, 1)
+            plan = G.grouped_plan(M, Nn, K, epi, groups)
     out_n = Nn // 2 if epi == "silu_mul" else Nn
     if out is None:
         dt = torch.float32 if epi == "f32" else x.dtype

@@ -23,7 +23,13 @@ for s in "$@"; do
     bench)   step bench 900 python bench.py --steps 2 --warmup 1 ;;
     reference) step reference 900 python scripts/bench_reference.py --out gpurun_out/reference_strategy.json ;;
     prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
-          step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- python bench.py --steps 1 --warmup 1 ;;
+          step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- python bench.py --steps 1 --warmup 1
+          python scripts/prof_summary.py gpurun_out/prof 40 --tail-ms 900 > gpurun_out/prof_summary.txt
+          rm -f gpurun_out/prof/*trace.csv ;;
+    prof_mixtral) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+          step prof_mixtral 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_mixtral -o bench -- python bench.py --model mixtral-8x7b --steps 1 --warmup 1 --batch 512
+          python scripts/prof_summary.py gpurun_out/prof_mixtral 40 --tail-ms 4000 > gpurun_out/prof_mixtral_summary.txt
+          rm -f gpurun_out/prof_mixtral/*trace.csv ;;
     pp2) step pp2 900 env DLI_DIST_BACKEND=gloo DLI_SAME_DEVICE=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 1 --warmup 1 --batch 64 ;;
     pp4) step pp4 900 env DLI_DIST_BACKEND=gloo DLI_SAME_DEVICE=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 4 --steps 1 --warmup 1 --batch 32 ;;
     gemm) step gemm 1100 python scripts/bench_gemm.py ;;
@@ -41,6 +47,15 @@ for s in "$@"; do
           step tune_on256 900 env DLI_GEMM_AUTOTUNE=1 python bench.py --steps 2 --warmup 1 --batch 256 ;;
     sweep) for b in 128 384 512 768; do
              step sweep_b$b 600 python bench.py --steps 2 --warmup 1 --batch $b
+           done ;;
+    moe_tiles) for t in 12 10; do
+             step moe_tile$t 900 env DLI_MOE_TILE=$t python bench.py --model mixtral-8x7b --steps 1 --warmup 1 --batch 512
+           done ;;
+    moe_tuned) for b in 128 512; do
+             step moe_tuned_b$b 900 env DLI_GEMM_AUTOTUNE_LOG=1 python bench.py --model mixtral-8x7b --steps 1 --warmup 1 --batch $b
+           done ;;
+    mixtral_sweep) for b in 256 512; do
+             step mixtral_b$b 900 python bench.py --model mixtral-8x7b --steps 1 --warmup 1 --batch $b
            done ;;
     llama70b) for b in 128 256; do
              step llama70_b$b 900 python bench.py --model llama3-70b --steps 1 --warmup 1 --batch $b
