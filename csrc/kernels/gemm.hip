@@ -15,7 +15,8 @@
 //    one W panel in an XCD's L2.
 //  * split-K over grid.y writes fp32 slabs; a second pass reduces and applies the epilogue.
 //  * grouped mode (MoE): grid.z = expert; rows of group g are [off[g], off[g+1]) of A/C,
-//    weights W + g*N*ldw. Rows past the group end are skipped.
+//    weights W + g*N*ldw. Rows past the group end are skipped. Split-K composes with it
+//    (slab rows are the permuted rows), for long-K expert GEMMs with few row tiles.
 // Epilogues: 0 bf16 store, 1 fp32 store (logits), 2 SiLU(gate)*up over the 16-row-interleaved
 // gate/up weight (output width N/2), 3 bias + tanh-GELU, 4 bias.
 #include "common.h"
@@ -317,7 +318,7 @@ extern "C" int dli_gemm(const void* A, int lda, const void* W, int ldw, void* C,
   if (M <= 0 || N <= 0) return 0;
   if (K % BK || lda % 8 || ldw % 8 || splits < 1) return (int)hipErrorInvalidValue;
   if (epi == EPI_SILU && N % 32) return (int)hipErrorInvalidValue;
-  if (splits > 1 && (ws == nullptr || group_off != nullptr)) return (int)hipErrorInvalidValue;
+  if (splits > 1 && ws == nullptr) return (int)hipErrorInvalidValue;
   if (groups < 1) groups = 1;
   switch (epi) {
     case EPI_BF16: return dispatch_tile<EPI_BF16>(tile_cfg, A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, group_off, groups, st);

@@ -120,7 +120,7 @@ def _gemm_native(x, w, epi: str, bias=None, out=None, plan: Optional[G.GemmPlan]
                          _st())
             out.copy_(y)
         return out
-    splits = plan.splits if group_off is None else 1
+    splits = plan.splits
     ws = None
     if splits > 1:
         ws = G.workspace(x.device, splits * M * Nn * 4)

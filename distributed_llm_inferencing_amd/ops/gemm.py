@@ -125,10 +125,14 @@ def autotune_grouped(rows: int, w: torch.Tensor, epi: str, iters: int = 5, log=N
                        dtype=torch.int32, device=dev)
     x = (torch.randn(max(rows, 1), K, device=dev) * 0.5).to(w.dtype)
     best = None
+    cands = []
     for tile in sorted(TILES):
         if TILES[tile][0] > 2 * max(64, rows // E + 32):
             continue                                  # far taller than an expert's rows
-        p = GemmPlan("dli", tile, 1)
+        for splits in (1, 2, 4):                      # split-K for long-K expert GEMMs
+            if splits == 1 or (K % (64 * splits) == 0 and K // splits >= 2048):
+                cands.append(GemmPlan("dli", tile, splits))
+    for p in cands:
         try:
             ms = ops.benchmark(lambda p=p: ops._gemm_native(
                 x, w, epi, plan=p, groups=E, group_off=off, rows_per_group=rows),

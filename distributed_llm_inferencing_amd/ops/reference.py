@@ -90,7 +90,7 @@ def split_gate_up(gu: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     """Inverse of the interleave on the last dim of activations [T, 2F]."""
     t, f2 = gu.shape
     v = gu.reshape(t, f2 // (2 * GU_GROUP), 2, GU_GROUP)
-    return v[:, :, 0, :].reshape(t, -1), v[:, :, 1, :].reshape(t, -1)
+    return v[:, :, 0, :].reshape(t, f2 // 2), v[:, :, 1, :].reshape(t, f2 // 2)
 
 
 def silu_mul(gu: torch.Tensor) -> torch.Tensor:

@@ -314,3 +314,28 @@ def test_sampling_fallback_path_adversarial(gpu):
                          torch.arange(B, device=gpu, dtype=torch.int64) + 1000 * rep)
         assert torch.isfinite(filt.gather(1, tok.long()[:, None])).all()
         assert (tok % 512 == 0).all()
+
+
+@pytest.mark.parametrize("epi", ["none", "silu_mul"])
+def test_grouped_gemm_all_tiles_and_splitk(gpu, epi):
+    """Grouped (MoE) GEMM over uneven groups (one empty, one past a 128-row tile) for every
+    tile id and split-K factor, against per-group fp32 references."""
+    torch.manual_seed(12)
+    sizes = [0, 37, 170, 5]
+    E, N, K = len(sizes), 256, 1024
+    rows = sum(sizes)
+    x = rnd(rows, K, dev=gpu)
+    w = rnd(E, N, K, dev=gpu, scale=0.05)
+    off = torch.tensor([0] + list(__import__("itertools").accumulate(sizes)), dtype=torch.int32,
+                       device=gpu)
+    refs = []
+    for e in range(E):
+        xe = x[off[e]:off[e + 1]]
+        y = R.linear(xe, w[e])
+        refs.append(R.silu_mul(y.float().to(BF)) if epi == "silu_mul" else y)
+    ref = torch.cat(refs)
+    for tile in G.TILES:
+        for splits in (1, 2, 4):
+            out = ops._gemm_native(x, w, epi, plan=G.GemmPlan("dli", tile, splits), groups=E,
+                                   group_off=off, rows_per_group=rows)
+            close(out, ref, rtol=2e-2, atol=2e-2)
