@@ -339,3 +339,17 @@ def test_grouped_gemm_all_tiles_and_splitk(gpu, epi):
             out = ops._gemm_native(x, w, epi, plan=G.GemmPlan("dli", tile, splits), groups=E,
                                    group_off=off, rows_per_group=rows)
             close(out, ref, rtol=2e-2, atol=2e-2)
+
+
+def test_moe_mlp_prefill_blas_path(gpu, monkeypatch):
+    """Prefill-sized MoE (rows per expert above the threshold) takes the per-expert
+    hipBLASLt path; same result as the reference."""
+    monkeypatch.setattr(ops, "_MOE_BLAS_ROWS", 16)
+    torch.manual_seed(13)
+    T, E, k, D, F = 200, 4, 2, 256, 512
+    x = rnd(T, D, dev=gpu)
+    rw, rids = R.router_topk(rnd(T, E, dev=gpu), k)
+    wgu = rnd(E, 2 * F, D, dev=gpu, scale=0.05)
+    wd = rnd(E, D, F, dev=gpu, scale=0.05)
+    close(ops.moe_mlp(x, wgu, wd, rw, rids), R.moe_mlp(x, wgu, wd, rw, rids),
+          rtol=3e-2, atol=3e-2)
