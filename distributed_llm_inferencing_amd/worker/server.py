@@ -47,6 +47,22 @@ from .service import EngineService
 log = logging.getLogger("dli.worker")
 
 
+def gpu_busy_percent(index: int) -> Optional[float]:
+    """Device busy % from the amdgpu driver (sysfs ``gpu_busy_percent`` of the PCI device
+    backing HIP device `index`); None where unavailable (reference W3 only had a memory
+    ratio proxy, worker/app.py:60-67)."""
+    try:
+        p = torch.cuda.get_device_properties(index)
+        bus = getattr(p, "pci_bus_id", None)
+        if bus is None:
+            return None
+        dom, dev = getattr(p, "pci_domain_id", 0), getattr(p, "pci_device_id", 0)
+        path = Path(f"/sys/bus/pci/devices/{dom:04x}:{bus:02x}:{dev:02x}.0/gpu_busy_percent")
+        return float(path.read_text().strip()) if path.exists() else None
+    except Exception:  # noqa: BLE001
+        return None
+
+
 class WorkerState:
     def __init__(self, settings: Settings, device: Optional[str] = None,
                  engine_kwargs: Optional[dict] = None):
@@ -159,6 +175,9 @@ class WorkerState:
                 extra = {"hbm_total_bytes": total, "hbm_used_bytes": total - free,
                          "gpu_name": torch.cuda.get_device_name(self.device),
                          "gpu_index": self.device.index}
+                busy = gpu_busy_percent(self.device.index or 0)
+                if busy is not None:
+                    extra["gpu_busy"] = busy / 100.0
             except Exception:  # noqa: BLE001
                 pass
         return {"cpu": psutil.cpu_percent() / 100.0,
