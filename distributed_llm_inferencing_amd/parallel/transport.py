@@ -63,6 +63,17 @@ class PipeChannel:
         self.max_pending = max_pending
         self.side_stream = (torch.cuda.Stream(self.device)
                             if self.nccl and self.device.type == "cuda" else None)
+        if self.world > 1:
+            # every rank joins one grouped ring exchange up front, so whatever point-to-point
+            # communicator state RCCL builds lazily is built with all ranks present (the
+            # session's first exchanges involve only some ranks)
+            t = torch.full((1,), float(self.rank), device=self.data_device)
+            r = torch.empty(1, device=self.data_device)
+            for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, t, self.next),
+                                             dist.P2POp(dist.irecv, r, self.prev)]):
+                w.wait()
+            if int(r.item()) != self.prev:
+                raise RuntimeError(f"pipeline ring check failed on rank {self.rank}")
 
     @property
     def next(self) -> int:
