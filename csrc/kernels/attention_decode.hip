@@ -8,16 +8,22 @@
 //   online softmax along tokens (exp2 domain; max across the 4 lane groups = 2 shuffles)
 //   O[head, d] += P[head, tok] . V[tok, d]       (the S^T accumulator IS the A operand with a
 //                                                permuted token order, so P never leaves
-//                                                registers; V^T is stored token-contiguous in
-//                                                the cache so the B operand is two 8-B loads)
+//                                                registers; the V tile is staged row-major in
+//                                                a per-wave LDS tile and read as the B operand
+//                                                with the transposing ds_read_b64_tr_b16, as
+//                                                in the prefill kernel)
 // With >1 split the per-split (m, l, O) go to a workspace merged by a second kernel.
 //
-// Layouts: q rows of stride q_stride (the fused QKV buffer), k_cache [nblk,Hkv,bs,hd],
-// v_cache [nblk,Hkv,hd,bs], block_tables [B, max_blocks], out [B, Hq, hd].
+// Layouts: q rows of stride q_stride (the fused QKV buffer), k_cache and v_cache
+// [nblk,Hkv,bs,hd] (token-major: the per-step cache write is a contiguous row),
+// block_tables [B, max_blocks], out [B, Hq, hd].
 #include "common.h"
 
 #define DEC_WAVES 4
 #define DEC_TILE 32
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
 
 template <int HD>
 __global__ void __launch_bounds__(256) decode_attn_kernel(
@@ -27,7 +33,11 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
     int B, int hq, int hkv, int block_size, float scale_log2, int num_splits, int split_tokens,
     float* __restrict__ ws_o, float* __restrict__ ws_ml) {
   constexpr int KK = HD / 32;     // MFMA k-steps over head_dim
-  constexpr int DB = HD / 16;     // 16-wide output column blocks
+  constexpr int DB = HD / 16;     // 16-wide output column blocks (= V pieces per lane)
+  constexpr int VROW = HD + 16;   // padded LDS row of the V tile, in u16
+  constexpr int VCH = HD / 8;     // 16-B chunks per V row
+  __shared__ __attribute__((aligned(16))) u16 vtile_all[DEC_WAVES][DEC_TILE * VROW];
+  u16* vt = vtile_all[threadIdx.x >> 6];
   const int lane = threadIdx.x & 63;
   // one WAVE per work item (sequence, kv head, KV split): no LDS, no barriers, so every
   // resident wave of the chip streams a different (seq, head) pair concurrently
@@ -75,20 +85,15 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
       for (int kk = 0; kk < KK; ++kk)
         kreg[s][kk] = *reinterpret_cast<const uint4*>(kp + kk * 32 + grp * 8);
     }
-    // V rows: tokens t0 + pi(grp, j), pi(grp, j) = 16(j>>2) + 4grp + (j&3), from V^T [d][tok]
-    const int tokA = min(t0 + 4 * grp, s_end - 1) & ~3;         // 4-aligned, in-range rows
-    const int tokB = min(t0 + 16 + 4 * grp, s_end - 1) & ~3;
-    const int blkA = bt[tokA / block_size], offA = tokA % block_size;
-    const int blkB = bt[tokB / block_size], offB = tokB % block_size;
-    const u16* vA = v_cache + ((long)blkA * hkv + kvh) * kv_head_stride + offA;
-    const u16* vB = v_cache + ((long)blkB * hkv + kvh) * kv_head_stride + offB;
+    // V rows t0 .. t0+31 (row-major, 16-B chunks; piece lane + 64m = row r, chunk c)
     uint4 vreg[DB];
 #pragma unroll
-    for (int i = 0; i < DB; ++i) {
-      const long drow = (long)(16 * i + col) * block_size;
-      const uint2 a = *reinterpret_cast<const uint2*>(vA + drow);
-      const uint2 c = *reinterpret_cast<const uint2*>(vB + drow);
-      vreg[i] = make_uint4(a.x, a.y, c.x, c.y);
+    for (int m = 0; m < DB; ++m) {
+      const int piece = lane + 64 * m, r = piece / VCH, c = piece % VCH;
+      const int tok = min(t0 + r, s_end - 1);                  // clamp: always-written rows
+      const int blk = bt[tok / block_size], off = tok % block_size;
+      vreg[m] = *reinterpret_cast<const uint4*>(
+          v_cache + ((long)blk * hkv + kvh) * kv_head_stride + (long)off * HD + c * 8);
     }
     // ---- S^T = K . Q^T for the two 16-token subtiles
     f32x4 s_acc[2];
@@ -128,14 +133,34 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
 #pragma unroll
       for (int i = 0; i < DB; ++i) o_acc[i][r] *= a;
     }
-    // A operand: P[head=col][k = 8grp + j] in the permuted token order pi(grp, j)
+    // stage the V tile in this wave's LDS rows (previous tile's reads retired below)
+#pragma unroll
+    for (int m = 0; m < DB; ++m) {
+      const int piece = lane + 64 * m, r = piece / VCH, c = piece % VCH;
+      *reinterpret_cast<uint4*>(vt + r * VROW + c * 8) = vreg[m];
+    }
+    // A operand: P[head=col][k = 8grp + j] in the permuted token order
+    // pi(grp, j) = 16(j>>2) + 4grp + (j&3)
     bf16x8 pa;
 #pragma unroll
     for (int j = 0; j < 8; ++j) pa[j] = (__bf16)p[j];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // V tile writes landed (same wave)
+    // B operand: rows (tokens) 4grp+q and 16+4grp+q, columns 16i + 4p, transposed by
+    // ds_read_b64_tr_b16 (lane 4q+p of each 16-lane group names row q, columns 4p..4p+3)
+    const int qrow = (lane >> 2) & 3, pcol = lane & 3;
 #pragma unroll
-    for (int i = 0; i < DB; ++i)
-      o_acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, *reinterpret_cast<bf16x8*>(&vreg[i]),
+    for (int i = 0; i < DB; ++i) {
+      const u16* a0 = vt + (4 * grp + qrow) * VROW + 16 * i + 4 * pcol;
+      const u16* a1 = vt + (16 + 4 * grp + qrow) * VROW + 16 * i + 4 * pcol;
+      s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) s16x4*)(a0));
+      s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) s16x4*)(a1));
+      s16x8 w = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      o_acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, *reinterpret_cast<bf16x8*>(&w),
                                                         o_acc[i], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before next overwrite
   }
   // ---- finalize: denominator of head `col`, then rows 4grp + r of O
   float l_tot = l_part + __shfl_xor(l_part, 16, 64);

@@ -123,18 +123,11 @@ __global__ void __launch_bounds__(256) splitk_rope_cache_kernel(
   const int slot = slot_mapping[t];
   if (slot < 0) return;
   const int blk = slot / block_size, off = slot - blk * block_size;
-  if (is_k) {
-    u16* dst = k_cache + (((long)blk * hkv + (h - hq)) * block_size + off) * hd;
-    store8(dst + d0, x1);
-    store8(dst + half + d0, x2);
-  } else {
-    u16* dst = v_cache + ((long)blk * hkv + (h - hq - hkv)) * hd * block_size + off;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      dst[(long)(d0 + j) * block_size] = f2bf(x1[j]);
-      dst[(long)(half + d0 + j) * block_size] = f2bf(x2[j]);
-    }
-  }
+  // K and V share the token-major [blk, head, off, hd] layout: whole-row 16-B stores
+  u16* dst = is_k ? k_cache + (((long)blk * hkv + (h - hq)) * block_size + off) * hd
+                  : v_cache + (((long)blk * hkv + (h - hq - hkv)) * block_size + off) * hd;
+  store8(dst + d0, x1);
+  store8(dst + half + d0, x2);
 }
 
 extern "C" int dli_splitk_rope_cache(void* qkv, const float* ws, int splits, int T, int N,

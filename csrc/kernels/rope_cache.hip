@@ -6,7 +6,7 @@
 // cross-lane traffic. cos/sin come from a host-precomputed fp32 table [max_pos, hd]
 // (cdna_hip_programming.md App. B: no on-device trig in memory-bound elementwise ops).
 //
-// Cache layouts (see ops/reference.py): k_cache [nblk, Hkv, bs, hd], v_cache [nblk, Hkv, hd, bs].
+// Cache layouts (see ops/reference.py): k_cache and v_cache both [nblk, Hkv, bs, hd].
 #include "common.h"
 
 __global__ void __launch_bounds__(256) rope_cache_kernel(
@@ -49,20 +49,13 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(
   const int slot = slot_mapping[t];
   if (slot < 0) return;
   const int blk = slot / block_size, off = slot - blk * block_size;
-  if (is_k) {
-    const int kh = h - hq;
-    u16* dst = k_cache + (((long)blk * hkv + kh) * block_size + off) * hd;
-    store8(dst + d0, x1);
-    store8(dst + half + d0, x2);
-  } else {
-    const int vh = h - hq - hkv;
-    u16* dst = v_cache + ((long)blk * hkv + vh) * hd * block_size + off;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      dst[(long)(d0 + j) * block_size] = f2bf(x1[j]);
-      dst[(long)(half + d0 + j) * block_size] = f2bf(x2[j]);
-    }
-  }
+  // K and V share the token-major [blk, head, off, hd] layout: whole-row 16-B stores (a
+  // transposed V made every decode step a 2-byte scatter, i.e. a read-modify-write of a
+  // memory sector per element)
+  u16* dst = is_k ? k_cache + (((long)blk * hkv + (h - hq)) * block_size + off) * hd
+                  : v_cache + (((long)blk * hkv + (h - hq - hkv)) * block_size + off) * hd;
+  store8(dst + d0, x1);
+  store8(dst + half + d0, x2);
 }
 
 extern "C" int dli_rope_cache(void* qkv, int row_stride, const int* positions,

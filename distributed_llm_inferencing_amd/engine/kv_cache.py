@@ -2,9 +2,9 @@
 
 Two tensors per stage (one allocation each, sized from free HBM):
     K: [L_stage, num_blocks, Hkv, block_size, hd]
-    V: [L_stage, num_blocks, Hkv, hd, block_size]   (transposed inside a block, see ops/reference.py)
+    V: [L_stage, num_blocks, Hkv, block_size, hd]   (token-major like K, see ops/reference.py)
 Zero-initialised once so rows past a sequence's context are always finite (the decode
-kernel reads whole 4-token groups and multiplies the masked ones by 0).
+kernel reads whole 32-token tiles and multiplies the masked ones by 0).
 """
 from __future__ import annotations
 
@@ -48,7 +48,7 @@ class KVCache:
         self.block_size = block_size
         hkv, hd = cfg.num_kv_heads, cfg.head_dim
         self.k = torch.zeros(num_layers, num_blocks, hkv, block_size, hd, dtype=dtype, device=device)
-        self.v = torch.zeros(num_layers, num_blocks, hkv, hd, block_size, dtype=dtype, device=device)
+        self.v = torch.zeros(num_layers, num_blocks, hkv, block_size, hd, dtype=dtype, device=device)
 
     def layers(self) -> List[Tuple[torch.Tensor, torch.Tensor]]:
         return [(self.k[i], self.v[i]) for i in range(self.num_layers)]

@@ -8,8 +8,9 @@ CPU test), and (b) the golden each HIP kernel is tested against
 * fused QKV activations: ``[T, (Hq + 2*Hkv) * hd]``
 * paged KV cache, per layer:
     ``k_cache [num_blocks, Hkv, block_size, hd]``
-    ``v_cache [num_blocks, Hkv, hd, block_size]``  (V stored transposed inside a
-    block so the decode kernel's P·V MFMA reads token-contiguous 16-B fragments)
+    ``v_cache [num_blocks, Hkv, block_size, hd]``  (token-major like K: a decode step's
+    K/V write is one contiguous 2*hd-byte row per head; the decode kernel transposes V
+    tiles through LDS with ds_read_b64_tr_b16 for its P·V MFMA)
 * ``slot_mapping[t] = block * block_size + offset`` (int32)
 * gate/up weights interleaved in 16-row groups: rows ``[32i, 32i+16)`` are gate
   features ``[16i, 16i+16)`` and rows ``[32i+16, 32i+32)`` the matching up
@@ -142,7 +143,7 @@ def write_kv(k: torch.Tensor, v: torch.Tensor, slot_mapping: torch.Tensor,
     slots, kk, vv = slots[valid], k[valid], v[valid]
     blk, off = slots // bs, slots % bs
     k_cache[blk, :, off, :] = kk.to(k_cache.dtype)
-    v_cache[blk, :, :, off] = vv.to(v_cache.dtype)
+    v_cache[blk, :, off, :] = vv.to(v_cache.dtype)
 
 
 def rope_and_cache(qkv, positions, slot_mapping, cos_sin, k_cache, v_cache,
@@ -187,7 +188,7 @@ def gather_kv(k_cache, v_cache, block_table: torch.Tensor, ctx_len: int):
     nblk = (ctx_len + bs - 1) // bs
     blocks = block_table[:nblk].long()
     kk = k_cache[blocks].permute(0, 2, 1, 3).reshape(nblk * bs, k_cache.shape[1], -1)[:ctx_len]
-    vv = v_cache[blocks].permute(0, 3, 1, 2).reshape(nblk * bs, v_cache.shape[1], -1)[:ctx_len]
+    vv = v_cache[blocks].permute(0, 2, 1, 3).reshape(nblk * bs, v_cache.shape[1], -1)[:ctx_len]
     return kk, vv
 
 

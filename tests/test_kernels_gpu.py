@@ -168,7 +168,7 @@ def _paged_setup(gpu, lens, hq, hkv, hd, bs, nblk=64, seed=4):
     qkv = rnd(T, (hq + 2 * hkv) * hd, dev=gpu)
     pos = torch.cat([torch.arange(n) for n in lens]).to(gpu, torch.int32)
     kc = torch.zeros(nblk, hkv, bs, hd, device=gpu, dtype=BF)
-    vc = torch.zeros(nblk, hkv, hd, bs, device=gpu, dtype=BF)
+    vc = torch.zeros(nblk, hkv, bs, hd, device=gpu, dtype=BF)
     perm = torch.randperm(nblk).tolist()
     tables, slots, o = [], [], 0
     maxb = max(-(-n // bs) for n in lens)
