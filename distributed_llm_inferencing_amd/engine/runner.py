@@ -155,9 +155,11 @@ class StageRunner:
             add(lp.get("wqkv"), "splitk"), add(lp.get("wo"), "splitk")
             if not m.cfg.is_moe:
                 add(lp.get("w_gu"), "silu_mul"), add(lp.get("w_down"), "splitk")
-        if m.is_last:
+        if m.is_last and not m.vocab_parallel:
             head = m.params["embed"] if m.cfg.tie_embeddings else m.params.get("lm_head")
             add(head, "f32")
+        if m.vocab_parallel:                 # this rank's slice of the LM head
+            add(m.params.get("head_slice"), "f32")
         return shapes, weights
 
     def autotune(self, buckets=None):

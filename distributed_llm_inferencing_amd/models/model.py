@@ -49,6 +49,10 @@ class TransformerLM:
         # tensor-parallel mode (parallel/tensor.py): all-reduce(sum) of the row-parallel
         # O / down projections before their residual add
         self.tp_reduce: Optional[Callable] = None
+        # vocab-parallel LM head (parallel/pipeline.py): the last stage returns the final
+        # normed hidden state; every stage holds a vocab slice of the head
+        self.vocab_parallel = False
+        self.vocab_offset = 0
         self.layers = [self._layer_params(i) for i in range(self.layer_start, self.layer_end)]
 
     # ------------------------------------------------------------------ construction
@@ -188,17 +192,27 @@ class TransformerLM:
         e0 = self.expert_range[0] if self.expert_range else 0
         return ops.moe_mlp(h, lp["w_gu"], lp["w_down"], topk_w, topk_ids, e0)
 
-    def logits(self, hidden: torch.Tensor, b: DeviceBatch) -> torch.Tensor:
-        """Final norm + LM head on the last token of each sequence -> fp32 [S, V]."""
+    def final_hidden(self, hidden: torch.Tensor, b: DeviceBatch) -> torch.Tensor:
+        """Final norm of the last token of each sequence -> bf16 [S, D]."""
         cfg, p = self.cfg, self.params
         if b.is_prefill:
             hidden = hidden.index_select(0, b.last_token_idx)
         if cfg.arch == "gpt2":
-            h = ops.layernorm(hidden, p["final_norm"], p["final_norm_b"], cfg.norm_eps)
-        else:
-            h = ops.rmsnorm(hidden, p["final_norm"], cfg.norm_eps)
-        head = p["embed"] if cfg.tie_embeddings else p["lm_head"]
-        return ops.linear(h, head, epi="f32")
+            return ops.layernorm(hidden, p["final_norm"], p["final_norm_b"], cfg.norm_eps)
+        return ops.rmsnorm(hidden, p["final_norm"], cfg.norm_eps)
+
+    def head_logits(self, h: torch.Tensor) -> torch.Tensor:
+        p = self.params
+        return ops.linear(h, p["embed"] if self.cfg.tie_embeddings else p["lm_head"], epi="f32")
+
+    def logits(self, hidden: torch.Tensor, b: DeviceBatch) -> torch.Tensor:
+        """Final norm + LM head on the last token of each sequence -> fp32 [S, V]."""
+        return self.head_logits(self.final_hidden(hidden, b))
+
+    def head_candidates(self, h: torch.Tensor, c: int = 64):
+        """This rank's slice of a vocab-parallel LM head (``params['head_slice']`` = rows
+        ``[vocab_offset, vocab_offset + V_r)``): top-``c`` (fp32 values, int32 ids)."""
+        return ops.head_candidates(h, self.params["head_slice"], self.vocab_offset, c)
 
     def sample(self, logits: torch.Tensor, b: DeviceBatch, generator=None) -> torch.Tensor:
         return ops.sample(logits, b.temperature, b.top_k, b.top_p, b.seeds, generator=generator)
@@ -212,6 +226,8 @@ class TransformerLM:
         x = self.forward_layers(x, b, kv_caches)
         if not self.is_last:
             return x
+        if self.vocab_parallel:          # the LM head runs sliced on every pipeline rank
+            return self.final_hidden(x, b)
         lg = self.logits(x, b)
         tok = self.sample(lg, b)
         return (tok, lg) if return_logits else tok

@@ -303,15 +303,36 @@ def decode_attention(qkv, k_cache, v_cache, block_tables, context_lens, max_cont
 
 
 # ----------------------------------------------------------------------------- sampling
-def sample(logits, temperature, top_k, top_p, seeds, generator=None):
-    """logits fp32 [B, V] -> int32 tokens [B]. temperature<=0 -> greedy."""
+def sample(logits, temperature, top_k, top_p, seeds, generator=None, ids=None):
+    """logits fp32 [B, V] -> int32 tokens [B]. temperature<=0 -> greedy. With ``ids``
+    [B, V] the row holds candidates (vocab-parallel LM head) in ascending token-id order,
+    and the sampled column is mapped to its token id (ties then break by token id exactly
+    as over the full vocabulary)."""
     if not _use_native(logits):
-        return R.sample(logits, temperature, top_k, top_p, generator=generator, seeds=seeds)
+        return R.sample(logits, temperature, top_k, top_p, generator=generator, seeds=seeds,
+                        ids=ids)
     B, V = logits.shape
     out = torch.empty(B, dtype=torch.int32, device=logits.device)
     _native_call("dli_sample", _p(out), _p(logits), logits.stride(0), B, V, _p(temperature),
                  _p(top_k), _p(top_p), _p(seeds), _st())
+    if ids is not None:
+        out = ids.gather(1, out.long().unsqueeze(1)).squeeze(1).to(torch.int32)
     return out
+
+
+def head_candidates(h, w_slice, offset: int, c: int):
+    """Vocab-parallel LM head slice on this rank: fp32 logits for token ids
+    ``[offset, offset + V_r)`` and the top-``c`` per row, returned in ascending token-id
+    order (values fp32 [S, c], ids int32 [S, c]). The union over ranks contains every
+    token a top-k <= c sampler can pick."""
+    if not _use_native(h):
+        v, i = R.head_candidates(h, w_slice, offset, c)
+    else:
+        lg = linear(h, w_slice, epi="f32")
+        v, i = torch.topk(lg, min(c, lg.shape[1]), dim=-1)
+        i = (i + offset).to(torch.int32)
+    i, perm = torch.sort(i, dim=-1)
+    return v.gather(1, perm), i
 
 
 # ----------------------------------------------------------------------------- MoE

@@ -235,30 +235,66 @@ def topk_topp_filter(logits: torch.Tensor, temperature: torch.Tensor, top_k: tor
     return out
 
 
+def _draw(probs: torch.Tensor, ids: torch.Tensor, g: torch.Generator) -> int:
+    """Inverse-CDF draw over the support ordered by (probability desc, token id asc): the
+    token drawn depends only on (token id, probability) pairs, not on where they sit in the
+    row, so sampling from a candidate list (vocab-parallel LM head) equals sampling from the
+    full vocabulary (same contract as the HIP sampler's sorted inverse-CDF draw)."""
+    nz = (probs > 0).nonzero().squeeze(-1)
+    pv, iv = probs[nz].double(), ids[nz]
+    o1 = torch.argsort(iv)
+    pv, iv = pv[o1], iv[o1]
+    o2 = torch.sort(-pv, stable=True).indices
+    pv, iv = pv[o2], iv[o2]
+    u = torch.rand((), generator=g, dtype=torch.float64) * pv.sum()
+    j = int(torch.searchsorted(pv.cumsum(0), u, right=True).clamp_max(pv.numel() - 1))
+    return int(iv[j])
+
+
 def sample(logits: torch.Tensor, temperature: torch.Tensor, top_k: torch.Tensor,
            top_p: torch.Tensor, generator: Optional[torch.Generator] = None,
-           seeds: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Returns int32 token ids [B]. temperature<=0 (or top_k == 1) -> greedy argmax.
-    With per-row ``seeds`` each row draws from its own generator, so a request's tokens do
-    not depend on its batch neighbours (same contract as the HIP sampler)."""
+           seeds: Optional[torch.Tensor] = None,
+           ids: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Returns int32 token ids [B]. temperature<=0 (or top_k == 1) -> greedy argmax (lowest
+    token id on ties). ``ids`` [B, C]: the row holds candidates (vocab-parallel LM head)
+    whose token ids are ``ids``; default ids = column index. With per-row ``seeds`` each row
+    draws from its own generator, so a request's tokens do not depend on its batch
+    neighbours (same contract as the HIP sampler)."""
+    B, V = logits.shape
+    if ids is None:
+        ids = torch.arange(V, device=logits.device, dtype=torch.int64).expand(B, V)
+    ids = ids.long()
     greedy = (temperature <= 0) | (top_k == 1)
-    out = torch.empty(logits.shape[0], dtype=torch.int32, device=logits.device)
-    if greedy.any():
-        out[greedy] = logits[greedy].float().argmax(-1).to(torch.int32)
+    out = torch.empty(B, dtype=torch.int32, device=logits.device)
+    x = logits.float()
+    for r in greedy.nonzero().squeeze(-1).tolist():
+        m = x[r] == x[r].max()
+        out[r] = int(ids[r][m].min())
     ng = ~greedy
     if ng.any():
-        filt = topk_topp_filter(logits[ng], temperature[ng], top_k[ng], top_p[ng])
+        rows = ng.nonzero().squeeze(-1).tolist()
+        filt = topk_topp_filter(x[ng], temperature[ng], top_k[ng], top_p[ng])
         probs = filt.softmax(-1)
-        if seeds is None:
-            out[ng] = torch.multinomial(probs, 1, generator=generator).squeeze(-1).to(torch.int32)
-        else:
-            rows = ng.nonzero().squeeze(-1).tolist()
-            sd = seeds.tolist()
-            for j, r in enumerate(rows):
+        sd = seeds.tolist() if seeds is not None else None
+        for j, r in enumerate(rows):
+            if sd is None:
+                g = generator
+                if g is None:
+                    g = torch.Generator(device=probs.device)
+                    g.seed()
+            else:
                 g = torch.Generator(device=probs.device)
                 g.manual_seed(int(sd[r]) & 0x7FFF_FFFF_FFFF_FFFF)
-                out[r] = torch.multinomial(probs[j], 1, generator=g).to(torch.int32)[0]
+            out[r] = _draw(probs[j], ids[r], g)
     return out
+
+
+def head_candidates(h: torch.Tensor, w_slice: torch.Tensor, offset: int, c: int):
+    """Vocab-parallel LM head slice: fp32 logits of rows ``[offset, offset + V_r)`` and
+    their top-``c`` (values desc, token ids) -> (fp32 [S, c], int32 [S, c])."""
+    lg = linear(h, w_slice, out_dtype=torch.float32)
+    v, i = torch.topk(lg, min(c, lg.shape[1]), dim=-1)
+    return v, (i + offset).to(torch.int32)
 
 
 # ----------------------------------------------------------------------------- MoE (K15, K16)

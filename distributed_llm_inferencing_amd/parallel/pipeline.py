@@ -26,7 +26,7 @@ from __future__ import annotations
 
 import os
 import time
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -38,6 +38,8 @@ from ..engine.llm_engine import EngineStats, seq_to_output
 from ..engine.runner import StageRunner
 from ..engine.scheduler import Scheduler
 from ..engine.sequence import RequestOutput, SamplingParams
+from .. import ops
+from ..models import weights as W
 from ..models.configs import ModelConfig, get_config
 from ..models.model import TransformerLM
 from ..runtime import BlockManager
@@ -59,21 +61,44 @@ def _ctrl(kind: int, tick: int, meta: Optional[StepMeta] = None):
     return h, p
 
 
-def num_microbatches(world: int) -> int:
-    """M = N + 1 microbatches in flight: the head schedules microbatch m one full tick after
-    the tail returned its tokens, so no stage ever waits on the head's host (M = N would
-    put the head's token sync + scheduling on the critical path of every tick)."""
+def num_microbatches(world: int, vocab_parallel: bool = False) -> int:
+    """Microbatches in flight. M = N + 1: the head re-schedules a microbatch one full tick
+    after the tail returned its tokens, so no stage waits on the head's host (M = N would put
+    the token sync + scheduling on the critical path of every tick). With the vocab-parallel
+    head the tokens exist on rank 0 two ticks later (candidates, then sampling): M = N + 3."""
     if world <= 1:
         return 1
-    return int(os.environ.get("DLI_PP_MICROBATCHES", str(world + 1)))
+    return int(os.environ.get("DLI_PP_MICROBATCHES",
+                              str(world + (3 if vocab_parallel else 1))))
+
+
+def use_vocab_parallel(cfg: ModelConfig, world: int) -> bool:
+    """Vocab-parallel LM head: every stage computes 1/N of the 1 GB Llama-3 head, which
+    otherwise sits on the tail and (32 layers over 8 stages) leaves the 5-layer stages 17 %
+    over the mean. DLI_PP_VOCAB_PARALLEL=0/1 forces it; default on for N >= 4."""
+    env = os.environ.get("DLI_PP_VOCAB_PARALLEL", "auto")
+    ok = world > 1 and not cfg.tie_embeddings and cfg.arch == "llama"
+    if env in ("0", "1"):
+        return ok and env == "1"
+    return ok and world >= 4
+
+
+CAND = 64          # per-rank candidates of the vocab-parallel LM head (max top_k served)
+
+
+def vocab_slices(vocab: int, n: int) -> List[Tuple[int, int]]:
+    b = [round(i * vocab / n) for i in range(n + 1)]
+    return [(b[i], b[i + 1]) for i in range(n)]
 
 
 class StageWorker:
-    """Model slice + KV pool + hipGraph runner of one pipeline stage."""
+    """Model slice + KV pool + hipGraph runner of one pipeline stage; with a vocab-parallel
+    head also this rank's slice of the LM head (candidates) and, on rank 0, the sampler."""
 
     def __init__(self, cfg: ModelConfig, plan: StagePlan, device, num_blocks: int,
                  block_size: int, max_batch: int, table_width: int, seed: int = 0,
-                 use_graphs: Optional[bool] = None, params=None, dtype=torch.bfloat16):
+                 use_graphs: Optional[bool] = None, params=None, dtype=torch.bfloat16,
+                 vocab_slice: Optional[Tuple[int, int]] = None):
         self.cfg, self.plan = cfg, plan
         self.device = torch.device(device)
         if params is None:
@@ -82,6 +107,18 @@ class StageWorker:
         else:
             self.model = TransformerLM(cfg, {k: v.to(self.device) for k, v in params.items()},
                                        plan.start_layer, plan.end_layer, self.device)
+        self.vocab_parallel = vocab_slice is not None
+        if self.vocab_parallel:
+            lo, hi = vocab_slice
+            if "head_slice" not in self.model.params:
+                full = self.model.params.get("lm_head")
+                if full is None:        # same per-name deterministic init as the tail's head
+                    shape = W.stage_param_shapes(cfg, 0, cfg.num_layers, False, True)["lm_head"]
+                    full = W.random_init({"lm_head": shape}, self.device, dtype, seed)["lm_head"]
+                self.model.params["head_slice"] = full[lo:hi].contiguous()
+                del full
+            self.model.vocab_parallel = True
+            self.model.vocab_offset = lo
         self.kv = KVCache(cfg, plan.end_layer - plan.start_layer, num_blocks, block_size,
                           self.device, dtype)
         self.runner = StageRunner(self.model, self.kv, max_batch, table_width, use_graphs)
@@ -91,9 +128,47 @@ class StageWorker:
         return self.model.is_last
 
     def compute(self, meta: StepMeta, data: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+        """Layers of this stage. Last stage: int32 tokens, or with a vocab-parallel head the
+        final normed hidden [S, D] of each sequence."""
         if meta.kind not in (PREFILL, DECODE) or meta.num_seqs == 0:
             return None
         return self.runner.run(meta, hidden=data)
+
+    def _sampling(self, meta: StepMeta):
+        d = self.device
+        return (torch.from_numpy(np.ascontiguousarray(meta.temperature, np.float32)).to(d),
+                torch.from_numpy(np.ascontiguousarray(meta.top_k, np.int32)).to(d),
+                torch.from_numpy(np.ascontiguousarray(meta.top_p, np.float32)).to(d),
+                torch.from_numpy(np.ascontiguousarray(meta.seeds, np.int64)).to(d))
+
+    def candidates(self, hf: torch.Tensor) -> torch.Tensor:
+        """This rank's top-CAND of its vocab slice, packed int32 [S, 2*CAND] (values | ids)."""
+        v, i = self.model.head_candidates(hf, CAND)
+        return torch.cat([v.contiguous().view(torch.int32), i], dim=1)
+
+    def sample_candidates(self, meta: StepMeta, packed: List[torch.Tensor]) -> torch.Tensor:
+        """Rank 0: merge every rank's candidates (rank order = ascending token ids) and
+        sample with the request's warpers and Philox seed -> int32 tokens [S]."""
+        vals = torch.cat([c[:, :CAND].contiguous().view(torch.float32) for c in packed], 1)
+        ids = torch.cat([c[:, CAND:] for c in packed], 1).contiguous()
+        return ops.sample(vals, *self._sampling(meta), ids=ids)
+
+    def tokens_full(self, meta: StepMeta, hf: torch.Tensor) -> torch.Tensor:
+        """Tail fallback (a row needs more than CAND candidates): full LM head + sampler."""
+        return ops.sample(self.model.head_logits(hf), *self._sampling(meta))
+
+
+def vp_ok(meta: Optional[StepMeta]) -> bool:
+    """The vocab-parallel head serves a step when every row's top-k fits in CAND
+    candidates per rank (greedy included); top_k <= 0 (full-vocab sampling) falls back."""
+    if meta is None or meta.top_k is None or meta.num_seqs == 0:
+        return False
+    tk = np.asarray(meta.top_k)
+    greedy = np.asarray(meta.temperature) <= 0
+    return bool(np.all(greedy | ((tk >= 1) & (tk <= CAND))))
+
+
+H_VP = 13          # ctrl header word: 1 = vocab-parallel head for this step
 
 
 def _stage_capacity_blocks(cfg, plan, block_size, device, kv_fraction, cap_tokens):
@@ -101,20 +176,49 @@ def _stage_capacity_blocks(cfg, plan, block_size, device, kv_fraction, cap_token
                            kv_fraction, cap_tokens=cap_tokens)
 
 
-class PipelineHead:
-    """Rank-0 driver: scheduler + tick loop over M = N + 1 microbatches.
+class _Host:
+    """Tokens on their way to the head's host: a pinned copy + event (sampled on rank 0),
+    an exchange handle (received from the tail), or already a host array."""
 
-    Tick k: consume the tokens of the microbatch started at tick k - M (they arrived in the
-    exchange of tick k - 1), schedule that microbatch's next step, broadcast its metadata
-    on the control plane, post this tick's exchange {hidden of tick k-1 -> stage 1, ids of
-    the microbatch started at k - N <- tail}, then replay stage 0 for tick k."""
+    def __init__(self, dev_tokens=None, handle=None, array=None):
+        self.handle, self.array = handle, array
+        if dev_tokens is not None and not dev_tokens.is_cuda:
+            self.array = dev_tokens.numpy()
+        elif dev_tokens is not None:
+            self.host = torch.empty(dev_tokens.shape, dtype=torch.int32, pin_memory=True)
+            self.host.copy_(dev_tokens, non_blocking=True)
+            self.ev = torch.cuda.Event()
+            self.ev.record()
+
+    def get(self, ch) -> np.ndarray:
+        if self.array is not None:
+            return self.array
+        if self.handle is not None:
+            return ch.to_host(self.handle)
+        self.ev.synchronize()
+        return self.host.numpy()
+
+
+class PipelineHead:
+    """Rank-0 driver: scheduler + tick loop over M microbatches (stage 0 is also this rank).
+
+    Tick k (all ranks exchange once, anti-diagonal: rank r runs the layers of the microbatch
+    the head started at tick k - r):
+      consume tokens of the microbatch started at k - M, schedule its next step, broadcast
+      the step's metadata (control plane), post exchange(k), then
+        vocab-parallel head: candidates of microbatch k - N from its final hidden (received
+          from the tail); merge every rank's candidates of microbatch k - 1 - N and sample;
+        tail head (fallback): tokens of microbatch k - N arrive from the tail;
+      and run stage 0's layers for tick k. M = N + 3 with the vocab-parallel head (tokens
+      exist on rank 0 one tick after the candidates), N + 1 otherwise."""
 
     def __init__(self, stage: StageWorker, channel, scheduler: Scheduler, tokenizer,
                  microbatches: Optional[int] = None):
         self.stage, self.ch, self.sched, self.tok = stage, channel, scheduler, tokenizer
         self.N = channel.world
-        self.M = microbatches or num_microbatches(self.N)
-        assert self.N == 1 or self.M > self.N, "need M > N microbatches"
+        self.vp = stage.vocab_parallel
+        self.M = microbatches or num_microbatches(self.N, self.vp)
+        assert self.N == 1 or self.M >= self.N + (3 if self.vp else 1), "too few microbatches"
         self.stats = EngineStats()
 
     def _account(self, meta: StepMeta):
@@ -126,44 +230,65 @@ class PipelineHead:
             self.stats.decode_steps += 1
 
     def run_session(self) -> List[RequestOutput]:
-        N, M, k = self.N, self.M, 0
-        started: Dict[int, StepMeta] = {}          # start tick -> meta awaiting its tokens
-        tokens: Dict[int, object] = {}             # start tick -> exchange handle / host ids
-        prev_out = None
+        N, M, k, ch, st = self.N, self.M, 0, self.ch, self.stage
+        started: Dict[int, Tuple[StepMeta, bool]] = {}   # start tick -> (meta, vocab-parallel)
+        tokens: Dict[int, _Host] = {}
+        prev_out = None                # stage-0 output of tick k-1 (hidden -> rank 1)
+        my_cand = None                 # own candidates of microbatch k-1-N (vocab-parallel)
+        D = self.stage.cfg.hidden_size
         while True:
             t0 = time.perf_counter()
             s = k - M
             if s in started:
-                m = started.pop(s)
-                h = tokens.pop(s)
-                self.sched.update(m, h if isinstance(h, np.ndarray) else self.ch.to_host(h))
+                m, _ = started.pop(s)
+                self.sched.update(m, tokens.pop(s).get(ch))
                 self.stats.tokens_out += m.num_seqs
             meta = self.sched.schedule(k % M) if self.sched.has_work() else None
             if meta is None and not started and not self.sched.has_work():
                 break
             if N == 1:
                 if meta is not None:
-                    out = self.stage.compute(meta, None)
-                    started[k], tokens[k] = meta, out.cpu().numpy()
+                    out = st.compute(meta, None)
+                    started[k] = (meta, False)
+                    tokens[k] = _Host(array=out.cpu().numpy())
                     self._account(meta)
                 k += 1
                 continue
-            self.ch.broadcast_ctrl(*_ctrl(EMPTY if meta is None else meta.kind, k, meta))
-            ret = started.get(k - N)
-            h = self.ch.exchange(prev_out, None if ret is None else (ret.num_seqs,),
-                                 torch.int32)
+            vp_k = self.vp and vp_ok(meta)
+            h, p = _ctrl(EMPTY if meta is None else meta.kind, k, meta)
+            h[H_VP] = int(vp_k)
+            ch.broadcast_ctrl(h, p)
+            ret = started.get(k - N)             # its last stage ran at tick k - 1
+            smp = started.get(k - 1 - N)         # its candidates were made at tick k - 1
+            recvs = []
             if ret is not None:
-                tokens[k - N] = h
+                recvs.append(((ret[0].num_seqs, D), ch.dtype, N - 1, 2) if ret[1] else
+                             ((ret[0].num_seqs,), torch.int32, N - 1, 2))
+            if smp is not None and smp[1]:
+                recvs += [((smp[0].num_seqs, 2 * CAND), torch.int32, q, 3) for q in range(1, N)]
+            hd = ch.exchange_many([(prev_out, 1, 1)] if prev_out is not None else [], recvs)
+            cand_now = None
+            if ret is not None:
+                if ret[1]:
+                    hf = ch.wait_all(hd)[0]
+                    cand_now = st.candidates(hf)
+                else:
+                    tokens[k - N] = _Host(handle=(hd[0][0], hd[1]))
+            if smp is not None and smp[1]:
+                bufs = ch.wait_all(hd)
+                tok = st.sample_candidates(smp[0], [my_cand] + bufs[-(N - 1):])
+                tokens[k - 1 - N] = _Host(dev_tokens=tok)
+            my_cand = cand_now
             prev_out = None
             if meta is not None:
-                prev_out = self.stage.compute(meta, None)
-                started[k] = meta
+                prev_out = st.compute(meta, None)
+                started[k] = (meta, vp_k)
                 self._account(meta)
             self.stats.busy_s += time.perf_counter() - t0
             k += 1
         if N > 1:
-            self.ch.broadcast_ctrl(*_ctrl(STOP, k))
-            self.ch.flush()
+            ch.broadcast_ctrl(*_ctrl(STOP, k))
+            ch.flush()
         outs = []
         for seq in self.sched.pop_finished():
             o = seq_to_output(seq, self.tok)
@@ -180,10 +305,17 @@ class PipelineHead:
 
 def serve_session(stage: StageWorker, channel) -> int:
     """Non-head rank r: every tick of one head session; returns STOP or SHUTDOWN.
-    At tick k it runs the microbatch the head started at tick k - r (control message k - r,
-    received in order). The host never waits on this GPU: receive, replay and send are all
-    stream-ordered."""
-    r, k, prev_out = channel.rank, 0, None
+    Tick k: layers of the microbatch started at k - r (control message k - r, received in
+    order), with the vocab-parallel head also the candidates of microbatch k - N; the tail
+    returns either its final hidden (to every rank) or its sampled tokens (to rank 0). The
+    host never waits on this GPU: receives, replays and sends are all stream-ordered."""
+    r, N, k = channel.rank, channel.world, 0
+    tail = r == N - 1
+    D = stage.cfg.hidden_size
+    metas: Dict[int, Tuple[StepMeta, bool]] = {}
+    prev_out = None                 # my layer output of tick k-1 (hidden / tokens / final hidden)
+    prev_vp = False
+    my_cand = None                  # my candidates of microbatch k-1-N
     while True:
         meta = None
         if k >= r:
@@ -194,11 +326,41 @@ def serve_session(stage: StageWorker, channel) -> int:
                 return kind
             if kind in (PREFILL, DECODE):
                 meta = StepMeta.unpack(h, p)
-        rshape = None if meta is None else (meta.num_tokens, stage.cfg.hidden_size)
-        hd = channel.exchange(prev_out, rshape)
-        prev_out = None
+                metas[k - r] = (meta, bool(h[H_VP]))
+        ret = metas.get(k - N)
+        smp = metas.get(k - 1 - N)
+        sends, recvs = [], []
+        if not tail and prev_out is not None:
+            sends.append((prev_out, r + 1, 1))
+        if tail and prev_out is not None:
+            if prev_vp:
+                sends += [(prev_out, q, 2) for q in range(N - 1)]
+            else:
+                sends.append((prev_out, 0, 2))
+        if smp is not None and smp[1] and my_cand is not None:
+            sends.append((my_cand, 0, 3))
         if meta is not None:
-            prev_out = stage.compute(meta, channel.wait(hd))
+            recvs.append(((meta.num_tokens, D), channel.dtype, r - 1, 1))
+        if ret is not None and ret[1] and not tail:
+            recvs.append(((ret[0].num_seqs, D), channel.dtype, N - 1, 2))
+        hd = channel.exchange_many(sends, recvs)
+        bufs = channel.wait_all(hd) if recvs else []
+        # candidates first: on the tail they read the final hidden of tick k-1 (prev_out),
+        # which this tick's replay overwrites
+        cand_now = None
+        if ret is not None and ret[1]:
+            hf = prev_out if tail else bufs[-1]
+            cand_now = stage.candidates(hf)
+        my_cand = cand_now
+        prev_out, prev_vp = None, False
+        if meta is not None:
+            out = stage.compute(meta, bufs[0])
+            vp_m = metas[k - r][1]
+            if tail and not vp_m and stage.vocab_parallel:
+                out = stage.tokens_full(meta, out)        # a row needs the whole vocabulary
+            prev_out, prev_vp = out, vp_m
+        for old in [t for t in metas if t < k - 1 - N]:
+            del metas[old]
         k += 1
 
 
@@ -212,19 +374,22 @@ def run_stage_loop(stage: StageWorker, channel) -> None:
 def build_stage(cfg: ModelConfig, rank: int, world: int, device, max_batch: int,
                 max_model_len: int, block_size: int = 16, kv_fraction: float = 0.85,
                 policy: str = "balanced", seed: int = 0, use_graphs=None,
-                num_blocks: Optional[int] = None, dtype=torch.bfloat16):
-    plans = plan_stages(cfg, world, policy)
+                num_blocks: Optional[int] = None, dtype=torch.bfloat16,
+                vocab_parallel: bool = False, microbatches: Optional[int] = None):
+    plans = plan_stages(cfg, world, policy, head_on_all=vocab_parallel)
     plan = plans[rank]
     table_width = -(-max_model_len // block_size)
+    M = microbatches or num_microbatches(world, vocab_parallel)
     if num_blocks is None:
         cap = _stage_capacity_blocks(cfg, plan, block_size, device, kv_fraction,
-                                     cap_tokens=max((world + 1) * max_batch * max_model_len, 1 << 16))
+                                     cap_tokens=max(M * max_batch * max_model_len, 1 << 16))
         t = torch.tensor([cap], dtype=torch.int64,
                          device=device if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MIN)     # block ids are global: same pool size
         num_blocks = int(t.item())
+    vs = vocab_slices(cfg.vocab_size, world)[rank] if vocab_parallel else None
     stage = StageWorker(cfg, plan, device, num_blocks, block_size, max_batch, table_width,
-                        seed=seed, use_graphs=use_graphs, dtype=dtype)
+                        seed=seed, use_graphs=use_graphs, dtype=dtype, vocab_slice=vs)
     return stage, plans, num_blocks, table_width
 
 
@@ -234,16 +399,19 @@ class DistributedPipelineEngine:
     def __init__(self, model: str, device, max_batch: int = 256, max_model_len: int = 2048,
                  block_size: int = 16, policy: str = "balanced", seed: int = 0,
                  use_graphs=None, max_prefill_tokens: int = 16384, num_blocks=None,
-                 dtype=torch.bfloat16):
+                 dtype=torch.bfloat16, vocab_parallel: Optional[bool] = None):
         self.rank, self.world = init_distributed(device=torch.device(device)
                                                  if torch.device(device).type == "cuda" else None)
         self.cfg = get_config(model)
         self.device = torch.device(device)
+        self.vocab_parallel = (use_vocab_parallel(self.cfg, self.world)
+                               if vocab_parallel is None else vocab_parallel)
+        self.microbatches = num_microbatches(self.world, self.vocab_parallel)
         self.stage, self.plans, nb, tw = build_stage(
             self.cfg, self.rank, self.world, self.device, max_batch, max_model_len, block_size,
-            policy=policy, seed=seed, use_graphs=use_graphs, num_blocks=num_blocks, dtype=dtype)
+            policy=policy, seed=seed, use_graphs=use_graphs, num_blocks=num_blocks, dtype=dtype,
+            vocab_parallel=self.vocab_parallel, microbatches=self.microbatches)
         self.channel = PipeChannel(self.device, dtype=dtype)
-        self.microbatches = num_microbatches(self.world)
         self.head = None
         if self.rank == 0:
             bm = BlockManager(nb, block_size)

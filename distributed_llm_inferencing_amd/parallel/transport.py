@@ -110,20 +110,24 @@ class PipeChannel:
         return h.numpy(), p.numpy()
 
     # ------------------------------------------------------------------ data plane
-    def exchange(self, send: Optional[torch.Tensor], recv_shape: Optional[tuple],
-                 recv_dtype=None):
-        """Post this tick's grouped send/recv. ``send`` is snapshotted (graph outputs are
-        static buffers). Returns a handle for ``wait`` / ``to_host``, or None."""
-        ops, keep, buf = [], [], None
+    def exchange_many(self, sends, recvs):
+        """Post this tick's grouped exchange. ``sends`` = [(tensor, peer, tag)] (snapshotted:
+        graph outputs are static buffers), ``recvs`` = [(shape, dtype, peer, tag)]. Tags
+        keep several messages between one pair apart (gloo matches per (peer, tag); RCCL
+        ignores them). Returns (recv buffers, record) for ``wait_all``, or None."""
+        ops, keep, bufs = [], [], []
         with trace_range("pp.exchange"):
-            if send is not None and send.numel() > 0:
-                snap = send.clone() if self.nccl else send.to("cpu")
+            for t, peer, tag in sends:
+                if t is None or t.numel() == 0:
+                    continue
+                snap = t.clone() if self.nccl else t.to("cpu")
+                snap = snap.contiguous()
                 keep.append(snap)
-                ops.append(dist.P2POp(dist.isend, snap.contiguous(), self.next))
-            if recv_shape is not None:
-                buf = torch.empty(recv_shape, dtype=recv_dtype or self.dtype,
-                                  device=self.data_device)
-                ops.append(dist.P2POp(dist.irecv, buf, self.prev))
+                ops.append(dist.P2POp(dist.isend, snap, peer, tag=tag))
+            for shape, dt, peer, tag in recvs:
+                buf = torch.empty(shape, dtype=dt, device=self.data_device)
+                bufs.append(buf)
+                ops.append(dist.P2POp(dist.irecv, buf, peer, tag=tag))
             if not ops:
                 return None
             works = dist.batch_isend_irecv(ops)
@@ -131,7 +135,24 @@ class PipeChannel:
         self._inflight.append(rec)
         while len(self._inflight) > self.max_pending:
             self._finish(self._inflight.popleft())
-        return buf, rec
+        return bufs, rec
+
+    def exchange(self, send: Optional[torch.Tensor], recv_shape: Optional[tuple],
+                 recv_dtype=None):
+        """Ring-only form: {send -> next, receive <- prev} (tag 1)."""
+        r = self.exchange_many([(send, self.next, 1)] if send is not None else [],
+                               [(recv_shape, recv_dtype or self.dtype, self.prev, 1)]
+                               if recv_shape is not None else [])
+        if r is None:
+            return None
+        bufs, rec = r
+        return (bufs[0] if bufs else None), rec
+
+    def wait_all(self, handle):
+        """Receive buffers of an exchange (on RCCL a stream dependency, not a host wait)."""
+        bufs, rec = handle
+        self._finish(rec)
+        return [b if b.device == self.device else b.to(self.device) for b in bufs]
 
     def _finish(self, rec) -> None:
         # a gloo Work must be waited exactly once (a second wait on a completed receive

@@ -89,7 +89,9 @@ def _min_max_partition(costs: Sequence[float], n: int, head_extra: float,
 
 def plan_stages(cfg: ModelConfig, num_stages: int, policy: str = "balanced",
                 dtype_bytes: int = 2, hbm_bytes: int = HBM_BYTES,
-                kv_reserve_frac: float = 0.1) -> List[StagePlan]:
+                kv_reserve_frac: float = 0.1, head_on_all: bool = False) -> List[StagePlan]:
+    """``head_on_all``: the LM head runs vocab-parallel on every stage (parallel/pipeline.py),
+    so its cost is the same on each stage and the layers split evenly."""
     L = cfg.num_layers
     layer_b = cfg.layer_param_count() * dtype_bytes
     embed_b = cfg.embed_param_count() * dtype_bytes
@@ -101,7 +103,7 @@ def plan_stages(cfg: ModelConfig, num_stages: int, policy: str = "balanced",
     elif policy == "balanced":
         # decode step time ~ bytes streamed; the LM head is streamed, the embedding gathered;
         # the sampler over the vocab costs roughly one more pass over fp32 logits
-        tail_time = head_b + 4 * cfg.vocab_size * 256
+        tail_time = 0 if head_on_all else head_b + 4 * cfg.vocab_size * 256
         ranges = _min_max_partition([float(layer_b)] * L, num_stages, 0.0, float(tail_time))
     else:
         raise ValueError(f"unknown policy {policy}")
@@ -111,7 +113,10 @@ def plan_stages(cfg: ModelConfig, num_stages: int, policy: str = "balanced",
         wb = (e - s) * layer_b + (embed_b if first else 0) + (head_b if last else 0)
         if last and cfg.tie_embeddings and not first:
             wb += embed_b
-        tc = (e - s) * layer_b + ((head_b + 4 * cfg.vocab_size * 256) if last else 0)
+        if head_on_all:
+            tc = (e - s) * layer_b + (head_b + 4 * cfg.vocab_size * 256) / len(ranges)
+        else:
+            tc = (e - s) * layer_b + ((head_b + 4 * cfg.vocab_size * 256) if last else 0)
         plans.append(StagePlan(i, s, e, wb, float(tc), first, last))
     limit = hbm_bytes * (1 - kv_reserve_frac)
     for p in plans:

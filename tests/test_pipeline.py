@@ -58,9 +58,9 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, model, q):
+def _worker(rank, world, port, model, q, vp="auto"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
-                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), DLI_PP_VOCAB_PARALLEL=vp)
     torch.set_num_threads(1)
     import torch.distributed as dist
     from distributed_llm_inferencing_amd.parallel.pipeline import DistributedPipelineEngine
@@ -74,6 +74,10 @@ def _worker(rank, world, port, model, q):
         # a second session on the same ring (sessions start/stop cleanly)
         res.append([o.all_ids for o in eng.generate(PROMPTS[:2], SamplingParams(
             max_length=12, do_sample=False, ignore_eos=True))])
+        # top_k = 0 (full-vocabulary top-p) falls back to the tail's LM head per step
+        res.append([o.all_ids for o in eng.generate(PROMPTS[:3], SamplingParams(
+            max_length=16, top_k=0, top_p=0.9, seed=5, ignore_eos=True))])
+        res.append(eng.vocab_parallel)
         eng.shutdown()
         q.put(res)
     else:
@@ -82,13 +86,17 @@ def _worker(rank, world, port, model, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_ring_matches_single_stage(world):
+@pytest.mark.parametrize("world,vp", [(2, "0"), (3, "0"), (2, "1"), (4, "auto")])
+def test_gloo_ring_matches_single_stage(world, vp):
+    """Pipeline over gloo ranks == single-stage engine, token for token (greedy, sampled,
+    second session, full-vocab fallback), with the tail LM head and with the vocab-parallel
+    head (every rank scores 1/N of the vocabulary; rank 0 samples from the candidates)."""
     model = "llama-tiny"
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, model, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, model, q, vp))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = q.get(timeout=300)
@@ -102,6 +110,9 @@ def test_gloo_ring_matches_single_stage(world):
                     num_blocks=64)
     assert res[2] == [o.all_ids for o in eng.generate(PROMPTS[:2], SamplingParams(
         max_length=12, do_sample=False, ignore_eos=True))]
+    assert res[3] == [o.all_ids for o in eng.generate(PROMPTS[:3], SamplingParams(
+        max_length=16, top_k=0, top_p=0.9, seed=5, ignore_eos=True))]
+    assert res[4] == (vp == "1" or (vp == "auto" and world >= 4))
 
 
 def _ep_worker(rank, world, port, q):
