@@ -353,3 +353,26 @@ def test_moe_mlp_prefill_blas_path(gpu, monkeypatch):
     wd = rnd(E, D, F, dev=gpu, scale=0.05)
     close(ops.moe_mlp(x, wgu, wd, rw, rids), R.moe_mlp(x, wgu, wd, rw, rids),
           rtol=3e-2, atol=3e-2)
+
+
+def test_vocab_parallel_candidates_sample_like_full_vocab(gpu):
+    """Vocab-parallel head: per-slice top-64 candidates (ascending ids) merged on rank 0 and
+    sampled with the same seeds give the same tokens as sampling the full vocabulary."""
+    torch.manual_seed(14)
+    B, D, V, N = 64, 256, 8000, 4
+    h = rnd(B, D, dev=gpu)
+    w = rnd(V, D, dev=gpu, scale=0.2)
+    full = ops.linear(h, w, epi="f32")
+    bounds = [round(i * V / N) for i in range(N + 1)]
+    vals, ids = zip(*[ops.head_candidates(h, w[bounds[r]:bounds[r + 1]].contiguous(), bounds[r],
+                                          64) for r in range(N)])
+    vals, ids = torch.cat(vals, 1), torch.cat(ids, 1)
+    assert torch.all(ids[:, 1:] > ids[:, :-1])                # ascending token ids
+    temp = torch.full((B,), 0.8, device=gpu)
+    topk = torch.full((B,), 50, device=gpu, dtype=torch.int32)
+    topk[::7] = 1                                             # some greedy rows
+    topp = torch.full((B,), 0.95, device=gpu)
+    seeds = torch.arange(B, device=gpu, dtype=torch.int64) * 7919 + 11
+    a = ops.sample(full, temp, topk, topp, seeds)
+    b = ops.sample(vals, temp, topk, topp, seeds, ids=ids)
+    assert torch.equal(a, b)
