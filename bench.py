@@ -54,11 +54,12 @@ def make_prompts(n, prompt_len, vocab, seed):
     return [rng.integers(lo, hi, size=prompt_len).tolist() for _ in range(n)]
 
 
-def run_single(args):
+def run_single(args, barrier=None):
     from distributed_llm_inferencing_amd.engine import SamplingParams
     from distributed_llm_inferencing_amd.engine.llm_engine import LLMEngine
 
-    dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
+    dev = (torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available()
+           else torch.device("cpu"))
     eng = LLMEngine(args.model, device=str(dev), max_batch=args.batch,
                     max_model_len=args.max_model_len, seed=0,
                     max_prefill_tokens=max(args.batch * args.prompt_len, 8192))
@@ -75,6 +76,8 @@ def run_single(args):
         wave(10_000 + w)
     if dev.type == "cuda":
         torch.cuda.synchronize()
+    if barrier is not None:
+        barrier()
     t0 = time.perf_counter()
     toks, lats = 0, []
     for s in range(args.steps):
@@ -83,9 +86,38 @@ def run_single(args):
         lats += l
     if dev.type == "cuda":
         torch.cuda.synchronize()
+    if barrier is not None:
+        barrier()
     dt = time.perf_counter() - t0
     return {"tokens": toks, "seconds": dt, "latencies": lats, "global_batch": args.batch,
             "parallelism": "single", "engine": eng.stats.snapshot()}
+
+
+def run_data_parallel(args, world, rank):
+    """Each rank serves its own --batch requests on its own GPU with the single-GPU engine
+    (the DP-replica deployment of cli.py serve-cluster); waves are timed between barriers
+    and the slowest rank's time is used for the whole-node rate."""
+    import torch.distributed as dist
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)
+    from distributed_llm_inferencing_amd.parallel.transport import init_distributed
+    init_distributed(device=torch.device("cuda", local) if torch.cuda.is_available() else None)
+    res = run_single(args, barrier=dist.barrier)
+    cdev = torch.device("cuda", local) if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([res["seconds"], res["tokens"]], dtype=torch.float64, device=cdev)
+    mx = t.clone()
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    lats = [None] * world
+    dist.all_gather_object(lats, res["latencies"])
+    dist.barrier()
+    dist.destroy_process_group()
+    if rank != 0:
+        return None
+    return {"tokens": float(t[1].item()), "seconds": float(mx[0].item()),
+            "latencies": [x for l in lats for x in l], "global_batch": args.batch * world,
+            "parallelism": f"dp{world}"}
 
 
 def run_pipeline(args, world, rank):
@@ -96,6 +128,8 @@ def run_pipeline(args, world, rank):
     if mode == "ep":      # Mixtral: DP attention + experts sharded over ranks (all-to-all)
         from distributed_llm_inferencing_amd.parallel.expert import bench_expert_parallel
         return bench_expert_parallel(args, world, rank, make_prompts)
+    if mode == "dp":      # N independent replicas (serve-cluster --dp N), no inter-GPU traffic
+        return run_data_parallel(args, world, rank)
     if mode == "tp":      # ablation: Megatron-style head/FFN sharding, 2 all-reduces/layer
         from distributed_llm_inferencing_amd.parallel.tensor import bench_tensor_parallel
         return bench_tensor_parallel(args, world, rank, make_prompts)
@@ -113,9 +147,10 @@ def main():
     ap.add_argument("--prompt-len", type=int, default=32)
     ap.add_argument("--max-length", type=int, default=100)
     ap.add_argument("--max-model-len", type=int, default=512)
-    ap.add_argument("--mode", default="auto", choices=["auto", "pp", "ep", "tp"],
-                    help="N>1: pp = layer-sharded pipeline (dense), ep = expert parallel (MoE),"
-                         " tp = tensor-parallel ablation (dense)")
+    ap.add_argument("--mode", default="auto", choices=["auto", "pp", "ep", "tp", "dp"],
+                    help="N>1: pp = layer-sharded pipeline (dense, default), ep = expert "
+                         "parallel (MoE), tp = tensor-parallel ablation, dp = independent "
+                         "replicas")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
