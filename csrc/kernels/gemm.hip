@@ -2,8 +2,8 @@
 // SURVEY.md §2.4 K4/K9-K12 (dense projections) and K16 (MoE grouped GEMM).
 //
 // Structure (cdna_hip_programming.md §5):
-//  * 256 threads = 4 waves in a 2x2 grid; block tile BM x BN x 64; wave tile (BM/2) x (BN/2)
-//    built from v_mfma_f32_16x16x32_bf16 (the bf16 shape that holds the higher clock on random
+//  * WM x WN waves (2x2 = 256 threads, or 2x4 / 4x2 = 512 threads for 256-wide tiles); block
+//    tile BM x BN x 64; wave tile (BM/WM) x (BN/WN) built from v_mfma_f32_16x16x32_bf16 (the bf16 shape that holds the higher clock on random
 //    data, MI355X_MICROARCH.md 'DVFS give-back' item 7).
 //  * global -> LDS by global_load_lds_dwordx4 (16 B per lane, no VGPR round trip), 2 LDS
 //    buffers: the next K-tile's DMA is issued before the current tile's ds_reads + MFMAs.
@@ -21,7 +21,6 @@
 // gate/up weight (output width N/2), 3 bias + tanh-GELU, 4 bias.
 #include "common.h"
 
-#define GEMM_THREADS 256
 #define BK 64
 
 enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_SILU = 2, EPI_BIAS_GELU = 3, EPI_BIAS = 4 };
@@ -53,12 +52,14 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-template <int BM, int BN, int EPI, int NS>
-__global__ void __launch_bounds__(GEMM_THREADS) gemm_bf16_kernel(
+template <int BM, int BN, int EPI, int NS, int WM, int WN>
+__global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(
     const u16* __restrict__ A, int lda, const u16* __restrict__ W, int ldw,
     void* __restrict__ C, int ldc, int M, int N, int K, int k_split_len,
     const u16* __restrict__ bias, float* __restrict__ ws, const int* __restrict__ group_off) {
-  constexpr int MI = BM / 32, NI = BN / 32;        // 16x16 blocks per wave (wave = BM/2 x BN/2)
+  constexpr int NW = WM * WN;                      // waves: WM along M x WN along N
+  constexpr int TM = BM / WM, TN = BN / WN;        // wave tile
+  constexpr int MI = TM / 16, NI = TN / 16;        // 16x16 MFMA blocks per wave
   constexpr int A_BYTES = BM * BK * 2, W_BYTES = BN * BK * 2;
   constexpr int BUF = A_BYTES + W_BYTES;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -82,23 +83,25 @@ __global__ void __launch_bounds__(GEMM_THREADS) gemm_bf16_kernel(
   const int nk = min(k_split_len, K - kb) / BK;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WN, wn = wid % WN;
   const u16* Ab = A + (long)row0 * lda;
 
   // ---- per-lane glds source pointers (row clamped in range; swizzled chunk)
-  constexpr int A_INSTR = BM / 32, W_INSTR = BN / 32;   // glds per wave per K-tile
+  // one glds wave-instruction stages 8 rows x 128 B; all NW waves share each tile
+  constexpr int A_INSTR = BM / (8 * NW), W_INSTR = BN / (8 * NW);
+  static_assert(A_INSTR * 8 * NW == BM && W_INSTR * 8 * NW == BN, "tile vs waves");
   const u16* a_src[A_INSTR];
   const u16* w_src[W_INSTR];
 #pragma unroll
   for (int i = 0; i < A_INSTR; ++i) {
-    const int r = (i * 4 + wid) * 8 + (lane >> 3);
+    const int r = (i * NW + wid) * 8 + (lane >> 3);
     const int c = (lane & 7) ^ ((r >> 1) & 7);
     const int gr = min(m0 + r, Mg - 1);
     a_src[i] = Ab + (long)gr * lda + kb + c * 8;
   }
 #pragma unroll
   for (int i = 0; i < W_INSTR; ++i) {
-    const int r = (i * 4 + wid) * 8 + (lane >> 3);
+    const int r = (i * NW + wid) * 8 + (lane >> 3);
     const int c = (lane & 7) ^ ((r >> 1) & 7);
     const int gr = min(n0 + r, N - 1);
     w_src[i] = Wg + (long)gr * ldw + kb + c * 8;
@@ -108,11 +111,11 @@ __global__ void __launch_bounds__(GEMM_THREADS) gemm_bf16_kernel(
 #pragma unroll
     for (int i = 0; i < A_INSTR; ++i)
       __builtin_amdgcn_global_load_lds((gbl_void*)(a_src[i] + kt * BK),
-                                       (lds_void*)(base + (i * 4 + wid) * 1024), 16, 0, 0);
+                                       (lds_void*)(base + (i * NW + wid) * 1024), 16, 0, 0);
 #pragma unroll
     for (int i = 0; i < W_INSTR; ++i)
       __builtin_amdgcn_global_load_lds((gbl_void*)(w_src[i] + kt * BK),
-                                       (lds_void*)(base + A_BYTES + (i * 4 + wid) * 1024), 16,
+                                       (lds_void*)(base + A_BYTES + (i * NW + wid) * 1024), 16,
                                        0, 0);
   };
 
@@ -126,9 +129,9 @@ __global__ void __launch_bounds__(GEMM_THREADS) gemm_bf16_kernel(
   const int fr = lane & 15, fq = lane >> 4;
   int a_row[MI], w_row[NI];
 #pragma unroll
-  for (int i = 0; i < MI; ++i) a_row[i] = wm * (BM / 2) + i * 16 + fr;
+  for (int i = 0; i < MI; ++i) a_row[i] = wm * TM + i * 16 + fr;
 #pragma unroll
-  for (int j = 0; j < NI; ++j) w_row[j] = wn * (BN / 2) + j * 16 + fr;
+  for (int j = 0; j < NI; ++j) w_row[j] = wn * TN + j * 16 + fr;
 
   auto compute = [&](int buf) {
     const char* abuf = smem + buf * BUF;
@@ -196,11 +199,11 @@ __global__ void __launch_bounds__(GEMM_THREADS) gemm_bf16_kernel(
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * (BM / 2) + 16 * i + 4 * fq + r;
+        const int row = m0 + wm * TM + 16 * i + 4 * fq + r;
         if (row >= Mg) continue;
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
-          const int col = n0 + wn * (BN / 2) + 16 * j + fr;
+          const int col = n0 + wn * TN + 16 * j + fr;
           if (col < N) slab[(long)(row0 + row) * N + col] = acc[i][j][r];
         }
       }
@@ -212,11 +215,11 @@ __global__ void __launch_bounds__(GEMM_THREADS) gemm_bf16_kernel(
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * (BM / 2) + 16 * i + 4 * fq + r;
+        const int row = m0 + wm * TM + 16 * i + 4 * fq + r;
         if (row >= Mg) continue;
 #pragma unroll
         for (int j = 0; j < NI; j += 2) {
-          const int gcol = n0 + wn * (BN / 2) + 16 * j;       // first gate row of the pair
+          const int gcol = n0 + wn * TN + 16 * j;       // first gate row of the pair
           if (gcol < N) {
             const int f = (gcol >> 5) * 16 + fr;
             const float v = silu_f(acc[i][j][r]) * acc[i][j + 1][r];
@@ -230,11 +233,11 @@ __global__ void __launch_bounds__(GEMM_THREADS) gemm_bf16_kernel(
   for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int row = m0 + wm * (BM / 2) + 16 * i + 4 * fq + r;
+      const int row = m0 + wm * TM + 16 * i + 4 * fq + r;
       if (row >= Mg) continue;
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
-        const int col = n0 + wn * (BN / 2) + 16 * j + fr;
+        const int col = n0 + wn * TN + 16 * j + fr;
         if (col < N) store_pair_or_one<EPI>(C, ldc, row0 + row, col, acc[i][j][r], bias);
       }
     }
@@ -263,10 +266,11 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(void* __restrict__ C
   }
 }
 
-template <int BM, int BN, int EPI, int NS>
+template <int BM, int BN, int EPI, int NS, int WM = 2, int WN = 2>
 static int launch_cfg(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M,
                       int N, int K, int splits, const void* bias, void* ws,
                       const int* group_off, int groups, hipStream_t st) {
+  if (EPI == EPI_SILU && (BN / WN) % 32) return (int)hipErrorInvalidValue;  // gate/up pairs
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   int ksl = K / splits;
   ksl = (ksl / BK) * BK;
@@ -274,12 +278,12 @@ static int launch_cfg(const void* A, int lda, const void* W, int ldw, void* C, i
   const size_t lds = NS * (size_t)(BM + BN) * BK * 2;
   static bool attr_done = false;                   // > 64 KiB dynamic LDS needs the opt-in
   if (!attr_done) {
-    hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, EPI, NS>,
+    hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, EPI, NS, WM, WN>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_done = true;
   }
   dim3 grid(tiles, splits, groups);
-  gemm_bf16_kernel<BM, BN, EPI, NS><<<grid, GEMM_THREADS, lds, st>>>(
+  gemm_bf16_kernel<BM, BN, EPI, NS, WM, WN><<<grid, 64 * WM * WN, lds, st>>>(
       (const u16*)A, lda, (const u16*)W, ldw, C, ldc, M, N, K, ksl, (const u16*)bias,
       (float*)ws, group_off);
   if (splits > 1 && C != nullptr) {       // C == nullptr: leave the fp32 partial slabs for a
@@ -303,6 +307,14 @@ static int dispatch_tile(int tile_cfg, const void* A, int lda, const void* W, in
     DLI_CFG(5, 64, 64, 3) DLI_CFG(6, 64, 128, 3) DLI_CFG(7, 128, 128, 3) DLI_CFG(8, 128, 256, 3)
     DLI_CFG(9, 256, 128, 3)
     DLI_CFG(10, 192, 128, 2) DLI_CFG(11, 192, 128, 3) DLI_CFG(12, 160, 128, 2)
+#define DLI_CFG8(id, bm, bn, ns, wm, wn) \
+    case id: return launch_cfg<bm, bn, EPI, ns, wm, wn>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
+    // 8 waves (512 threads): 256-wide tiles halve the L2 re-reads of A/W at M >= 256
+    DLI_CFG8(13, 256, 256, 2, 2, 4) DLI_CFG8(14, 256, 128, 2, 4, 2) DLI_CFG8(15, 128, 256, 2, 2, 4)
+    DLI_CFG8(16, 256, 128, 3, 4, 2) DLI_CFG8(17, 128, 256, 3, 2, 4)
+    // grid-filling shapes for N = 6144 / 4096 at M = 512 (4 x 64 = 256 workgroups)
+    DLI_CFG(18, 128, 96, 2) DLI_CFG(19, 128, 96, 3) DLI_CFG(20, 128, 64, 2) DLI_CFG(21, 128, 64, 3)
+#undef DLI_CFG8
 #undef DLI_CFG
     default: return (int)hipErrorInvalidValue;
   }
@@ -310,7 +322,9 @@ static int dispatch_tile(int tile_cfg, const void* A, int lda, const void* W, in
 
 // tile_cfg: 0=64x64 1=64x128 2=128x128 3=128x256 4=256x128 (2 LDS stages); 5..9 = the same
 // tiles with 3 LDS stages (one tile in flight across the barrier); 10/11 = 192x128 with 2/3
-// stages, 12 = 160x128 (MoE experts of ~130-190 rows in one pass). ws: fp32 [splits, M, N] when splits>1.
+// stages, 12 = 160x128 (MoE experts of ~130-190 rows in one pass); 13-17 = 8-wave tiles
+// 256x256, 256x128, 128x256 (2 stages) and 256x128, 128x256 (3 stages); 18/19 = 128x96 and
+// 20/21 = 128x64 with 2/3 stages. ws: fp32 [splits, M, N] when splits>1.
 // group_off (nullable): int[groups+1] row offsets; M is then the max rows of any group.
 extern "C" int dli_gemm(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M,
                         int N, int K, int epi, int tile_cfg, int splits, const void* bias,

@@ -26,7 +26,23 @@ import torch
 # buffers and one tile kept in flight across the K-step barrier (gemm.hip)
 TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256), 4: (256, 128),
          5: (64, 64), 6: (64, 128), 7: (128, 128), 8: (128, 256), 9: (256, 128),
-         10: (192, 128), 11: (192, 128), 12: (160, 128)}
+         10: (192, 128), 11: (192, 128), 12: (160, 128),
+         # 8 waves / 512 threads (fewer L2 re-reads of A and W at M >= 256)
+         13: (256, 256), 14: (256, 128), 15: (128, 256), 16: (256, 128), 17: (128, 256),
+         # grid-filling tiles for N = 6144 / 4096 at M = 512
+         18: (128, 96), 19: (128, 96), 20: (128, 64), 21: (128, 64)}
+TILE_WAVES = {13: (2, 4), 14: (4, 2), 15: (2, 4), 16: (4, 2), 17: (2, 4)}   # default 2 x 2
+
+
+def tile_ok(tile: int, epi: str) -> bool:
+    """The SiLU*up epilogue pairs 16-column gate/up blocks inside a wave's column range,
+    which must therefore be a multiple of 32."""
+    if epi != "silu_mul":
+        return True
+    bn = TILES[tile][1]
+    return (bn // TILE_WAVES.get(tile, (2, 2))[1]) % 32 == 0
+
+
 # "splitk": a plain GEMM whose fp32 partial slabs feed a fused reduce (ops.linear_add_rmsnorm,
 # ops.linear_rope_cache); planned/tuned separately (a non-split winner runs unfused).
 EPI = {"none": 0, "f32": 1, "silu_mul": 2, "bias_gelu": 3, "bias": 4, "splitk": 0}
@@ -127,7 +143,7 @@ def autotune_grouped(rows: int, w: torch.Tensor, epi: str, iters: int = 5, log=N
     best = None
     cands = []
     for tile in sorted(TILES):
-        if TILES[tile][0] > 2 * max(64, rows // E + 32):
+        if TILES[tile][0] > 2 * max(64, rows // E + 32) or not tile_ok(tile, epi):
             continue                                  # far taller than an expert's rows
         for splits in (1, 2, 4):                      # split-K for long-K expert GEMMs
             if splits == 1 or (K % (64 * splits) == 0 and K // splits >= 2048):
@@ -236,6 +252,8 @@ _tuned: set = set()
 def candidate_plans(M: int, N: int, K: int, epi: str):
     out = []
     for tile, (bm, bn) in TILES.items():
+        if not tile_ok(tile, epi):
+            continue
         if M <= 64 and bm > 64:
             continue
         if M > 512 and bm < 128:
@@ -247,6 +265,13 @@ def candidate_plans(M: int, N: int, K: int, epi: str):
             if splits > 1 and tiles * splits > 4 * NUM_CUS:
                 continue
             out.append(GemmPlan("dli", tile, splits))
-    if epi in ("none", "splitk", "silu_mul", "f32"):   # silu_mul: + our SiLU*up pass
+    # hipBLASLt (+ our epilogue pass for silu_mul) competes for decode-sized GEMMs only when
+    # DLI_GEMM_DECODE_BLAS=1: measured in-situ at M = 512 our kernels (8-wave 256x256 gate/up
+    # with fused SiLU, 3-stage 128-row tiles) run the decode layer as fast as the library mix
+    # (249.5 vs 257 us per layer, profiles/r1_final/), so the decode hot path stays entirely
+    # on hand-written MFMA kernels. Prefill-sized plain GEMMs (M >= LARGE_M) use hipBLASLt.
+    if (epi in ("none", "splitk", "silu_mul", "f32")
+            and os.environ.get("DLI_GEMM_DECODE_BLAS", "0") == "1"
+            and os.environ.get("DLI_GEMM_NO_BLAS") != "1"):
         out.append(GemmPlan("hipblaslt", 0, 1))
     return out

@@ -26,6 +26,10 @@ for s in "$@"; do
           step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- python bench.py --steps 1 --warmup 1
           python scripts/prof_summary.py gpurun_out/prof 40 --tail-ms 900 > gpurun_out/prof_summary.txt
           rm -f gpurun_out/prof/*trace.csv ;;
+    prof_noblas) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+          step prof_noblas 900 env DLI_GEMM_NO_BLAS=1 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_noblas -o bench -- python bench.py --steps 1 --warmup 1
+          python scripts/prof_summary.py gpurun_out/prof_noblas 40 --tail-ms 900 > gpurun_out/prof_noblas_summary.txt
+          rm -f gpurun_out/prof_noblas/*trace.csv ;;
     prof_mixtral) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
           step prof_mixtral 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_mixtral -o bench -- python bench.py --model mixtral-8x7b --steps 1 --warmup 1 --batch 512
           python scripts/prof_summary.py gpurun_out/prof_mixtral 40 --tail-ms 4000 > gpurun_out/prof_mixtral_summary.txt
@@ -42,6 +46,8 @@ for s in "$@"; do
     ep2) step ep2 900 env DLI_DIST_BACKEND=gloo DLI_SAME_DEVICE=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29535 bench.py --model mixtral-8x7b --gpus 2 --steps 1 --warmup 1 --batch 32 ;;
     llama70) step llama70 1100 python bench.py --model llama3-70b --steps 1 --warmup 1 --batch 64 ;;
     bench_small) step bench_small 600 python bench.py --steps 2 --warmup 1 --batch 64 ;;
+    noblas) step noblas 900 env DLI_GEMM_AUTOTUNE_LOG=1 python bench.py --steps 2 --warmup 1
+            step withblas 900 env DLI_GEMM_DECODE_BLAS=1 DLI_GEMM_AUTOTUNE_LOG=1 python bench.py --steps 2 --warmup 1 ;;
     tune) step tune_off 600 python bench.py --steps 2 --warmup 1
           step tune_on 900 env DLI_GEMM_AUTOTUNE=1 DLI_GEMM_AUTOTUNE_LOG=1 python bench.py --steps 2 --warmup 1
           step tune_on256 900 env DLI_GEMM_AUTOTUNE=1 python bench.py --steps 2 --warmup 1 --batch 256 ;;
