@@ -16,6 +16,8 @@ launcher for an 8-GPU MI355X box.
                     §2.5 "DP replicas"); every replica head registers as a node and the
                     master's dispatcher load-balances across them (least in flight)
     shard-model     --model_name M --num_shards N [--output_dir D] [--policy even|hbm|balanced]
+    loadgen         --master URL --model M [--requests N] [--concurrency C | --rate R]
+                    end-to-end load through the master API: tokens/s, p50/p99 latency
     bench           ... (bench.py)
 """
 from __future__ import annotations
@@ -179,6 +181,9 @@ def main(argv=None):
         return _serve_cluster(rest)
     if cmd == "shard-model":
         from .shard.writer import main as m
+        return m(rest)
+    if cmd == "loadgen":
+        from .loadgen import main as m
         return m(rest)
     if cmd == "bench":
         root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -304,3 +304,24 @@ def test_dp_replica_plan_and_pipeline_head_routing(tmp_path):
         r = c.post("/inference", json={"model_name": "llama3-8b", "prompt": "hi", **extra})
         assert r.status_code == 200 and r.get_json()["result"] == "hi!"
     assert FakePipe.calls == 2 and "llama3-8b" not in st.services
+
+
+def test_loadgen_end_to_end(tmp_path, master):
+    """Load generator through the public master API: concurrent clients, every request
+    completes; the worker batches them (continuous batching across HTTP requests)."""
+    from distributed_llm_inferencing_amd.loadgen import LoadGen
+    w = Server(create_worker_app(settings(tmp_path), device="cpu", engine_kwargs=SMALL))
+    ms = Server(master)
+    try:
+        requests.post(f"{ms.url}/api/nodes/add/", data={"hostname": "cpu0",
+                                                       "ip_address": "127.0.0.1",
+                                                       "port": w.port}, timeout=10)
+        lg = LoadGen(ms.url, "gpt2-tiny", poll_s=0.02, timeout_s=120)
+        wall = lg.closed_loop([f"hello {i}" for i in range(12)], concurrency=6)
+        rep = lg.report(wall)
+        assert rep["completed"] == 12 and rep["failed"] == 0
+        assert rep["p50_latency_s"] <= rep["p99_latency_s"]
+        assert rep["requests_per_s"] > 0
+    finally:
+        ms.close()
+        w.close()
