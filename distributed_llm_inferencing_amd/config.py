@@ -9,7 +9,7 @@ reference (worker, ``worker/app.py:19-30``):
     MODEL_CACHE_DIR, USE_GPU, AUTH_ENABLED, AUTH_KEY
 
 new:
-    NUM_GPUS, PIPELINE_STAGES, DP_REPLICAS, QUEUE_BACKEND (inproc|sqlite|redis),
+    NUM_GPUS, PIPELINE_STAGES, DP_REPLICAS, DISPATCH_WORKERS, QUEUE_BACKEND (inproc|sqlite|redis),
     TRANSPORT (rccl|gloo|loopback), MAX_NEW_TOKENS, KV_CACHE_FRACTION,
     MASTER_DB, MAX_BATCH, DLI_FAULT (fault-injection spec, see utils/faults.py)
 """
@@ -64,6 +64,9 @@ class Settings:
     kv_cache_fraction: float = 0.85
     master_db: str = str(REPO_ROOT / "db.sqlite3")
     max_batch: int = 256
+    # master dispatcher threads = requests in flight to workers (each blocks on one HTTP
+    # call); a worker batches concurrent requests, so this bounds its decode batch
+    dispatch_workers: int = 256
     log_dir: str = str(REPO_ROOT / "logs")
     fault: str = ""
     extra: dict = field(default_factory=dict)
@@ -89,6 +92,7 @@ class Settings:
         s.kv_cache_fraction = _env_float("KV_CACHE_FRACTION", s.kv_cache_fraction)
         s.master_db = os.environ.get("MASTER_DB", s.master_db)
         s.max_batch = _env_int("MAX_BATCH", s.max_batch)
+        s.dispatch_workers = _env_int("DISPATCH_WORKERS", s.dispatch_workers)
         s.log_dir = os.environ.get("DLI_LOG_DIR", s.log_dir)
         s.fault = os.environ.get("DLI_FAULT", "")
         return s

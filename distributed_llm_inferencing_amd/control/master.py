@@ -42,12 +42,13 @@ TEMPLATES = Path(__file__).resolve().parent / "templates"
 
 class MasterState:
     def __init__(self, settings: Settings, store: Store, start_background: bool = True,
-                 dispatch_workers: int = 4, health_interval: float = 10.0):
+                 dispatch_workers: Optional[int] = None, health_interval: float = 10.0):
         self.settings = settings
         self.store = store
         self.queue = make_queue(settings.queue_backend, store, settings)
         self.health = HealthMonitor(store, settings, interval=health_interval)
-        self.dispatcher = Dispatcher(store, self.queue, settings, num_workers=dispatch_workers,
+        self.dispatcher = Dispatcher(store, self.queue, settings,
+                                     num_workers=dispatch_workers or settings.dispatch_workers,
                                      on_node_error=self.health.report_failure)
         recovered = store.recover("requeue")
         for rid in store.pending_ids():

@@ -93,6 +93,8 @@ class WorkerState:
                 return False            # a pipeline head serves its model across all stages
             cfg = get_config(name)
             eng = LLMEngine(cfg, device=str(self.device), **self.engine_kwargs)
+            if eng.device.type == "cuda":
+                eng.warmup()          # capture decode graphs (+ GEMM autotune) before serving
             self.services[name] = EngineService(eng, name=name.replace("/", "_"))
             self.tokenizers[name] = eng.tokenizer
             return True

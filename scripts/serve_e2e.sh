@@ -1,0 +1,37 @@
+#!/bin/bash
+# End-to-end serving on one MI355X through the public API: master (Flask, sqlite, dispatcher
+# pool) + one GPU worker (continuous batching over HTTP requests) + the load generator.
+# Usage: bash scripts/serve_e2e.sh [requests] [concurrency] [max_batch]
+set -u
+N=${1:-1024}; C=${2:-512}; B=${3:-512}
+mkdir -p gpurun_out/logs
+export MASTER_DB=/tmp/dli_e2e_$$.sqlite3 DLI_LOG_DIR=gpurun_out/logs DISPATCH_WORKERS=$C
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+python -m distributed_llm_inferencing_amd.cli serve-master --port 8000 > gpurun_out/e2e_master.log 2>&1 &
+MPID=$!
+python -m distributed_llm_inferencing_amd.cli serve-worker --port 5000 --gpu 0 --max-batch $B \
+    --preload llama3-8b > gpurun_out/e2e_worker.log 2>&1 &
+WPID=$!
+ok=0
+for i in $(seq 1 600); do
+  if curl -sf http://127.0.0.1:5000/health | grep -q llama3-8b; then ok=1; break; fi
+  if ! kill -0 $WPID 2>/dev/null; then break; fi
+  sleep 1
+done
+rc=1
+if [ $ok = 1 ]; then
+  curl -s -X POST -d hostname=gpu0 -d ip_address=127.0.0.1 -d port=5000 \
+      http://127.0.0.1:8000/api/nodes/add/ > gpurun_out/e2e_addnode.json
+  timeout -k 10 900 python -m distributed_llm_inferencing_amd.loadgen \
+      --master http://127.0.0.1:8000 --model llama3-8b --requests $N --concurrency $C \
+      > gpurun_out/e2e_loadgen.json
+  rc=$?
+  cat gpurun_out/e2e_loadgen.json
+  curl -s http://127.0.0.1:5000/metrics > gpurun_out/e2e_worker_metrics.json
+else
+  echo "worker did not become healthy"; tail -20 gpurun_out/e2e_worker.log
+fi
+kill $WPID $MPID 2>/dev/null
+wait
+rm -f $MASTER_DB
+exit $rc

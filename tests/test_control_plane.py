@@ -36,6 +36,7 @@ def settings(tmp_path, **kw):
     s = Settings()
     s.master_db = str(tmp_path / "db.sqlite3")
     s.model_cache_dir = str(tmp_path / "cache")
+    s.dispatch_workers = 8
     for k, v in kw.items():
         setattr(s, k, v)
     return s
