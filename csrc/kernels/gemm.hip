@@ -20,6 +20,7 @@
 // Epilogues: 0 bf16 store, 1 fp32 store (logits), 2 SiLU(gate)*up over the 16-row-interleaved
 // gate/up weight (output width N/2), 3 bias + tanh-GELU, 4 bias.
 #include "common.h"
+#include <type_traits>
 
 #define BK 64
 
@@ -243,6 +244,314 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// 256x256 "8-phase ping-pong" GEMM (cdna_hip_programming.md §5 'The 256² 8-phase template',
+// T3+T4+T5; MI355X_MICROARCH.md 'Two waves per SIMD' items 1, 7, 9).
+//
+// 8 waves = 2 groups of 4 (g = wid >> 2 = the wave's 128-row half of the tile; one wave of
+// each group per SIMD). Every K-tile (BK = 64) is 4 phases; a phase is a LOAD segment
+// (this phase's ds_reads + one quarter of a later K-tile's glds + a counted vmcnt) and a
+// MATRIX segment (16 MFMAs, one 64x32 quadrant of the wave's 128x64 output), separated by
+// raw s_barriers. Group 1 runs one barrier behind group 0, so on every SIMD one wave is in
+// its matrix segment while its partner is in its load segment.
+//
+//   phase | ds_read_b128 (this K-tile)        | MFMAs          | glds issued
+//   0     | A rows 0-63 of the half, B 0-31   | acc[0-3][0-1]  | slot 3 of K-tile T+1
+//   1     | B cols 32-63                      | acc[0-3][2-3]  | slot 0 of K-tile T+2
+//   2     | A rows 64-127                     | acc[4-7][2-3]  | slot 1 of K-tile T+2
+//   3     | -                                 | acc[4-7][0-1]  | slot 2 of K-tile T+2
+//
+// LDS: 2 buffers x (A 256x64 + W 256x64) bf16 = 128 KiB (1 workgroup / CU), 128-B rows with
+// the chunk XOR swizzle of gemm_bf16_kernel. Staging slots per group (2 glds per lane each):
+// group 0 stages A rows 0-63 / 64-127 and the even 32-row W chunks, group 1 A rows
+// 128-191 / 192-255 and the odd W chunks. With segments numbered s (group 0 loads in even
+// s, group 1 in odd s) every slot is restaged >= 2 segments after its last ds_read of the
+// K-tile two back (WAR) and retired by its issuer's vmcnt >= 1 barrier before its first
+// ds_read (RAW) when every load segment leaves the last 3 segments' glds in flight:
+// vmcnt(6) in steady state, fewer when the K loop's tail issues nothing.
+template <int EPI, int VAR = 0>
+__global__ void __launch_bounds__(512) gemm8p_kernel(
+    const u16* __restrict__ A, int lda, const u16* __restrict__ W, int ldw,
+    void* __restrict__ C, int ldc, int M, int N, int K, int k_split_len,
+    const u16* __restrict__ bias, float* __restrict__ ws, const int* __restrict__ group_off) {
+  constexpr int BM = 256, BN = 256;
+  constexpr int A_BYTES = BM * BK * 2, BUF = 2 * A_BYTES;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  int row0 = 0, Mg = M;
+  const u16* Wg = W;
+  if (group_off != nullptr) {
+    row0 = group_off[blockIdx.z];
+    Mg = group_off[blockIdx.z + 1] - row0;
+    Wg = W + (long)blockIdx.z * N * ldw;
+  }
+  const int tiles_m = (M + BM - 1) / BM;
+  const int tiles_n = (N + BN - 1) / BN;
+  const int tile = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  int tn, tm;
+  constexpr int GM = (VAR & 8) ? 4 : (VAR & 16) ? 8 : 1;
+  if (GM > 1) {
+    // grouped order: an XCD's ~32 consecutive tiles cover GM tile-rows x 32/GM tile-columns,
+    // so its CUs share both A and W panels in its L2 (n-major order shares W only)
+    const int per_group = GM * tiles_n;
+    const int first_m = (tile / per_group) * GM;
+    const int gsz = min(tiles_m - first_m, GM);
+    const int in_g = tile % per_group;
+    tm = first_m + in_g % gsz;
+    tn = in_g / gsz;
+  } else {
+    tn = tile / tiles_m;
+    tm = tile % tiles_m;
+  }
+  const int m0 = tm * BM, n0 = tn * BN;
+  if (m0 >= Mg) return;
+  const int kb = blockIdx.y * k_split_len;
+  const int nk = min(k_split_len, K - kb) / BK;
+  const u16* Ab = A + (long)row0 * lda;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = wid >> 2, gw = wid & 3;           // group (= M half), wave in group (= N quarter)
+
+  // ---- staging: slot s (0..3) x instruction i (0..1): element offset of this lane's source
+  // and the wave-uniform LDS byte offset of the 1-KiB piece (8 rows x 128 B)
+  int src[4][2];
+  int dst[4][2];
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      int rb, is_a;
+      if ((s & 1) == 0) { rb = 64 * (2 * g + (s >> 1)) + 32 * i + 8 * gw; is_a = 1; }
+      else { rb = 64 * (2 * (s >> 1) + i) + 32 * g + 8 * gw; is_a = 0; }
+      const int r = rb + (lane >> 3);
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      if (is_a) src[s][i] = min(m0 + r, Mg - 1) * lda + kb + c * 8;
+      else src[s][i] = min(n0 + r, N - 1) * ldw + kb + c * 8;
+      dst[s][i] = (is_a ? 0 : A_BYTES) + rb * 128;
+    }
+  // deep plan (VAR & 4): per group, A region h (2 glds) and all 4 W chunks of its parity (4 glds)
+  int srcB[4], dstB[4];
+#pragma unroll
+  for (int c4 = 0; c4 < 4; ++c4) {
+    const int rb = 64 * c4 + 32 * g + 8 * gw;
+    const int r = rb + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    srcB[c4] = min(n0 + r, N - 1) * ldw + kb + c * 8;
+    dstB[c4] = A_BYTES + rb * 128;
+  }
+  auto issue_a = [&](int h, int kt) {             // h: A rows 64h..64h+63 of the group's half
+    char* lds = smem + (kt & 1) * BUF;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((gbl_void*)(Ab + src[2 * h][i] + kt * BK),
+                                       (lds_void*)(lds + dst[2 * h][i]), 16, 0, 0);
+  };
+  auto issue_b = [&](int kt) {
+    char* lds = smem + (kt & 1) * BUF;
+#pragma unroll
+    for (int c4 = 0; c4 < 4; ++c4)
+      __builtin_amdgcn_global_load_lds((gbl_void*)(Wg + srcB[c4] + kt * BK),
+                                       (lds_void*)(lds + dstB[c4]), 16, 0, 0);
+  };
+  auto issue = [&](auto S, int kt) {
+    constexpr int s = decltype(S)::value;
+    const u16* base = (s & 1) ? Wg : Ab;
+    char* lds = smem + (kt & 1) * BUF;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((gbl_void*)(base + src[s][i] + kt * BK),
+                                       (lds_void*)(lds + dst[s][i]), 16, 0, 0);
+  };
+
+  // ---- fragments
+  const int fr = lane & 15, fq = lane >> 4;
+  auto read_frag = [&](const char* part, int row, int kk) -> bf16x8 {
+    const int c = kk * 4 + fq;
+    return *reinterpret_cast<const bf16x8*>(part + row * 128 + ((c ^ ((row >> 1) & 7)) << 4));
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // ---- prologue: K-tiles 0 and 1 in full
+  if (nk > 0) {
+    issue(std::integral_constant<int, 0>{}, 0); issue(std::integral_constant<int, 1>{}, 0);
+    issue(std::integral_constant<int, 2>{}, 0); issue(std::integral_constant<int, 3>{}, 0);
+  }
+  if (nk > 1) {
+    issue(std::integral_constant<int, 0>{}, 1); issue(std::integral_constant<int, 1>{}, 1);
+    issue(std::integral_constant<int, 2>{}, 1); issue(std::integral_constant<int, 3>{}, 1);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (g == 1) {                                    // stagger: group 1 runs one segment behind
+    __builtin_amdgcn_s_barrier();
+    if (VAR & 256) __builtin_amdgcn_s_setprio(1);  // static priority for the younger half
+  }
+
+  const int last_issue_seg = 4 * nk - 8;          // load segments 1..last issue glds
+  bf16x8 a0[4][2], a1[4][2], b0[2][2], b1[2][2];
+
+  auto barrier = [&]() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
+  };
+  auto wait_deep = [&](int u) {                   // keep the last 5 load segments' glds in flight
+    int cnt = 0;
+#pragma unroll
+    for (int d = 0; d < 5; ++d) {
+      const int v = u - d;
+      const int q = v & 3;
+      if (v >= 1 && q != 0 && (v >> 2) + 2 < nk) cnt += (q == 2) ? 4 : 2;
+    }
+    switch (cnt) {                                 // wave-uniform
+      case 0: wait_vmcnt<0>(); break;
+      case 2: wait_vmcnt<2>(); break;
+      case 4: wait_vmcnt<4>(); break;
+      case 6: wait_vmcnt<6>(); break;
+      case 8: wait_vmcnt<8>(); break;
+      case 10: wait_vmcnt<10>(); break;
+      default: wait_vmcnt<12>(); break;
+    }
+  };
+  auto wait_issued = [&](int u) {
+    if (VAR & 4) { wait_deep(u); return; }
+    const int lo = max(1, u - 2), hi = min(u, last_issue_seg);
+    const int cnt = hi >= lo ? hi - lo + 1 : 0;    // wave-uniform
+    if (cnt >= 3) wait_vmcnt<6>();
+    else if (cnt == 2) wait_vmcnt<4>();
+    else if (cnt == 1) wait_vmcnt<2>();
+    else wait_vmcnt<0>();
+  };
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* abuf = smem + (kt & 1) * BUF;
+    const char* wbuf = abuf + A_BYTES;
+    const int arow = g * 128 + fr, wrow = gw * 64 + fr;
+    const int u0 = 4 * kt;
+    auto phase = [&](auto P) {
+      constexpr int p = decltype(P)::value;
+      auto reads = [&]() {
+        if (p == 0) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) a0[i][kk] = read_frag(abuf, arow + 16 * i, kk);
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) b0[j][kk] = read_frag(wbuf, wrow + 16 * j, kk);
+        } else if (p == 1) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) b1[j][kk] = read_frag(wbuf, wrow + 32 + 16 * j, kk);
+        } else if (p == 2) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) a1[i][kk] = read_frag(abuf, arow + 64 + 16 * i, kk);
+        }
+      };
+      auto stage = [&]() {
+        if (p == 0) {
+          if (!(VAR & 4) && kt >= 1 && kt + 1 < nk) issue(std::integral_constant<int, 3>{}, kt + 1);
+        } else if (kt + 2 < nk) {
+          if (VAR & 4) {
+            if (p == 1) issue_a(0, kt + 2);
+            else if (p == 2) issue_b(kt + 2);
+            else issue_a(1, kt + 2);
+          } else {
+            issue(std::integral_constant<int, (p + 3) & 3>{}, kt + 2);
+          }
+        }
+      };
+      if (VAR & 64) { stage(); reads(); }
+      else { reads(); stage(); }
+      if (!(VAR & 32)) wait_issued(u0 + p);
+      barrier();
+      if (!(VAR & 256)) __builtin_amdgcn_s_setprio(1);
+      const bf16x8 (&af)[4][2] = (p < 2) ? a0 : a1;
+      const bf16x8 (&bf)[2][2] = (p == 0 || p == 3) ? b0 : b1;
+      constexpr int I0 = (p < 2) ? 0 : 4, J0 = (p == 0 || p == 3) ? 0 : 2;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[I0 + i][J0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                af[i][kk], bf[j][kk], acc[I0 + i][J0 + j], 0, 0, 0);
+      if (!(VAR & 256)) __builtin_amdgcn_s_setprio(0);
+      barrier();
+    };
+    phase(std::integral_constant<int, 0>{});
+    phase(std::integral_constant<int, 1>{});
+    phase(std::integral_constant<int, 2>{});
+    phase(std::integral_constant<int, 3>{});
+  }
+  if (g == 0) {                                    // balance group 1's stagger barrier
+    __builtin_amdgcn_s_barrier();
+  }
+
+  // ---- epilogue: acc[I][J][r] = C[m0 + 128g + 16I + 4fq + r][n0 + 64gw + 16J + fr]
+  const int wr0 = m0 + 128 * g, wc0 = n0 + 64 * gw;
+  if (gridDim.y > 1) {
+    float* slab = ws + (long)blockIdx.y * M * N;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wr0 + 16 * i + 4 * fq + r;
+        if (row >= Mg) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int col = wc0 + 16 * j + fr;
+          if (col < N) slab[(long)(row0 + row) * N + col] = acc[i][j][r];
+        }
+      }
+    return;
+  }
+  if (EPI == EPI_SILU) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wr0 + 16 * i + 4 * fq + r;
+        if (row >= Mg) continue;
+#pragma unroll
+        for (int j = 0; j < 4; j += 2) {
+          const int gcol = wc0 + 16 * j;
+          if (gcol < N) {
+            const int f = (gcol >> 5) * 16 + fr;
+            const float v = silu_f(acc[i][j][r]) * acc[i][j + 1][r];
+            ((u16*)C)[(long)(row0 + row) * ldc + f] = f2bf(v);
+          }
+        }
+      }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = wr0 + 16 * i + 4 * fq + r;
+      if (row >= Mg) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = wc0 + 16 * j + fr;
+        if (col < N) store_pair_or_one<EPI>(C, ldc, row0 + row, col, acc[i][j][r], bias);
+      }
+    }
+}
+
 // split-K reduction + epilogue: one thread per output element group of 4 columns
 template <int EPI>
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(void* __restrict__ C, int ldc,
@@ -295,6 +604,39 @@ static int launch_cfg(const void* A, int lda, const void* W, int ldw, void* C, i
   DLI_RETURN_LAUNCH();
 }
 
+// measured on MI355X (scripts/bench_gemm8p.py, profiles/r1_gemm8p/): grouped tile order
+// (+6-14 % on prefill shapes) and a static priority for waves 4-7 (+1.5-5 %) over per-cluster
+// flips; the deep-prefetch plan (VAR 4) and glds-before-ds_read order measured slower / equal
+constexpr int GEMM8P_DEFAULT = 8 | 256;
+
+template <int EPI, int VAR = 0>
+static int launch_8p(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M,
+                     int N, int K, int splits, const void* bias, void* ws, const int* group_off,
+                     int groups, hipStream_t st) {
+  if (EPI == EPI_SILU && N % 64) return (int)hipErrorInvalidValue;
+  const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  int ksl = K / splits;
+  ksl = (ksl / BK) * BK;
+  if (ksl * splits != K) return (int)hipErrorInvalidValue;
+  constexpr size_t lds = 2 * (size_t)(256 + 256) * BK * 2;
+  static bool attr_done = false;
+  if (!attr_done) {
+    hipFuncSetAttribute((const void*)gemm8p_kernel<EPI, VAR>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_done = true;
+  }
+  dim3 grid(tiles, splits, groups);
+  gemm8p_kernel<EPI, VAR><<<grid, 512, lds, st>>>((const u16*)A, lda, (const u16*)W, ldw, C, ldc, M,
+                                             N, K, ksl, (const u16*)bias, (float*)ws, group_off);
+  if (splits > 1 && C != nullptr) {
+    const int outN = (EPI == EPI_SILU) ? N / 2 : N;
+    const long total = (long)M * outN;
+    splitk_reduce_kernel<EPI><<<(int)((total + 255) / 256), 256, 0, st>>>(
+        C, ldc, (const float*)ws, M, N, splits, (const u16*)bias);
+  }
+  DLI_RETURN_LAUNCH();
+}
+
 template <int EPI>
 static int dispatch_tile(int tile_cfg, const void* A, int lda, const void* W, int ldw, void* C,
                          int ldc, int M, int N, int K, int splits, const void* bias, void* ws,
@@ -314,6 +656,8 @@ static int dispatch_tile(int tile_cfg, const void* A, int lda, const void* W, in
     DLI_CFG8(16, 256, 128, 3, 4, 2) DLI_CFG8(17, 128, 256, 3, 2, 4)
     // grid-filling shapes for N = 6144 / 4096 at M = 512 (4 x 64 = 256 workgroups)
     DLI_CFG(18, 128, 96, 2) DLI_CFG(19, 128, 96, 3) DLI_CFG(20, 128, 64, 2) DLI_CFG(21, 128, 64, 3)
+    // 256x256 8-phase ping-pong (gemm8p_kernel)
+    case 22: return launch_8p<EPI, GEMM8P_DEFAULT>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
 #undef DLI_CFG8
 #undef DLI_CFG
     default: return (int)hipErrorInvalidValue;
@@ -324,7 +668,7 @@ static int dispatch_tile(int tile_cfg, const void* A, int lda, const void* W, in
 // tiles with 3 LDS stages (one tile in flight across the barrier); 10/11 = 192x128 with 2/3
 // stages, 12 = 160x128 (MoE experts of ~130-190 rows in one pass); 13-17 = 8-wave tiles
 // 256x256, 256x128, 128x256 (2 stages) and 256x128, 128x256 (3 stages); 18/19 = 128x96 and
-// 20/21 = 128x64 with 2/3 stages. ws: fp32 [splits, M, N] when splits>1.
+// 20/21 = 128x64 with 2/3 stages; 22 = 256x256 8-phase ping-pong. ws: fp32 [splits, M, N] when splits>1.
 // group_off (nullable): int[groups+1] row offsets; M is then the max rows of any group.
 extern "C" int dli_gemm(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M,
                         int N, int K, int epi, int tile_cfg, int splits, const void* bias,

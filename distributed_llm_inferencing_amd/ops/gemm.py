@@ -30,8 +30,11 @@ TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256), 4: (256, 128),
          # 8 waves / 512 threads (fewer L2 re-reads of A and W at M >= 256)
          13: (256, 256), 14: (256, 128), 15: (128, 256), 16: (256, 128), 17: (128, 256),
          # grid-filling tiles for N = 6144 / 4096 at M = 512
-         18: (128, 96), 19: (128, 96), 20: (128, 64), 21: (128, 64)}
-TILE_WAVES = {13: (2, 4), 14: (4, 2), 15: (2, 4), 16: (4, 2), 17: (2, 4)}   # default 2 x 2
+         18: (128, 96), 19: (128, 96), 20: (128, 64), 21: (128, 64),
+         # 256x256 8-phase ping-pong (two wave groups alternate MFMA / load segments)
+         22: (256, 256)}
+TILE_WAVES = {13: (2, 4), 14: (4, 2), 15: (2, 4), 16: (4, 2), 17: (2, 4),
+              22: (2, 4)}   # default 2 x 2
 
 
 def tile_ok(tile: int, epi: str) -> bool:

@@ -100,7 +100,7 @@ def test_gemm_epilogues(gpu, epi, M, N, K):
         ref = R.gelu_tanh(R.linear(x, w, b))
     else:
         ref = R.linear(x, w, b)
-    for tile in (0, 2, 13, 14, 20):
+    for tile in (0, 2, 13, 14, 20, 22):
         for splits in (1, 2):
             out = ops._gemm_native(x, w, epi, bias=b if "bias" in epi else None,
                                    plan=G.GemmPlan("dli", tile, splits))
