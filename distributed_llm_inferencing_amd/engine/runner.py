@@ -207,7 +207,10 @@ class StageRunner:
             torch.cuda.current_stream(self.device).wait_stream(s)
             torch.cuda.synchronize(self.device)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=self._pool):
+            # thread-local capture: the RCCL process group's watchdog thread keeps polling
+            # its events while a stage captures; under the default global mode such a call
+            # from another thread invalidates the capture (and aborts the watchdog)
+            with torch.cuda.graph(g, pool=self._pool, capture_error_mode="thread_local"):
                 out = self._forward_static(b)
             if self._pool is None:
                 self._pool = g.pool()

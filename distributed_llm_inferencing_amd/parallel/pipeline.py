@@ -267,6 +267,7 @@ class PipelineHead:
             if smp is not None and smp[1]:
                 recvs += [((smp[0].num_seqs, 2 * CAND), torch.int32, q, 3) for q in range(1, N)]
             hd = ch.exchange_many([(prev_out, 1, 1)] if prev_out is not None else [], recvs)
+            ch.reap_ctrl()
             cand_now = None
             if ret is not None:
                 if ret[1]:

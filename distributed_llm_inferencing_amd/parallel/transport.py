@@ -96,9 +96,26 @@ class PipeChannel:
                 self._ctrl_sends.append((dist.isend(h, r, group=self.ctrl_group), h))
                 if p.numel():
                     self._ctrl_sends.append((dist.isend(p, r, group=self.ctrl_group), p))
-        while len(self._ctrl_sends) > 8 * self.world:
-            w, _ = self._ctrl_sends.popleft()
-            w.wait()
+        # never block here: stage r consumes the message of tick j only after the head has
+        # posted its data exchange of tick j (and stage r-1 has run), so a blocking drain
+        # BEFORE this tick's exchange can deadlock a deep ring (8 stages: ~2 x 28 messages
+        # are legitimately in flight). The head drains in reap_ctrl() after its exchange.
+        self._reap(blocking_above=None)
+
+    def _reap(self, blocking_above):
+        q = self._ctrl_sends
+        while q and q[0][0].is_completed():
+            q.popleft()[0].wait()          # completed: returns at once, releases the Work
+        if blocking_above is not None:
+            while len(q) > blocking_above:
+                w, _ = q.popleft()
+                w.wait()
+
+    def reap_ctrl(self) -> None:
+        """Head, after posting this tick's data exchange: release delivered control messages
+        and bound the backlog (safe to block now: every stage can consume the messages of
+        ticks <= the one just posted)."""
+        self._reap(blocking_above=64 * self.world)
 
     def recv_ctrl(self) -> Tuple[np.ndarray, np.ndarray]:
         h = torch.empty(HEADER_LEN, dtype=torch.int64)

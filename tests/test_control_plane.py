@@ -240,7 +240,8 @@ def test_failover_and_no_nodes(tmp_path, master):
                                                        "prompt": f"p{i}"}).get_json()["request_id"]
                 for i in range(3)]
         for rid in rids:
-            for _ in range(300):
+            deadline = time.time() + 180        # generous: CPU-loaded parallel test runs
+            while time.time() < deadline:
                 st = c.get(f"/api/inference/status/{rid}/").get_json()
                 if st["status"] in ("completed", "failed"):
                     break

@@ -58,13 +58,16 @@ def _free_port():
         return s.getsockname()[1]
 
 
+MANY = [[3 + (7 * i + j) % 200 for j in range(4 + i % 5)] for i in range(96)]
+
+
 def _worker(rank, world, port, model, q, vp="auto"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank), DLI_PP_VOCAB_PARALLEL=vp)
     torch.set_num_threads(1)
     import torch.distributed as dist
     from distributed_llm_inferencing_amd.parallel.pipeline import DistributedPipelineEngine
-    eng = DistributedPipelineEngine(model, "cpu", max_batch=8, max_model_len=64, num_blocks=64,
+    eng = DistributedPipelineEngine(model, "cpu", max_batch=8, max_model_len=64, num_blocks=256,
                                     dtype=torch.float32)
     if rank == 0:
         res = []
@@ -78,6 +81,11 @@ def _worker(rank, world, port, model, q, vp="auto"):
         res.append([o.all_ids for o in eng.generate(PROMPTS[:3], SamplingParams(
             max_length=16, top_k=0, top_p=0.9, seed=5, ignore_eos=True))])
         res.append(eng.vocab_parallel)
+        if world >= 8:
+            # every microbatch full for many ticks: the head's control-plane backlog to the
+            # far stages is deepest here (a blocking drain before the exchange deadlocked)
+            res.append([o.all_ids for o in eng.generate(MANY, SamplingParams(
+                max_length=28, do_sample=False, ignore_eos=True))])
         eng.shutdown()
         q.put(res)
     else:
@@ -86,7 +94,7 @@ def _worker(rank, world, port, model, q, vp="auto"):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,vp", [(2, "0"), (3, "0"), (2, "1"), (4, "auto")])
+@pytest.mark.parametrize("world,vp", [(2, "0"), (3, "0"), (2, "1"), (4, "auto"), (8, "auto")])
 def test_gloo_ring_matches_single_stage(world, vp):
     """Pipeline over gloo ranks == single-stage engine, token for token (greedy, sampled,
     second session, full-vocab fallback), with the tail LM head and with the vocab-parallel
@@ -113,6 +121,9 @@ def test_gloo_ring_matches_single_stage(world, vp):
     assert res[3] == [o.all_ids for o in eng.generate(PROMPTS[:3], SamplingParams(
         max_length=16, top_k=0, top_p=0.9, seed=5, ignore_eos=True))]
     assert res[4] == (vp == "1" or (vp == "auto" and world >= 4))
+    if world >= 8:
+        assert res[5] == [o.all_ids for o in eng.generate(MANY, SamplingParams(
+            max_length=28, do_sample=False, ignore_eos=True))]
 
 
 def _ep_worker(rank, world, port, q):
