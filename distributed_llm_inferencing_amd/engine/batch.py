@@ -35,6 +35,9 @@ class StepMeta:
     seeds: Optional[np.ndarray] = None                      # [S] int64
     microbatch: int = 0
     step_id: int = 0
+    # lookahead (single stage, not on the wire): row of the in-flight step's device output
+    # that holds this sequence's input id, -1 = input_ids holds it
+    feed_src: Optional[np.ndarray] = None
 
     @property
     def num_seqs(self) -> int:
@@ -47,11 +50,21 @@ class StepMeta:
     # ---- wire format: header (int64) + payload (int32) ------------------------------------
     def pack(self) -> (np.ndarray, np.ndarray):
         S, T = self.num_seqs, self.num_tokens
-        mb = 0 if self.block_tables is None else int(self.block_tables.shape[1])
+        tables = self.block_tables
+        width = 0 if tables is None else int(tables.shape[1])
+        if tables is not None and tables.shape[1] > 1:
+            # trailing all-zero columns are dropped and restored by unpack (zeros either way:
+            # padding or block 0): a 100-token decode needs 7 of the 32 columns, 2.5x less
+            # control-plane payload
+            used = np.flatnonzero(np.asarray(tables).any(axis=0))
+            keep = int(used[-1]) + 1 if used.size else 1
+            if keep < tables.shape[1]:
+                tables = np.ascontiguousarray(tables[:, :keep])
+        mb = 0 if tables is None else int(tables.shape[1])
         parts = [np.asarray(self.seq_ids, dtype=np.int32),
                  _i32(self.input_ids, T), _i32(self.positions, T), _i32(self.slot_mapping, T),
                  _i32(self.seq_lens, S), _i32(self.context_lens, S),
-                 _i32(self.block_tables, S * mb).reshape(-1),
+                 _i32(tables, S * mb).reshape(-1),
                  _f32_as_i32(self.temperature, S), _i32(self.top_k, S),
                  _f32_as_i32(self.top_p, S),
                  (np.zeros(S, np.int64) if self.seeds is None else
@@ -60,6 +73,7 @@ class StepMeta:
         header = np.zeros(HEADER_LEN, dtype=np.int64)
         header[:7] = [self.kind, S, T, mb, payload.shape[0], self.microbatch, self.step_id]
         header[7] = 1 if self.input_ids is not None else 0
+        header[8] = width
         return header, payload
 
     @staticmethod
@@ -78,6 +92,9 @@ class StepMeta:
         positions, slots = take(T), take(T)
         seq_lens, ctx = take(S), take(S)
         bt = take(S * mb).reshape(S, mb)
+        width = int(header[8])
+        if width > mb:                       # restore the trimmed all-zero columns
+            bt = np.concatenate([bt, np.zeros((S, width - mb), np.int32)], axis=1)
         temp = take(S, np.float32)
         topk = take(S)
         topp = take(S, np.float32)

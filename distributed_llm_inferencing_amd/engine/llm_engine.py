@@ -8,6 +8,7 @@ hipGraph decode on our HIP kernels. Multi-GPU pipelines use the same pieces thro
 from __future__ import annotations
 
 import itertools
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Dict, Iterable, List, Optional, Union
@@ -48,6 +49,28 @@ class EngineStats:
                 "p50_latency_s": pct(0.5), "p99_latency_s": pct(0.99)}
 
 
+class _HostTokens:
+    """Sampled ids of a launched step on their way to the host: an async D2H copy into pinned
+    memory + event, enqueued right behind the step (before any later replay can overwrite
+    the graph's static output buffer)."""
+
+    def __init__(self, tokens: torch.Tensor):
+        self.array = None
+        if not tokens.is_cuda:
+            self.array = tokens.numpy()
+            return
+        self.host = torch.empty(tokens.shape, dtype=tokens.dtype, pin_memory=True)
+        self.host.copy_(tokens, non_blocking=True)
+        self.ev = torch.cuda.Event()
+        self.ev.record()
+
+    def get(self) -> np.ndarray:
+        if self.array is None:
+            self.ev.synchronize()
+            self.array = self.host.numpy()
+        return self.array
+
+
 def seq_to_output(seq: Sequence, tokenizer=None) -> RequestOutput:
     end = seq.finish_time or time.perf_counter()
     out = RequestOutput(request_id=seq.request_id, prompt_ids=seq.prompt_ids,
@@ -68,7 +91,7 @@ class LLMEngine:
                  kv_fraction: float = 0.85, seed: int = 0, use_graphs: Optional[bool] = None,
                  params: Optional[Dict[str, torch.Tensor]] = None, tokenizer_path=None,
                  max_prefill_tokens: int = 16384, num_layers: Optional[int] = None,
-                 lm: Optional[TransformerLM] = None):
+                 lm: Optional[TransformerLM] = None, lookahead: Optional[bool] = None):
         self.cfg = get_config(model, num_layers) if isinstance(model, str) else model
         self.device = torch.device(device)
         if self.device.type == "cuda" and self.device.index is None:
@@ -100,6 +123,11 @@ class LLMEngine:
         self._ids = itertools.count()
         self.max_batch = max_batch
         self.max_model_len = max_model_len
+        # lookahead scheduling (one step in flight ahead of the host); DLI_LOOKAHEAD=0 = off.
+        # Engines whose every step must stay in lockstep with peer ranks (EP / TP) pass False.
+        self.lookahead = (os.environ.get("DLI_LOOKAHEAD", "1") == "1"
+                          if lookahead is None else bool(lookahead))
+        self._inflight = None           # (meta, device tokens, host copy) of the in-flight step
 
     # ------------------------------------------------------------------ API
     def add_request(self, prompt: Union[str, List[int]], params: Optional[SamplingParams] = None,
@@ -113,32 +141,48 @@ class LLMEngine:
         return self.scheduler.abort(request_id)
 
     def has_work(self) -> bool:
-        return self.scheduler.has_work()
+        return self.scheduler.has_work() or self._inflight is not None
 
     def warmup(self, buckets=None):
         """Capture decode graphs ahead of serving (and touch every GEMM plan)."""
         self.runner.capture(buckets)
 
     def step(self) -> List[RequestOutput]:
+        """One engine iteration. With lookahead (default) it schedules and launches the next
+        step BEFORE the in-flight step's tokens reach the host, then applies those tokens:
+        the host's sync, scheduler update and metadata upload overlap the GPU's work instead
+        of leaving it idle between steps (measured ~8 % idle at batch 512 without)."""
+        prev = self._inflight
+        t0 = time.perf_counter()
+        meta = None
         with self.timer.phase("schedule"):
-            meta = self.scheduler.schedule(0)
+            if self.scheduler.has_work():
+                meta = self.scheduler.schedule(0, inflight=prev[0] if prev else None)
+        launched = None
         if meta is not None:
-            t0 = time.perf_counter()
             kind = "prefill" if meta.kind == 1 else "decode"
             with trace_range(f"engine.{kind}[{meta.num_seqs}]"), self.timer.phase(f"run_{kind}"):
-                tokens = self.runner.run(meta)
-            with self.timer.phase("sync"):
-                tok = tokens.cpu().numpy() if tokens.is_cuda else tokens.numpy()
-            with self.timer.phase("update"):
-                self.scheduler.update(meta, tok)
-            self.stats.busy_s += time.perf_counter() - t0
+                tokens = self.runner.run(meta, feed=prev[1] if prev is not None else None)
+            launched = (meta, tokens, _HostTokens(tokens))
             self.stats.steps += 1
-            self.stats.tokens_out += meta.num_seqs
             if meta.kind == 1:
                 self.stats.prefill_steps += 1
                 self.stats.prompt_tokens += meta.num_tokens
             else:
                 self.stats.decode_steps += 1
+        if self.lookahead:
+            self._inflight = launched
+            done = prev
+        else:
+            done = launched
+        if done is not None:
+            with self.timer.phase("sync"):
+                tok = done[2].get()
+            with self.timer.phase("update"):
+                self.scheduler.update(done[0], tok)
+            self.stats.tokens_out += done[0].num_seqs
+        if meta is not None or done is not None:
+            self.stats.busy_s += time.perf_counter() - t0
         outs = []
         for seq in self.scheduler.pop_finished():
             o = seq_to_output(seq, self.tokenizer)

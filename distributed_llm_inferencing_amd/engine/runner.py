@@ -47,11 +47,14 @@ class StageRunner:
     # ------------------------------------------------------------------ static buffers
     def _init_static(self):
         B, W = self.max_batch, self.W
-        # layout (int32 words): ids | pos | slots | ctx | temp | topk | topp | seeds(2B) | tables(B*W)
+        # layout (int32 words):
+        #   ids | pos | slots | ctx | temp | topk | topp | seeds(2B) | src | tables(B*W)
+        # src = lookahead feed rows (StepMeta.feed_src, -1 = host id)
         self._off = {}
         o = 0
         for name, n in (("ids", B), ("pos", B), ("slots", B), ("ctx", B), ("temp", B),
-                        ("topk", B), ("topp", B), ("seeds", 2 * B), ("tables", B * W)):
+                        ("topk", B), ("topp", B), ("seeds", 2 * B), ("src", B),
+                        ("tables", B * W)):
             self._off[name] = (o, n)
             o += n
         self._nwords = o
@@ -108,6 +111,7 @@ class StageRunner:
         put("topk", meta.top_k, 1)
         put("topp", meta.top_p.astype(np.float32), np.float32(1.0).view(np.int32))
         put("seeds", meta.seeds.astype(np.int64), 0)
+        put("src", meta.feed_src if meta.feed_src is not None else np.full(S, -1, np.int32), -1)
         o, _ = self._off["tables"]
         tb = np.asarray(meta.block_tables, dtype=np.int32)
         if tb.shape[1] != self.W:
@@ -219,8 +223,19 @@ class StageRunner:
         torch.cuda.synchronize(self.device)
 
     # ------------------------------------------------------------------ execution
-    def run(self, meta: StepMeta, hidden: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """Returns int32 tokens [S] on the last stage, else the hidden state [T, D]."""
+    @staticmethod
+    def _feed(ids: torch.Tensor, src: torch.Tensor, feed: torch.Tensor) -> None:
+        """Lookahead: ids[i] = feed[src[i]] where src[i] >= 0 (stream-ordered after the step
+        that produced ``feed``, before this step's replay overwrites it)."""
+        take = feed.index_select(0, src.clamp(min=0).long()).to(ids.dtype)
+        ids.copy_(torch.where(src >= 0, take, ids))
+
+    def run(self, meta: StepMeta, hidden: Optional[torch.Tensor] = None,
+            feed: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Returns int32 tokens [S] on the last stage, else the hidden state [T, D].
+        ``feed``: the in-flight step's token output, read where ``meta.feed_src`` says."""
+        if meta.feed_src is not None and feed is None:
+            raise ValueError("step has lookahead rows but no in-flight output to feed them")
         if meta.kind == DECODE and self.use_graphs and meta.num_seqs <= self.max_batch:
             S = meta.num_seqs
             b = self._bucket(S)
@@ -228,9 +243,14 @@ class StageRunner:
                 self.capture([b])
             self._fill_host(meta, b)
             self._upload(b)
+            if meta.feed_src is not None:
+                self._feed(self._view("ids", S), self._view("src", S), feed)
             if self.hidden_in is not None:
                 self.hidden_in[:S].copy_(hidden[:S])
             self.graphs[b].replay()
             return self.graph_out[b][:S]
         db = to_device(meta, self.device)
+        if meta.feed_src is not None:
+            src = torch.from_numpy(np.ascontiguousarray(meta.feed_src, np.int32)).to(self.device)
+            self._feed(db.input_ids, src, feed)
         return self.model.forward(db, self.kv_layers, hidden=hidden)

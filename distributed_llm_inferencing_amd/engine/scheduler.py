@@ -182,14 +182,22 @@ class Scheduler:
         return temp, topk, topp, seeds
 
     # ------------------------------------------------------------------ scheduling
-    def schedule(self, mb: int = 0) -> Optional[StepMeta]:
-        """Next step for microbatch ``mb`` (None if it has nothing to do)."""
+    def schedule(self, mb: int = 0, inflight: Optional[StepMeta] = None) -> Optional[StepMeta]:
+        """Next step for microbatch ``mb`` (None if it has nothing to do).
+
+        ``inflight``: a step of this microbatch whose tokens have not been applied yet
+        (lookahead scheduling, one step ahead of the host). Its sequences are scheduled as if
+        each had produced one more non-stop token: context and output index advance by one,
+        those that reach their length budget with it are left out, and their input id comes
+        from the in-flight step's device output (``meta.feed_src`` = row in that output, -1 =
+        host id). A sequence that instead stops on EOS wastes one row of the next step; its
+        token is dropped by ``update`` (the sequence is no longer running)."""
         self._expire()
         self._step += 1
         meta = self._try_prefill(mb)
         if meta is not None:
             return meta
-        return self._decode(mb)
+        return self._decode(mb, inflight)
 
     def _least_loaded_ok(self, mb: int) -> bool:
         # balance admissions across microbatches: only admit into mb if it is among the least loaded
@@ -237,34 +245,61 @@ class Scheduler:
             self._state[mb] = st
         return st
 
-    def _decode(self, mb: int) -> Optional[StepMeta]:
+    @staticmethod
+    def _advance(st: _MBState, inflight: Optional[StepMeta]):
+        """(adv, src): adv[i] = 1 if sequence i is in the in-flight step (its token is not
+        applied yet), src[i] = its row in that step's output (-1 otherwise)."""
+        n = len(st.seqs)
+        if inflight is None or inflight.num_seqs == 0:
+            return np.zeros(n, np.int32), np.full(n, -1, np.int32)
+        ks = np.asarray(inflight.seq_ids, dtype=np.int64)
+        order = np.argsort(ks, kind="stable")
+        sk = ks[order]
+        pos = np.minimum(np.searchsorted(sk, st.sid), len(sk) - 1)
+        hit = sk[pos] == st.sid
+        return hit.astype(np.int32), np.where(hit, order[pos], -1).astype(np.int32)
+
+    def _decode(self, mb: int, inflight: Optional[StepMeta] = None) -> Optional[StepMeta]:
         if not self.running[mb]:
             return None
         while True:
             st = self._mb_state(mb)
             if len(st.seqs) == 0:
                 return None
+            adv, src = self._advance(st, inflight)
+            ctx_all = st.ctx + adv
+            out_all = st.out_cnt + adv
+            # a sequence the in-flight token completes (length budget / model length) is
+            # not scheduled again
+            keep = (adv == 0) | ((out_all < st.budget) & (ctx_all < self.max_model_len))
+            idx = np.nonzero(keep)[0]
+            if idx.size == 0:
+                return None
+            sid, ctx = st.sid[idx], ctx_all[idx]
             # only sequences whose new token starts a fresh block need allocation
-            need = np.nonzero((st.ctx - 1) % self.bs == 0)[0]
+            need = np.nonzero((ctx - 1) % self.bs == 0)[0]
             ok = True
             for i in need.tolist():
-                if not self.bm.ensure(int(st.sid[i]), int(st.ctx[i])):
+                if not self.bm.ensure(int(sid[i]), int(ctx[i])):
                     ok = False
                     break
             if ok:
                 break
             if not self._preempt(mb):
                 return None
-        sid = st.sid
-        ctx = st.ctx.copy()
-        slots = self.bm.slot_mapping(sid, ctx - 1, np.ones(len(sid), np.int32))
+        n = len(sid)
+        slots = self.bm.slot_mapping(sid, ctx - 1, np.ones(n, np.int32))
         tables = self.bm.fill_tables(sid, self.table_width)
-        seeds = row_seeds(st.seed, st.out_cnt)
-        return StepMeta(kind=DECODE, seq_ids=sid.tolist(), input_ids=st.last.copy(),
+        seeds = row_seeds(st.seed[idx], out_all[idx])
+        feed = src[idx]
+        meta = StepMeta(kind=DECODE, seq_ids=sid.tolist(), input_ids=st.last[idx],
                         positions=ctx - 1, slot_mapping=slots,
-                        seq_lens=np.ones(len(sid), np.int32), context_lens=ctx,
-                        block_tables=tables, temperature=st.temp, top_k=st.topk, top_p=st.topp,
-                        seeds=seeds, microbatch=mb, step_id=self._step)
+                        seq_lens=np.ones(n, np.int32), context_lens=ctx,
+                        block_tables=tables, temperature=st.temp[idx], top_k=st.topk[idx],
+                        top_p=st.topp[idx], seeds=seeds, microbatch=mb, step_id=self._step)
+        if (feed >= 0).any():
+            meta.feed_src = feed
+        return meta
 
     # ------------------------------------------------------------------ results
     def update(self, meta: StepMeta, tokens) -> List[Sequence]:

@@ -135,7 +135,8 @@ class ExpertParallelEngine:
         self.engine = LLMEngine(cfg, device=str(dev), dtype=dtype, max_batch=max_batch,
                                 max_model_len=max_model_len, num_blocks=num_blocks,
                                 use_graphs=False, lm=lm,
-                                max_prefill_tokens=max_prefill_tokens)
+                                max_prefill_tokens=max_prefill_tokens,
+                                lookahead=False)   # every forward joins the ranks' all-to-alls
         self.device = dev
 
     def _any_work(self) -> bool:

@@ -36,6 +36,9 @@ for s in "$@"; do
           rm -f gpurun_out/prof_mixtral/*trace.csv ;;
     pp2) step pp2 900 env DLI_DIST_BACKEND=gloo DLI_SAME_DEVICE=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 1 --warmup 1 --batch 64 ;;
     pp4) step pp4 900 env DLI_DIST_BACKEND=gloo DLI_SAME_DEVICE=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 4 --steps 1 --warmup 1 --batch 32 ;;
+    pp8) step pp8 900 env DLI_DIST_BACKEND=gloo DLI_SAME_DEVICE=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29536 bench.py --gpus 8 --steps 1 --warmup 1 --batch 16 ;;
+    nccl1) step nccl1_pp 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29537 bench.py --gpus 2 --mode pp --steps 1 --warmup 1 --batch 64
+           step nccl1_dp 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29538 bench.py --gpus 2 --mode dp --steps 1 --warmup 1 --batch 64 ;;
     gemm) step gemm 1100 python scripts/bench_gemm.py ;;
     ops) step ops 600 python scripts/bench_ops.py ;;
     ab) step ab_fused 600 python bench.py --steps 2 --warmup 1
@@ -46,6 +49,10 @@ for s in "$@"; do
     ep2) step ep2 900 env DLI_DIST_BACKEND=gloo DLI_SAME_DEVICE=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29535 bench.py --model mixtral-8x7b --gpus 2 --steps 1 --warmup 1 --batch 32 ;;
     llama70) step llama70 1100 python bench.py --model llama3-70b --steps 1 --warmup 1 --batch 64 ;;
     bench_small) step bench_small 600 python bench.py --steps 2 --warmup 1 --batch 64 ;;
+    lookahead) step la_on 600 python bench.py --steps 3 --warmup 1
+               step la_off 600 env DLI_LOOKAHEAD=0 python bench.py --steps 3 --warmup 1
+               step la_on2 600 python bench.py --steps 3 --warmup 1 ;;
+    engine_tests) step engine_tests 900 python -u -m pytest tests/test_engine_gpu.py tests/test_lookahead.py -x -v --timeout 300 --timeout-method thread ;;
     noblas) step noblas 900 env DLI_GEMM_AUTOTUNE_LOG=1 python bench.py --steps 2 --warmup 1
             step withblas 900 env DLI_GEMM_DECODE_BLAS=1 DLI_GEMM_AUTOTUNE_LOG=1 python bench.py --steps 2 --warmup 1 ;;
     tune) step tune_off 600 python bench.py --steps 2 --warmup 1
