@@ -78,6 +78,51 @@ __device__ float block_scan(float v, float* tmp) {
   return v + add;
 }
 
+// Radix-select digit step: the largest bin d whose suffix count S(d) = sum_{b >= d} hist[b]
+// reaches k_rem (bins walked from 255 down), as one block scan over the 256 bins instead of
+// a serial walk by one thread (up to 256 dependent LDS reads per pass). sel = {digit, count
+// strictly above the digit's bin, count in it}; with S(0) < k_rem (fewer than k_rem keys):
+// {0, S(0), 0}, so sel[1] + sel[2] < k_rem tells that case apart.
+// All threads call it (block_scan barriers).
+__device__ __forceinline__ void find_digit(const uint32_t* hist, uint32_t k_rem, float* tmp,
+                                           uint32_t* sel) {
+  const int tid = threadIdx.x;
+  const uint32_t h = tid < 256 ? hist[255 - tid] : 0u;
+  const uint32_t S = (uint32_t)block_scan((float)h, tmp);     // exact: counts < 2^24
+  if (tid < 256) {
+    const bool hit = S >= k_rem && S - h < k_rem;
+    if (hit || (tid == 255 && S < k_rem)) {
+      sel[0] = 255u - (uint32_t)tid;
+      sel[1] = hit ? S - h : S;
+      sel[2] = hit ? h : 0u;
+    }
+  }
+}
+
+// k-th largest non-zero key of keys[0..n) (LDS), 8-bit digits. Key 0 (an all-ones NaN
+// pattern) marks an empty slot and is never counted. Returns 0 when fewer than k keys exist.
+__device__ uint32_t radix_kth(const uint32_t* keys, int n, uint32_t k, uint32_t* hist,
+                              float* tmp, uint32_t* sel) {
+  uint32_t prefix = 0, pmask = 0, k_rem = k;
+  for (int pass = 0; pass < 4; ++pass) {
+    const int shift = 24 - 8 * pass;
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) hist[i] = 0;
+    __syncthreads();
+    for (int e = threadIdx.x; e < n; e += blockDim.x) {
+      const uint32_t key = keys[e];
+      if (key != 0u && (key & pmask) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    find_digit(hist, k_rem, tmp, sel);
+    __syncthreads();
+    if (k_rem > sel[1] + sel[2]) return 0u;                    // fewer than k keys
+    k_rem -= sel[1];
+    prefix |= sel[0] << shift;
+    pmask |= 255u << shift;
+  }
+  return prefix;
+}
+
 // Visit every element of a row with 16-B loads, 4 loads in flight per thread (the sampler is
 // one workgroup per row, so memory-level parallelism per CU comes from ILP, not occupancy).
 template <typename F>
@@ -117,7 +162,7 @@ __global__ void __launch_bounds__(SMP_THREADS) sample_kernel(
   __shared__ float cprob[SMP_CAP];
   __shared__ float sv[16];
   __shared__ int si[16];
-  __shared__ uint32_t s_digit, s_above, s_inbin, s_cnt;
+  __shared__ uint32_t s_sel[3], s_cnt;
   const int row = blockIdx.x, tid = threadIdx.x;
   const float* x = logits + (long)row * row_stride;
   const float T = temperature[row];
@@ -157,18 +202,29 @@ __global__ void __launch_bounds__(SMP_THREADS) sample_kernel(
 
   int n = 0;
   bool fast_ok = false;
-  // ---- fast path: one pass over the row, each thread keeps its top-8 (key, index) in
-  // registers (static-index insertion network); the Keff-th largest of the 4096 candidates
-  // (tau) is exact iff no thread dropped an element >= tau, i.e. every thread's 8th kept key
-  // is < tau — checked with one block-wide OR. Otherwise fall back to the full radix select.
+  // ---- fast path, no full-row select:
+  //  (1) tau0 = the Keff-th largest of the 512 per-thread maxima over the row's first
+  //      quarter. At least Keff elements are >= tau0, so tau0 <= the row's Keff-th largest.
+  //  (2) one pass over the row; each thread keeps its top-8 (key, index) in registers
+  //      (static-index insertion network) among the elements >= tau0 only. Unguarded, the
+  //      network ran for nearly every element: some lane of the wave almost always had a
+  //      new local top-8 entry, and the whole wave pays for it.
+  //  The Keff-th largest of the candidates (tau) is exact iff no thread dropped an element
+  //  >= tau, i.e. every thread's 8th kept key is < tau — one block-wide OR. Otherwise the
+  //  full radix select below.
   if (Keff <= 256) {
+    uint32_t mk = 0u;
+    row_scan(x, (V >> 4) << 2, [&](float v, int) { mk = max(mk, f2key(v)); });
+    ckey[tid] = mk;
+    __syncthreads();
+    const uint32_t tau0 = radix_kth(ckey, SMP_THREADS, (uint32_t)Keff, hist, sv, s_sel);
     uint32_t tk[8];
     int ti[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) { tk[j] = 0u; ti[j] = 0x7fffffff; }
     row_scan(x, V, [&](float v, int i) {
       uint32_t k = f2key(v);
-      if (k > tk[7]) {
+      if (k >= tau0 && k > tk[7]) {
         int id = i;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -179,34 +235,14 @@ __global__ void __launch_bounds__(SMP_THREADS) sample_kernel(
         }
       }
     });
+    __syncthreads();                              // every thread is past radix_kth's reads
 #pragma unroll
     for (int j = 0; j < 8; ++j) { ckey[tid * 8 + j] = tk[j]; cidx[tid * 8 + j] = ti[j]; }
     __syncthreads();
-    uint32_t prefix = 0, pmask = 0, k_rem = (uint32_t)Keff;
-    for (int pass = 0; pass < 4; ++pass) {
-      const int shift = 24 - 8 * pass;
-      for (int i = tid; i < 256; i += blockDim.x) hist[i] = 0;
-      __syncthreads();
-      for (int e = tid; e < 8 * SMP_THREADS; e += blockDim.x) {
-        const uint32_t k = ckey[e];
-        if ((k & pmask) == prefix) atomicAdd(&hist[(k >> shift) & 255u], 1u);
-      }
-      __syncthreads();
-      if (tid == 0) {
-        uint32_t cum = 0, d = 0;
-        for (int bb = 255; bb >= 0; --bb) {
-          if (cum + hist[bb] >= k_rem) { d = (uint32_t)bb; break; }
-          cum += hist[bb];
-        }
-        s_digit = d; s_above = cum;
-      }
-      __syncthreads();
-      k_rem -= s_above;
-      prefix |= s_digit << shift;
-      pmask |= 255u << shift;
-    }
-    const uint32_t tau = prefix;                  // key of the Keff-th largest candidate
-    fast_ok = !__syncthreads_or(tk[7] >= tau ? 1 : 0);
+    // key of the Keff-th largest candidate (0: fewer than Keff candidates)
+    const uint32_t tau = radix_kth(ckey, 8 * SMP_THREADS, (uint32_t)Keff, hist, sv, s_sel);
+    const int dropped = __syncthreads_or(tk[7] >= tau ? 1 : 0);
+    fast_ok = tau != 0u && !dropped;
     if (fast_ok) {
       if (tid == 0) s_cnt = 0;
       __syncthreads();
@@ -238,20 +274,13 @@ __global__ void __launch_bounds__(SMP_THREADS) sample_kernel(
       if ((k & pmask) == prefix) atomicAdd(&hist[(k >> shift) & 255u], 1u);
     });
     __syncthreads();
-    if (tid == 0) {
-      uint32_t cum = 0, d = 0;
-      for (int b = 255; b >= 0; --b) {
-        if (cum + hist[b] >= k_rem) { d = (uint32_t)b; break; }
-        cum += hist[b];
-      }
-      s_digit = d; s_above = cum; s_inbin = hist[d];
-    }
+    find_digit(hist, k_rem, sv, s_sel);
     __syncthreads();
-    k_rem -= s_above;
-    above_total += s_above;
-    prefix |= s_digit << shift;
+    k_rem -= s_sel[1];
+    above_total += s_sel[1];
+    prefix |= s_sel[0] << shift;
     pmask |= 255u << shift;
-    if (above_total + s_inbin <= SMP_CAP) break;
+    if (above_total + s_sel[2] <= SMP_CAP) break;
   }
   // ---- gather everything at or above the boundary bin
   if (tid == 0) s_cnt = 0;
@@ -308,18 +337,26 @@ __global__ void __launch_bounds__(SMP_THREADS) sample_kernel(
   for (int j = 0; j < PER; ++j) { run += loc[j]; cprob[tid * PER + j] = run; }
   __syncthreads();
   const float Z = cprob[m - 1];
-  // keep entries whose exclusive prefix < P * Z
-  if (tid == 0) {
-    const float lim = P * Z;
-    int c = 1;
-    while (c < m && cprob[c - 1] < lim) ++c;
-    const float zk = cprob[c - 1];
-    const uint4 r = philox(key, make_uint4(0xfffffffu, 1u, 0xa5a5a5a5u, 7u));
-    const float u = u01(r.x) * zk;
-    int j = 0;
-    while (j < c - 1 && cprob[j] <= u) ++j;
-    out_tokens[row] = cidx[j];
-  }
+  // keep entries whose exclusive prefix < P * Z: c = 1 + (first j < m-1 with cprob[j] >= lim,
+  // else m-1); then the draw j = first j < c-1 with cprob[j] > u, else c-1. Both "first
+  // index" searches run over all threads with an LDS atomicMin (was one thread's serial walk)
+  const float lim = P * Z;
+  if (tid == 0) s_cnt = (uint32_t)(m - 1);
+  __syncthreads();
+  for (int e = tid; e < m - 1; e += blockDim.x)
+    if (cprob[e] >= lim) atomicMin(&s_cnt, (uint32_t)e);
+  __syncthreads();
+  const int c = (int)s_cnt + 1;
+  const float zk = cprob[c - 1];
+  const uint4 r = philox(key, make_uint4(0xfffffffu, 1u, 0xa5a5a5a5u, 7u));
+  const float u = u01(r.x) * zk;
+  __syncthreads();                                // s_cnt read by every thread
+  if (tid == 0) s_cnt = (uint32_t)(c - 1);
+  __syncthreads();
+  for (int e = tid; e < c - 1; e += blockDim.x)
+    if (cprob[e] > u) atomicMin(&s_cnt, (uint32_t)e);
+  __syncthreads();
+  if (tid == 0) out_tokens[row] = cidx[s_cnt];
 }
 
 extern "C" int dli_sample(int* out_tokens, const float* logits, long row_stride, int B, int V,
