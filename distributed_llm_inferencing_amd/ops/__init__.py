@@ -167,13 +167,17 @@ def _splitk_plan(x, w):
     return p if (p.backend == "dli" and p.splits > 1) else None
 
 
-def linear_add_rmsnorm(x, w, residual, norm_w, eps):
+def linear_add_rmsnorm(x, w, residual, norm_w, eps, plan: Optional[G.GemmPlan] = None):
     """residual += x @ w.T (bf16-rounded, in place); returns rmsnorm(residual) * norm_w
     (None when norm_w is None). Split-K GEMMs reduce their partial slabs inside the norm
-    kernel (fused_reduce.hip), so the bf16 GEMM output is never materialised."""
-    p = _splitk_plan(x, w)
+    kernel (fused_reduce.hip), so the bf16 GEMM output is never materialised.
+    ``plan`` forces the GEMM plan (the autotuner times every candidate with its consumer)."""
+    if plan is None:
+        p = _splitk_plan(x, w)
+    else:
+        p = plan if (plan.backend == "dli" and plan.splits > 1) else None
     if p is None:
-        y = linear(x, w)
+        y = linear(x, w) if plan is None else _gemm_native(x, w, "none", plan=plan)
         if norm_w is None:
             residual.add_(y)             # bf16 add computes in fp32 and rounds once
             return None

@@ -222,6 +222,13 @@ def autotune(shapes, weights: dict, device, iters: int = 6, log=None,
         n_copies = max(2, min(16, -(-cold_bytes // (w0.numel() * w0.element_size()))))
         ws_ = [w0] + [w0.clone() for _ in range(n_copies - 1)]
         x = (torch.randn(M, K, device=device) * 0.5).to(w0.dtype)
+        if epi == "splitk":
+            # a "splitk" GEMM is timed WITH its consumer: split plans reduce their slabs in a
+            # fused add+RMSNorm, unsplit plans write bf16 and run the separate add+RMSNorm
+            # pass (for QKV the real consumers are the RoPE/cache kernels of the same bytes
+            # pattern); timing the unsplit GEMM alone hid that pass and biased the choice
+            res = torch.zeros(M, N, dtype=w0.dtype, device=device)
+            nw = torch.ones(N, dtype=w0.dtype, device=device)
         best = None
         for p in candidate_plans(M, N, K, epi):
             if p.backend == "hipblaslt" and epi not in ("none", "splitk", "silu_mul", "f32"):
@@ -229,7 +236,10 @@ def autotune(shapes, weights: dict, device, iters: int = 6, log=None,
 
             def run(p=p):
                 for w in ws_:
-                    ops._gemm_native(x, w, epi, plan=p)
+                    if epi == "splitk":
+                        ops.linear_add_rmsnorm(x, w, res, nw, 1e-5, plan=p)
+                    else:
+                        ops._gemm_native(x, w, epi, plan=p)
             try:
                 ms = ops.benchmark(run, iters=iters, warmup=1) / len(ws_)
             except Exception:  # noqa: BLE001 — an invalid candidate is skipped
