@@ -20,6 +20,7 @@ import os
 import threading
 from dataclasses import dataclass
 
+import numpy as np
 import torch
 
 # tile id -> (BM, BN); 0-4 stage K through 2 LDS buffers, 5-9 are the same tiles with 3
@@ -131,15 +132,19 @@ def grouped_plan(rows: int, N: int, K: int, epi: str, groups: int) -> GemmPlan:
 
 def autotune_grouped(rows: int, w: torch.Tensor, epi: str, iters: int = 5, log=None):
     """Pick the grouped-GEMM tile for `rows` permuted rows over the experts of `w`
-    ([E, N, K]) with a uniform routing (what a decode step of rows/top_k tokens sees on
-    average). The expert weights together exceed the Infinity Cache, so every call is cold."""
+    ([E, N, K]) with a random routing (what a decode step of rows/top_k tokens sees). The
+    expert weights together exceed the Infinity Cache, so every call is cold."""
     from .. import ops
     E, N, K = w.shape
     key = (_bucket(rows), N, K, epi, E)
     if key in _grouped_cache or os.environ.get("DLI_MOE_TILE"):
         return _grouped_cache.get(key)
     dev = w.device
-    counts = [rows // E + (1 if e < rows % E else 0) for e in range(E)]
+    # per-expert rows of a RANDOM routing (seeded multinomial), not an exactly even split: with
+    # 1024 rows over 8 experts an even split fits 128-row tiles exactly, while in situ about
+    # half the experts get more than 128 rows and take a second tile pass over their weights
+    # (Mixtral b512: the even-split pick ran 13.6k tok/s, the 160-row tile 15.3k)
+    counts = np.random.default_rng(1234).multinomial(rows, [1.0 / E] * E).tolist()
     off = torch.tensor([0] + list(__import__("itertools").accumulate(counts)),
                        dtype=torch.int32, device=dev)
     x = (torch.randn(max(rows, 1), K, device=dev) * 0.5).to(w.dtype)
