@@ -658,6 +658,9 @@ static int dispatch_tile(int tile_cfg, const void* A, int lda, const void* W, in
     DLI_CFG(18, 128, 96, 2) DLI_CFG(19, 128, 96, 3) DLI_CFG(20, 128, 64, 2) DLI_CFG(21, 128, 64, 3)
     // 256x256 8-phase ping-pong (gemm8p_kernel)
     case 22: return launch_8p<EPI, GEMM8P_DEFAULT>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
+    // 192-wide tiles: N = 6144 (fused QKV) = 32 column tiles, so M = 512 fills 256 CUs with
+    // 4 x 32 x split 2 (128-row) or 2 x 32 x split 4 (256-row) workgroups of 8 waves
+    DLI_CFG8(23, 128, 192, 3, 2, 4) DLI_CFG8(24, 128, 192, 2, 2, 4) DLI_CFG8(25, 256, 192, 2, 4, 2)
 #undef DLI_CFG8
 #undef DLI_CFG
     default: return (int)hipErrorInvalidValue;
@@ -668,7 +671,8 @@ static int dispatch_tile(int tile_cfg, const void* A, int lda, const void* W, in
 // tiles with 3 LDS stages (one tile in flight across the barrier); 10/11 = 192x128 with 2/3
 // stages, 12 = 160x128 (MoE experts of ~130-190 rows in one pass); 13-17 = 8-wave tiles
 // 256x256, 256x128, 128x256 (2 stages) and 256x128, 128x256 (3 stages); 18/19 = 128x96 and
-// 20/21 = 128x64 with 2/3 stages; 22 = 256x256 8-phase ping-pong. ws: fp32 [splits, M, N] when splits>1.
+// 20/21 = 128x64 with 2/3 stages; 22 = 256x256 8-phase ping-pong; 23/24 = 128x192 (3/2
+// stages), 25 = 256x192, 8 waves. ws: fp32 [splits, M, N] when splits>1.
 // group_off (nullable): int[groups+1] row offsets; M is then the max rows of any group.
 extern "C" int dli_gemm(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M,
                         int N, int K, int epi, int tile_cfg, int splits, const void* bias,

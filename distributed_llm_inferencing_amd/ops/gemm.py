@@ -33,9 +33,12 @@ TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256), 4: (256, 128),
          # grid-filling tiles for N = 6144 / 4096 at M = 512
          18: (128, 96), 19: (128, 96), 20: (128, 64), 21: (128, 64),
          # 256x256 8-phase ping-pong (two wave groups alternate MFMA / load segments)
-         22: (256, 256)}
+         22: (256, 256),
+         # 192-wide, 8 waves: N = 6144 is 32 column tiles (fused QKV at M = 512 fills the chip
+         # with split-K 2 / 4)
+         23: (128, 192), 24: (128, 192), 25: (256, 192)}
 TILE_WAVES = {13: (2, 4), 14: (4, 2), 15: (2, 4), 16: (4, 2), 17: (2, 4),
-              22: (2, 4)}   # default 2 x 2
+              22: (2, 4), 23: (2, 4), 24: (2, 4), 25: (4, 2)}   # default 2 x 2
 
 
 def tile_ok(tile: int, epi: str) -> bool:
