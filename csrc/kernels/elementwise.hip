@@ -99,3 +99,23 @@ extern "C" int dli_bias_act(void* x, const void* bias, int T, int N, int act, hi
                                                                act);
   DLI_RETURN_LAUNCH();
 }
+
+// Lookahead input ids (engine/llm_engine.py): ids[i] = feed[src[i]] where src[i] >= 0, i.e. the
+// token the in-flight step sampled for that sequence; src[i] < 0 keeps the host-provided id.
+// One launch instead of a clamp / gather / compare / select / copy chain of torch ops.
+__global__ void __launch_bounds__(256) feed_ids_kernel(int* __restrict__ ids,
+                                                       const int* __restrict__ src,
+                                                       const int* __restrict__ feed, int n,
+                                                       int n_feed) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int s = src[i];
+  if (s >= 0 && s < n_feed) ids[i] = feed[s];
+}
+
+extern "C" int dli_feed_ids(int* ids, const int* src, const int* feed, int n, int n_feed,
+                            hipStream_t st) {
+  if (n <= 0) return 0;
+  feed_ids_kernel<<<(n + 255) / 256, 256, 0, st>>>(ids, src, feed, n, n_feed);
+  DLI_RETURN_LAUNCH();
+}

@@ -17,6 +17,7 @@ from typing import Dict, Optional
 import numpy as np
 import torch
 
+from .. import ops
 from ..models.model import TransformerLM
 from .batch import DECODE, PREFILL, DeviceBatch, StepMeta, to_device
 from .kv_cache import KVCache
@@ -227,8 +228,7 @@ class StageRunner:
     def _feed(ids: torch.Tensor, src: torch.Tensor, feed: torch.Tensor) -> None:
         """Lookahead: ids[i] = feed[src[i]] where src[i] >= 0 (stream-ordered after the step
         that produced ``feed``, before this step's replay overwrites it)."""
-        take = feed.index_select(0, src.clamp(min=0).long()).to(ids.dtype)
-        ids.copy_(torch.where(src >= 0, take, ids))
+        ops.feed_ids(ids, src, feed)
 
     def run(self, meta: StepMeta, hidden: Optional[torch.Tensor] = None,
             feed: Optional[torch.Tensor] = None) -> torch.Tensor:

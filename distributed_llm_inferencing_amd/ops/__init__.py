@@ -215,6 +215,19 @@ def linear_rope_cache(x, w, positions, slot_mapping, cos_sin, k_cache, v_cache, 
     return qkv
 
 
+def feed_ids(ids, src, feed):
+    """In place: ids[i] = feed[src[i]] where src[i] >= 0 (int32 tensors; lookahead input ids
+    taken from the in-flight step's sampled tokens)."""
+    if not _use_native(ids):
+        take = feed.index_select(0, src.clamp(min=0).long()).to(ids.dtype)
+        ids.copy_(torch.where(src >= 0, take, ids))
+        return ids
+    if ids.dtype != torch.int32 or src.dtype != torch.int32 or feed.dtype != torch.int32:
+        raise ValueError("feed_ids: int32 tensors expected")
+    _native_call("dli_feed_ids", _p(ids), _p(src), _p(feed), ids.shape[0], feed.shape[0], _st())
+    return ids
+
+
 def silu_mul(gu):
     if not _use_native(gu):
         return R.silu_mul(gu)

@@ -378,3 +378,14 @@ def test_vocab_parallel_candidates_sample_like_full_vocab(gpu):
     a = ops.sample(full, temp, topk, topp, seeds)
     b = ops.sample(vals, temp, topk, topp, seeds, ids=ids)
     assert torch.equal(a, b)
+
+
+def test_feed_ids(gpu):
+    """Lookahead id feed: ids[i] = feed[src[i]] where src[i] >= 0, host ids elsewhere."""
+    ids = torch.arange(100, 164, device=gpu, dtype=torch.int32)
+    feed = torch.arange(5000, 5040, device=gpu, dtype=torch.int32)
+    src = torch.full((64,), -1, device=gpu, dtype=torch.int32)
+    src[::3] = torch.arange(0, 64, 3, device=gpu, dtype=torch.int32) % 40
+    ref = torch.where(src >= 0, feed[src.clamp(min=0).long()], ids)
+    ops.feed_ids(ids, src, feed)
+    assert torch.equal(ids, ref)
