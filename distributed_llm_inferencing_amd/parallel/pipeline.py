@@ -45,6 +45,7 @@ from ..models.model import TransformerLM
 from ..runtime import BlockManager
 from ..shard.planner import StagePlan, plan_stages
 from ..tokenizer import load_tokenizer
+from ..utils import faults
 from .transport import H_TICK, PipeChannel, init_distributed
 
 SHUTDOWN = 4
@@ -318,6 +319,8 @@ def serve_session(stage: StageWorker, channel) -> int:
     prev_vp = False
     my_cand = None                  # my candidates of microbatch k-1-N
     while True:
+        if faults.active():
+            faults.check("pipeline.stage", tick=k)
         meta = None
         if k >= r:
             h, p = channel.recv_ctrl()

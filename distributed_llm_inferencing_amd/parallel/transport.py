@@ -206,7 +206,15 @@ class PipeChannel:
 
 
 def init_distributed(backend: Optional[str] = None, device: Optional[torch.device] = None):
-    """Initialise torch.distributed from torchrun env vars (127.0.0.1 rendezvous)."""
+    """Initialise torch.distributed from torchrun env vars (127.0.0.1 rendezvous).
+
+    Failure detection: data-plane operations get a bounded timeout
+    (``DLI_PP_TIMEOUT_S``, default 600 s), so a stage that dies mid-session turns a blocked
+    exchange into an error: RCCL's watchdog aborts the communicator when the timeout fires
+    (torch's ``TORCH_NCCL_ASYNC_ERROR_HANDLING`` default), gloo raises as soon as the dead
+    peer's sockets close. The head then fails its pending requests and reports unhealthy
+    (``worker/service.PipelineService``); the master's failure detector routes new requests
+    to the remaining replicas."""
     if dist.is_initialized():
         return dist.get_rank(), dist.get_world_size()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -214,7 +222,7 @@ def init_distributed(backend: Optional[str] = None, device: Optional[torch.devic
     if backend is None:
         backend = os.environ.get("DLI_DIST_BACKEND") or (
             "nccl" if torch.cuda.is_available() else "gloo")
-    kw = {}
+    kw = {"timeout": timedelta(seconds=float(os.environ.get("DLI_PP_TIMEOUT_S", "600")))}
     if backend == "nccl" and device is not None:
         kw["device_id"] = device
     dist.init_process_group(backend=backend, **kw)

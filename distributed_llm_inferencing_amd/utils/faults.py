@@ -8,6 +8,8 @@
     worker.inference:exit_after:<n>  hard-exit the worker process after n requests (node death)
     worker.health:error[:p]          /health answers 503 (drives the failure detector)
     transport.exchange:error:<tick>  the pipeline transport raises at that tick (link failure)
+    pipeline.stage:exit_after:<n>    a non-head pipeline rank hard-exits after n ticks (GPU /
+                                     process death mid-session)
     dispatch.post:error[:p]          the master's HTTP call to a worker fails (connection error)
 
 Rules are parsed once per process (``reload()`` re-reads the variable, used by tests).

@@ -211,6 +211,10 @@ def create_worker_app(settings: Optional[Settings] = None, device: Optional[str]
             faults.check("worker.health")
         except faults.InjectedFault as e:
             return jsonify({"status": "error", "message": str(e)}), 503
+        psvc = getattr(st, "pipeline_service", None)
+        if psvc is not None and psvc.error is not None:      # a stage of this ring died
+            return jsonify({"status": "error",
+                            "message": f"pipeline failed: {psvc.error}"}), 503
         shard_info = [{"model_name": m, "shard_id": sid, "path": r["path"],
                        "metadata": r["metadata"]}
                       for m, sh in st.shards.items() for sid, r in sh.items()]

@@ -92,7 +92,12 @@ class EngineService:
 
 class PipelineService:
     """Same interface, backed by the rank-0 head of a DistributedPipelineEngine: requests
-    are batched into ring sessions."""
+    are batched into ring sessions.
+
+    A session that raises (a stage died, a link failed, the data-plane timeout fired) leaves
+    the ring unusable: every pending and later request fails at once with that error, and
+    ``error`` is set so the worker's /health reports the node unhealthy (the master's failure
+    detector then takes it out of rotation) instead of hanging requests on a broken ring."""
 
     def __init__(self, pipe_engine, name: str = "pipeline"):
         self.engine = pipe_engine
@@ -101,16 +106,28 @@ class PipelineService:
         self._stop = threading.Event()
         self._ids = 0
         self._lock = threading.Lock()
+        self.error: Optional[BaseException] = None
         self._t = threading.Thread(target=self._run, name=f"dli-pipe-{name}", daemon=True)
         self._t.start()
 
     def submit(self, prompt, params=None) -> Future:
         fut: Future = Future()
+        if self.error is not None:
+            fut.set_exception(RuntimeError(f"pipeline {self.name} failed: {self.error}"))
+            return fut
         with self._lock:
             self._ids += 1
             rid = f"{self.name}-{self._ids}"
         self._inbox.put((rid, prompt, params, fut))
         return fut
+
+    def _fail_pending(self):
+        while True:
+            try:
+                _rid, _p, _s, fut = self._inbox.get_nowait()
+            except queue.Empty:
+                return
+            fut.set_exception(RuntimeError(f"pipeline {self.name} failed: {self.error}"))
 
     def generate(self, prompt, params=None, timeout=None):
         return self.submit(prompt, params).result(timeout=timeout)
@@ -137,10 +154,12 @@ class PipelineService:
                     fut.set_exception(e)
             try:
                 outs = head.run_session()
-            except BaseException as e:  # noqa: BLE001
+            except BaseException as e:  # noqa: BLE001 — the ring is broken: fail fast, for good
+                self.error = e
                 for f in futs.values():
                     f.set_exception(e)
-                continue
+                self._fail_pending()
+                return
             for o in outs:
                 f = futs.pop(o.request_id, None)
                 if f is not None:
@@ -149,6 +168,7 @@ class PipelineService:
     def stats(self) -> dict:
         s = self.engine.head.stats.snapshot()
         s["queued"] = self._inbox.qsize()
+        s["failed"] = None if self.error is None else str(self.error)
         return s
 
     def close(self):

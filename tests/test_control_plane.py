@@ -327,3 +327,15 @@ def test_loadgen_end_to_end(tmp_path, master):
     finally:
         ms.close()
         w.close()
+
+
+def test_worker_health_reports_failed_pipeline(worker):
+    """A pipeline head whose ring broke (PipelineService.error set) answers /health with 503,
+    so the master's heartbeat takes the node out of rotation."""
+    assert worker.get("/health").status_code == 200
+
+    class _Broken:
+        error = RuntimeError("stage 3 died")
+    worker.application.extensions["dli_worker"].pipeline_service = _Broken()
+    r = worker.get("/health")
+    assert r.status_code == 503 and "stage 3 died" in r.get_json()["message"]

@@ -203,3 +203,57 @@ def test_tensor_parallel_gloo_matches_dense():
     assert res[0][1][0] == greedy and res[1][1][0] == greedy
     assert res[0][1][1] == res[1][1][1]            # ranks agree on sampled tokens
     assert res[0][2] > 0 and res[0][3] == 1        # 2 kv heads split over 2 ranks
+
+
+def _dying_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), DLI_PP_VOCAB_PARALLEL="0",
+                      DLI_PP_TIMEOUT_S="60")
+    if rank == 1:
+        os.environ["DLI_FAULT"] = "pipeline.stage:exit_after:6"   # dies on its 7th tick
+    torch.set_num_threads(1)
+    import time
+    from distributed_llm_inferencing_amd.parallel.pipeline import DistributedPipelineEngine
+    from distributed_llm_inferencing_amd.worker.service import PipelineService
+    eng = DistributedPipelineEngine("llama-tiny", "cpu", max_batch=8, max_model_len=64,
+                                    num_blocks=256, dtype=torch.float32)
+    if rank != 0:
+        eng.serve()                   # never returns: the fault hard-exits this process
+        return
+    svc = PipelineService(eng, name="pp")
+    t0 = time.perf_counter()
+    sp = SamplingParams(max_length=30, do_sample=False, ignore_eos=True)
+    err = None
+    try:
+        svc.generate(PROMPTS[0], sp, timeout=120)
+    except Exception as e:  # noqa: BLE001
+        err = repr(e)
+    later = None
+    try:
+        svc.generate(PROMPTS[1], sp, timeout=5)
+    except Exception as e:  # noqa: BLE001
+        later = repr(e)
+    q.put((err, later, svc.error is not None, time.perf_counter() - t0))
+    q.close()
+    q.join_thread()                   # flush the queue before the hard exit below
+    os._exit(0)                       # the ring is gone: no collective teardown possible
+
+
+def test_pipeline_stage_death_fails_fast_and_marks_unhealthy():
+    """SURVEY.md §5.3 failure detection: a stage process that dies mid-session (injected
+    hard exit) turns into an error on the head within the data-plane timeout — not a hang —
+    the pending request fails, later requests fail immediately, and the service reports the
+    failure (the worker's /health then answers 503)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dying_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    err, later, failed, dt = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+    assert procs[1].exitcode == 17                       # the injected stage death
+    assert err is not None and later is not None and failed
+    assert "failed" in later
+    assert dt < 120
