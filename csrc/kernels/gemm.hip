@@ -12,7 +12,8 @@
 //    per-lane GLOBAL source address and the same XOR on the ds_read_b128 address (rule 21);
 //    verified conflict-free for all four ds_read_b128 lane groups of the 16x16x32 A/B maps.
 //  * XCD-aware bijective block remap (T1) with n-major tile order so consecutive tiles share
-//    one W panel in an XCD's L2.
+//    one W panel in an XCD's L2; split-K grids are remapped split-major so an XCD's blocks
+//    share one K slice of A and W (split_tile).
 //  * split-K over grid.y writes fp32 slabs; a second pass reduces and applies the epilogue.
 //  * grouped mode (MoE): grid.z = expert; rows of group g are [off[g], off[g+1]) of A/C,
 //    weights W + g*N*ldw. Rows past the group end are skipped. Split-K composes with it
@@ -53,6 +54,24 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
+// Block -> (output tile, K split). Without split-K: the XCD remap over tiles (n-major order,
+// so an XCD's tiles share W panels). With split-K, (split, tile) is one split-major index
+// remapped over the whole grid, so an XCD's blocks work on ONE K slice: its L2 fetches that
+// slice of A once instead of every XCD fetching all of A (rocprofv3 TCC_EA0_RDREQ_*: the
+// down projection at M=512, split 8, read 224 MB per call for 132 MB of operands).
+// The hardware places linear block id L = y * gridDim.x + x on XCD L % 8.
+__device__ __forceinline__ void split_tile(int nwg, bool grouped, int& tile, int& ks) {
+  if (grouped || gridDim.y == 1) {
+    tile = xcd_remap(blockIdx.x, nwg);
+    ks = blockIdx.y;
+    return;
+  }
+  const int total = nwg * (int)gridDim.y;
+  const int lg = xcd_remap((int)(blockIdx.y * gridDim.x + blockIdx.x), total);
+  ks = lg / nwg;
+  tile = lg - ks * nwg;
+}
+
 template <int BM, int BN, int EPI, int NS, int WM, int WN>
 __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(
     const u16* __restrict__ A, int lda, const u16* __restrict__ W, int ldw,
@@ -76,11 +95,12 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(
   const int tiles_m = (M + BM - 1) / BM;           // M = max rows per group in grouped mode
   const int tiles_n = (N + BN - 1) / BN;
   const int nwg = tiles_m * tiles_n;
-  const int tile = xcd_remap(blockIdx.x, nwg);
+  int tile, ks;
+  split_tile(nwg, group_off != nullptr, tile, ks);
   const int tn = tile / tiles_m, tm = tile % tiles_m;
   const int m0 = tm * BM, n0 = tn * BN;
   if (m0 >= Mg) return;                             // grouped: empty tile (block-uniform)
-  const int kb = blockIdx.y * k_split_len;
+  const int kb = ks * k_split_len;
   const int nk = min(k_split_len, K - kb) / BK;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -195,7 +215,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(
   // ---- epilogue. acc[i][j][r] = C[m0 + wm*BM/2 + 16i + 4fq + r][n0 + wn*BN/2 + 16j + fr]
   const bool split = gridDim.y > 1;
   if (split) {
-    float* slab = ws + (long)blockIdx.y * M * N;
+    float* slab = ws + (long)ks * M * N;
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -287,7 +307,8 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(
   }
   const int tiles_m = (M + BM - 1) / BM;
   const int tiles_n = (N + BN - 1) / BN;
-  const int tile = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  int tile, ks;
+  split_tile(tiles_m * tiles_n, group_off != nullptr, tile, ks);
   int tn, tm;
   constexpr int GM = (VAR & 8) ? 4 : (VAR & 16) ? 8 : 1;
   if (GM > 1) {
@@ -305,7 +326,7 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(
   }
   const int m0 = tm * BM, n0 = tn * BN;
   if (m0 >= Mg) return;
-  const int kb = blockIdx.y * k_split_len;
+  const int kb = ks * k_split_len;
   const int nk = min(k_split_len, K - kb) / BK;
   const u16* Ab = A + (long)row0 * lda;
 
@@ -504,7 +525,7 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(
   // ---- epilogue: acc[I][J][r] = C[m0 + 128g + 16I + 4fq + r][n0 + 64gw + 16J + fr]
   const int wr0 = m0 + 128 * g, wc0 = n0 + 64 * gw;
   if (gridDim.y > 1) {
-    float* slab = ws + (long)blockIdx.y * M * N;
+    float* slab = ws + (long)ks * M * N;
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
