@@ -19,7 +19,7 @@ import torch
 
 from .. import ops
 from ..models.model import TransformerLM
-from .batch import DECODE, PREFILL, DeviceBatch, StepMeta, to_device
+from .batch import DECODE, DeviceBatch, StepMeta, to_device
 from .kv_cache import KVCache
 
 DEFAULT_BUCKETS = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192, 256, 320, 384, 448, 512)

@@ -21,7 +21,7 @@ from __future__ import annotations
 
 import os
 import time
-from typing import List, Optional
+from typing import Optional
 
 import torch
 import torch.distributed as dist

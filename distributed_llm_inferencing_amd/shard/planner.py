@@ -16,7 +16,7 @@ HBM capacity (weights + a KV reserve).
 from __future__ import annotations
 
 from dataclasses import asdict, dataclass
-from typing import List, Optional, Sequence, Tuple
+from typing import List, Sequence, Tuple
 
 from ..models.configs import ModelConfig
 

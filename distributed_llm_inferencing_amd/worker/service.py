@@ -12,7 +12,7 @@ import queue
 import threading
 import time
 from concurrent.futures import Future
-from typing import Any, Optional
+from typing import Optional
 
 from ..engine.sequence import SamplingParams
 

@@ -3,7 +3,6 @@
 vs PyTorch TunableOp (which times every hipBLASLt/rocBLAS solution for the shape once).
 Prints one JSON line per shape: default_us, tuned_us."""
 import json
-import os
 import sys
 import time
 
