@@ -70,7 +70,9 @@ def test_gemm_bf16_all_tiles(gpu, M, N, K):
     x, w = rnd(M, K, dev=gpu), rnd(N, K, dev=gpu, scale=0.05)
     ref = R.linear(x, w, out_dtype=torch.float32)
     for tile in G.TILES:
-        for splits in (1, 2, 4):
+        # split 8: (split, tile) grids whose size is not a multiple of the 8 XCDs exercise
+        # the split-major block remap (gemm.hip split_tile)
+        for splits in (1, 2, 4, 8):
             if K % (64 * splits):
                 continue
             out = ops._gemm_native(x, w, "none", plan=G.GemmPlan("dli", tile, splits))
