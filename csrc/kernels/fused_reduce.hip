@@ -10,7 +10,10 @@
 // / rotation, exactly as the bf16 GEMM output would be.
 #include "common.h"
 
-template <int VPT>
+// SPL > 0: the split count is a compile-time constant, so every partial of a thread is
+// loaded before the first add (SPL x VPT x 2 16-B loads in flight per lane instead of 2 x VPT);
+// SPL == 0 reads `splits` partials in a runtime loop.
+template <int VPT, int SPL>
 __global__ void __launch_bounds__(256) splitk_add_rmsnorm_kernel(
     u16* __restrict__ out, u16* __restrict__ residual, const float* __restrict__ ws, int splits,
     int M, int N, const u16* __restrict__ w, float eps) {
@@ -24,11 +27,26 @@ __global__ void __launch_bounds__(256) splitk_add_rmsnorm_kernel(
     const int vi = threadIdx.x + i * blockDim.x;
     if (vi < nvec) {
       float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      for (int s = 0; s < splits; ++s) {
-        const float4* p = reinterpret_cast<const float4*>(ws + ((long)s * M + row) * N + vi * 8);
-        const float4 a = p[0], b = p[1];
-        acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
-        acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
+      if constexpr (SPL > 0) {
+        float4 pa[SPL], pb[SPL];
+#pragma unroll
+        for (int s = 0; s < SPL; ++s) {
+          const float4* p = reinterpret_cast<const float4*>(ws + ((long)s * M + row) * N + vi * 8);
+          pa[s] = p[0];
+          pb[s] = p[1];
+        }
+#pragma unroll
+        for (int s = 0; s < SPL; ++s) {
+          acc[0] += pa[s].x; acc[1] += pa[s].y; acc[2] += pa[s].z; acc[3] += pa[s].w;
+          acc[4] += pb[s].x; acc[5] += pb[s].y; acc[6] += pb[s].z; acc[7] += pb[s].w;
+        }
+      } else {
+        for (int s = 0; s < splits; ++s) {
+          const float4* p = reinterpret_cast<const float4*>(ws + ((long)s * M + row) * N + vi * 8);
+          const float4 a = p[0], b = p[1];
+          acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
+          acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
+        }
       }
       float r[8];
       u16* rp = residual + (long)row * N + vi * 8;
@@ -55,6 +73,20 @@ __global__ void __launch_bounds__(256) splitk_add_rmsnorm_kernel(
   }
 }
 
+template <int VPT>
+static int launch_add_rmsnorm(u16* o, u16* r, const float* ws, int splits, int M, int N,
+                              const u16* wp, float eps, int threads, hipStream_t st) {
+  // the register-resident partials of SPL x VPT cap the unrolled variants at 8 slabs
+  switch (VPT <= 2 ? splits : 0) {
+    case 2: splitk_add_rmsnorm_kernel<VPT, 2><<<M, threads, 0, st>>>(o, r, ws, 2, M, N, wp, eps); break;
+    case 3: splitk_add_rmsnorm_kernel<VPT, 3><<<M, threads, 0, st>>>(o, r, ws, 3, M, N, wp, eps); break;
+    case 4: splitk_add_rmsnorm_kernel<VPT, 4><<<M, threads, 0, st>>>(o, r, ws, 4, M, N, wp, eps); break;
+    case 8: splitk_add_rmsnorm_kernel<VPT, 8><<<M, threads, 0, st>>>(o, r, ws, 8, M, N, wp, eps); break;
+    default: splitk_add_rmsnorm_kernel<VPT, 0><<<M, threads, 0, st>>>(o, r, ws, splits, M, N, wp, eps);
+  }
+  DLI_RETURN_LAUNCH();
+}
+
 extern "C" int dli_splitk_add_rmsnorm(void* out, void* residual, const float* ws, int splits,
                                       int M, int N, const void* w, float eps, hipStream_t st) {
   if (M <= 0) return 0;
@@ -65,14 +97,13 @@ extern "C" int dli_splitk_add_rmsnorm(void* out, void* residual, const float* ws
   const int vpt = (nvec + threads - 1) / threads;
   auto o = (u16*)out; auto r = (u16*)residual; auto wp = (const u16*)w;
   switch (vpt) {
-    case 1: splitk_add_rmsnorm_kernel<1><<<M, threads, 0, st>>>(o, r, ws, splits, M, N, wp, eps); break;
-    case 2: splitk_add_rmsnorm_kernel<2><<<M, threads, 0, st>>>(o, r, ws, splits, M, N, wp, eps); break;
-    case 3: case 4: splitk_add_rmsnorm_kernel<4><<<M, threads, 0, st>>>(o, r, ws, splits, M, N, wp, eps); break;
+    case 1: return launch_add_rmsnorm<1>(o, r, ws, splits, M, N, wp, eps, threads, st);
+    case 2: return launch_add_rmsnorm<2>(o, r, ws, splits, M, N, wp, eps, threads, st);
+    case 3: case 4: return launch_add_rmsnorm<4>(o, r, ws, splits, M, N, wp, eps, threads, st);
     case 5: case 6: case 7: case 8:
-      splitk_add_rmsnorm_kernel<8><<<M, threads, 0, st>>>(o, r, ws, splits, M, N, wp, eps); break;
+      return launch_add_rmsnorm<8>(o, r, ws, splits, M, N, wp, eps, threads, st);
     default: return (int)hipErrorInvalidValue;
   }
-  DLI_RETURN_LAUNCH();
 }
 
 // one lane: 8 dims of the first half of a head + the matching 8 of the second half

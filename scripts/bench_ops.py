@@ -46,6 +46,16 @@ def main():
     w = torch.ones(D, device=dev, dtype=torch.bfloat16)
     ms = ops.benchmark(lambda: ops.add_rmsnorm(x, r, w, 1e-5), iters=50)
     res["add_rmsnorm"] = (ms * 1e3, 4 * B * D * 2 / ms / 1e9)
+    # split-K reduce + residual add + RMSNorm alone, at the decode O/down shape (M=512, N=4096)
+    from distributed_llm_inferencing_amd.ops import _native_call, _p, _st
+    M2 = 512
+    r2 = torch.randn(M2, D, device=dev).to(torch.bfloat16)
+    o2 = torch.empty_like(r2)
+    for spl in (2, 4, 8):
+        ws = torch.randn(spl * M2 * D, device=dev)
+        ms = ops.benchmark(lambda: _native_call("dli_splitk_add_rmsnorm", _p(o2), _p(r2), _p(ws),
+                                                spl, M2, D, _p(w), 1e-5, _st()), iters=50)
+        res[f"splitk{spl}_add_rmsnorm"] = (ms * 1e3, (spl * M2 * D * 4 + 3 * M2 * D * 2) / ms / 1e9)
     pos = ctx - 1
     slots = torch.arange(B, device=dev, dtype=torch.int32)
     cs = R.rope_cos_sin(2048, hd, 5e5, device=dev)

@@ -123,7 +123,7 @@ def test_fused_splitk_add_rmsnorm(gpu, M, N, K):
     r0, nw = rnd(M, N, dev=gpu), rnd(N, dev=gpu)
     y = R.linear(x, w)                                    # bf16-rounded GEMM output
     ref_out, ref_res = R.fused_add_rmsnorm(y, r0, nw, 1e-5)
-    for splits in (2, 4):
+    for splits in (2, 4, 8):                              # compile-time split variants
         G.set_plan(M, N, K, "splitk", G.GemmPlan("dli", 0, splits))
         res = r0.clone()
         out = ops.linear_add_rmsnorm(x, w, res, nw, 1e-5)
