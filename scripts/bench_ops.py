@@ -33,19 +33,19 @@ def main():
     kv_bytes = sum(lens) * hkv * hd * 2 * 2
     ms = ops.benchmark(lambda: ops.decode_attention(qkv, kc, vc, tables, ctx, 512, hq, hkv, hd,
                                                     1 / math.sqrt(hd)), iters=50)
-    res["decode_attention"] = (ms * 1e3, kv_bytes / ms / 1e9)
+    res["decode_attention"] = (ms * 1e3, kv_bytes / ms / 1e6)
     logits = torch.randn(B, V, device=dev) * 1.3
     t = torch.full((B,), 0.8, device=dev)
     k = torch.full((B,), 50, device=dev, dtype=torch.int32)
     p = torch.full((B,), 0.95, device=dev)
     s = torch.arange(B, device=dev, dtype=torch.int64)
     ms = ops.benchmark(lambda: ops.sample(logits, t, k, p, s), iters=30)
-    res["sample_topk_topp"] = (ms * 1e3, B * V * 4 / ms / 1e9)
+    res["sample_topk_topp"] = (ms * 1e3, B * V * 4 / ms / 1e6)
     x = torch.randn(B, D, device=dev).to(torch.bfloat16)
     r = torch.randn(B, D, device=dev).to(torch.bfloat16)
     w = torch.ones(D, device=dev, dtype=torch.bfloat16)
     ms = ops.benchmark(lambda: ops.add_rmsnorm(x, r, w, 1e-5), iters=50)
-    res["add_rmsnorm"] = (ms * 1e3, 4 * B * D * 2 / ms / 1e9)
+    res["add_rmsnorm"] = (ms * 1e3, 4 * B * D * 2 / ms / 1e6)
     # split-K reduce + residual add + RMSNorm alone, at the decode O/down shape (M=512, N=4096)
     from distributed_llm_inferencing_amd.ops import _native_call, _p, _st
     M2 = 512
@@ -55,13 +55,13 @@ def main():
         ws = torch.randn(spl * M2 * D, device=dev)
         ms = ops.benchmark(lambda: _native_call("dli_splitk_add_rmsnorm", _p(o2), _p(r2), _p(ws),
                                                 spl, M2, D, _p(w), 1e-5, _st()), iters=50)
-        res[f"splitk{spl}_add_rmsnorm"] = (ms * 1e3, (spl * M2 * D * 4 + 3 * M2 * D * 2) / ms / 1e9)
+        res[f"splitk{spl}_add_rmsnorm"] = (ms * 1e3, (spl * M2 * D * 4 + 3 * M2 * D * 2) / ms / 1e6)
     pos = ctx - 1
     slots = torch.arange(B, device=dev, dtype=torch.int32)
     cs = R.rope_cos_sin(2048, hd, 5e5, device=dev)
     ms = ops.benchmark(lambda: ops.rope_and_cache(qkv, pos, slots, cs, kc, vc, hq, hkv, hd),
                        iters=50)
-    res["rope_cache"] = (ms * 1e3, qkv.numel() * 2 * 2 / ms / 1e9)
+    res["rope_cache"] = (ms * 1e3, qkv.numel() * 2 * 2 / ms / 1e6)
     for kname, (us, gbs) in res.items():
         print(f"{kname:20s} {us:8.1f} us  {gbs:8.1f} GB/s")
 
