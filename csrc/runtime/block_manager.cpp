@@ -82,6 +82,27 @@ int dli_bm_ensure(void* h, long long seq, long long total_tokens) {
   return need;
 }
 
+// ensure() for (seqs[i], totals[i]) in order; stops at the first sequence that does not
+// fit. Returns how many succeeded.
+int dli_bm_ensure_batch(void* h, const long long* seqs, const int* totals, int n) {
+  auto* m = H(h);
+  std::lock_guard<std::mutex> g(m->mu);
+  for (int i = 0; i < n; ++i) {
+    auto& tab = m->tables[seqs[i]];
+    const int need = m->blocks_for(totals[i]) - (int)tab.size();
+    if (need <= 0) continue;
+    if ((int)m->free_list.size() < need) {
+      if (tab.empty()) m->tables.erase(seqs[i]);
+      return i;
+    }
+    for (int k = 0; k < need; ++k) {
+      tab.push_back(m->free_list.back());
+      m->free_list.pop_back();
+    }
+  }
+  return n;
+}
+
 // Release every block of `seq`. Returns the number released.
 int dli_bm_free(void* h, long long seq) {
   auto* m = H(h);
@@ -120,6 +141,43 @@ int dli_bm_fill_tables(void* h, const long long* seqs, int n, int* out, int max_
       if (cnt > max_blocks) return -1;
       std::memcpy(row, it->second.data(), sizeof(int) * cnt);
     }
+    std::fill(row + cnt, row + max_blocks, 0);
+    widest = std::max(widest, cnt);
+  }
+  return widest;
+}
+
+// One decode step's KV metadata in a single call (the per-tick hot path of the scheduler):
+// for each sequence i, grow its table to cover ctx[i] tokens (the new token is at position
+// ctx[i] - 1), write that token's slot to slots[i] and the padded table row to
+// tables[i * max_blocks ...]. Returns the widest table, or -(i + 1) if sequence i could not
+// get a block (earlier sequences keep theirs: they need them anyway), or -(n + 1) if a
+// table exceeds max_blocks.
+int dli_bm_decode_prepare(void* h, const long long* seqs, const int* ctx, int n, int* slots,
+                          int* tables, int max_blocks) {
+  auto* m = H(h);
+  std::lock_guard<std::mutex> g(m->mu);
+  const int bs = m->block_size;
+  int widest = 0;
+  for (int i = 0; i < n; ++i) {
+    auto& tab = m->tables[seqs[i]];
+    const int need = m->blocks_for(ctx[i]) - (int)tab.size();
+    if (need > 0) {
+      if ((int)m->free_list.size() < need) {
+        if (tab.empty()) m->tables.erase(seqs[i]);
+        return -(i + 1);
+      }
+      for (int k = 0; k < need; ++k) {
+        tab.push_back(m->free_list.back());
+        m->free_list.pop_back();
+      }
+    }
+    const int cnt = (int)tab.size();
+    if (cnt > max_blocks) return -(n + 1);
+    const int t = ctx[i] - 1;
+    slots[i] = tab[t / bs] * bs + (t % bs);
+    int* row = tables + (long)i * max_blocks;
+    std::memcpy(row, tab.data(), sizeof(int) * cnt);
     std::fill(row + cnt, row + max_blocks, 0);
     widest = std::max(widest, cnt);
   }

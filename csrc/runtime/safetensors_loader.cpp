@@ -260,4 +260,45 @@ long long dli_st_load_to_device(void* h, const int* idx, void* const* dsts, int 
   return total;
 }
 
+// Bytes [byte_off, byte_off + nbytes) of tensor i into dst (a row range of a row-major
+// tensor, e.g. one rank's vocabulary slice of the LM head): device = 1 streams through the
+// pinned ring with hipMemcpyAsync on `stream`, device = 0 is a host memcpy.
+long long dli_st_load_range(void* h, int i, long long byte_off, long long nbytes, void* dst,
+                            hipStream_t stream, int device) {
+  auto* f = H(h);
+  if (i < 0 || i >= (int)f->tensors.size()) return -2;
+  const auto& t = f->tensors[i];
+  if (byte_off < 0 || nbytes < 0 || byte_off + nbytes > t.end - t.begin) return -3;
+  const uint8_t* src = f->map + f->data_off + t.begin + byte_off;
+  if (!device) {
+    std::memcpy(dst, src, (size_t)nbytes);
+    return nbytes;
+  }
+  Staging s;
+  if (!s.ok) return -1;
+  size_t left = (size_t)nbytes, off = 0;
+  while (left > 0) {
+    const size_t piece = left < kPiece ? left : kPiece;
+    const int slot = s.next;
+    s.next = (s.next + 1) % kRing;
+    if (s.used[slot]) {
+      hipError_t e = hipEventSynchronize(s.ev[slot]);
+      if (e != hipSuccess) return -(long long)e;
+    }
+    std::memcpy(s.buf[slot], src + off, piece);
+    hipError_t e = hipMemcpyAsync((uint8_t*)dst + off, s.buf[slot], piece, hipMemcpyHostToDevice,
+                                  stream);
+    if (e != hipSuccess) return -(long long)e;
+    e = hipEventRecord(s.ev[slot], stream);
+    if (e != hipSuccess) return -(long long)e;
+    s.used[slot] = true;
+    off += piece;
+    left -= piece;
+  }
+  for (int k = 0; k < kRing; ++k)
+    if (s.used[k]) hipEventSynchronize(s.ev[k]);
+  for (int k = 0; k < kRing; ++k) s.used[k] = false;
+  return nbytes;
+}
+
 }  // extern "C"

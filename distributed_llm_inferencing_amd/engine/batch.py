@@ -38,6 +38,10 @@ class StepMeta:
     # lookahead (single stage, not on the wire): row of the in-flight step's device output
     # that holds this sequence's input id, -1 = input_ids holds it
     feed_src: Optional[np.ndarray] = None
+    # columns of block_tables that hold blocks (the scheduler knows it; pack trims to it)
+    table_used: Optional[int] = None
+    # seq_ids as int64 numpy (set by the decode scheduler; saves list -> array conversions)
+    seq_ids_arr: Optional[np.ndarray] = None
 
     @property
     def num_seqs(self) -> int:
@@ -56,20 +60,43 @@ class StepMeta:
             # trailing all-zero columns are dropped and restored by unpack (zeros either way:
             # padding or block 0): a 100-token decode needs 7 of the 32 columns, 2.5x less
             # control-plane payload
-            used = np.flatnonzero(np.asarray(tables).any(axis=0))
-            keep = int(used[-1]) + 1 if used.size else 1
+            if self.table_used is not None:
+                keep = int(self.table_used)
+            else:
+                used = np.flatnonzero(np.asarray(tables).any(axis=0))
+                keep = int(used[-1]) + 1 if used.size else 1
             if keep < tables.shape[1]:
-                tables = np.ascontiguousarray(tables[:, :keep])
+                tables = tables[:, :keep]
         mb = 0 if tables is None else int(tables.shape[1])
-        parts = [np.asarray(self.seq_ids, dtype=np.int32),
-                 _i32(self.input_ids, T), _i32(self.positions, T), _i32(self.slot_mapping, T),
-                 _i32(self.seq_lens, S), _i32(self.context_lens, S),
-                 _i32(tables, S * mb).reshape(-1),
-                 _f32_as_i32(self.temperature, S), _i32(self.top_k, S),
-                 _f32_as_i32(self.top_p, S),
-                 (np.zeros(S, np.int64) if self.seeds is None else
-                  self.seeds.astype(np.int64)).view(np.int32)]
-        payload = np.concatenate(parts).astype(np.int32)
+        n = S + 3 * T + 2 * S + S * mb + 3 * S + 2 * S
+        payload = np.empty(n, dtype=np.int32)
+        o = 0
+
+        def put(a, cnt, f32=False):
+            nonlocal o
+            if a is None:
+                payload[o:o + cnt] = 0
+            elif f32:
+                payload[o:o + cnt] = np.asarray(a, dtype=np.float32).reshape(-1).view(np.int32)
+            else:
+                payload[o:o + cnt].reshape(np.shape(a) if np.ndim(a) > 1 else -1)[...] = a
+            o += cnt
+        put(self.seq_ids_arr if self.seq_ids_arr is not None else
+            np.asarray(self.seq_ids, dtype=np.int64), S)
+        put(self.input_ids, T)
+        put(self.positions, T)
+        put(self.slot_mapping, T)
+        put(self.seq_lens, S)
+        put(self.context_lens, S)
+        put(tables, S * mb)
+        put(self.temperature, S, f32=True)
+        put(self.top_k, S)
+        put(self.top_p, S, f32=True)
+        if self.seeds is None:
+            payload[o:o + 2 * S] = 0
+        else:
+            payload[o:o + 2 * S] = np.asarray(self.seeds, dtype=np.int64).view(np.int32)
+        o += 2 * S
         header = np.zeros(HEADER_LEN, dtype=np.int64)
         header[:7] = [self.kind, S, T, mb, payload.shape[0], self.microbatch, self.step_id]
         header[7] = 1 if self.input_ids is not None else 0

@@ -77,10 +77,10 @@ def seq_to_output(seq: Sequence, tokenizer=None) -> RequestOutput:
                         output_ids=list(seq.output_ids), finish_reason=seq.finish_reason or "",
                         latency_s=end - seq.arrival,
                         ttft_s=(seq.first_token_time - seq.arrival) if seq.first_token_time else None)
-    if tokenizer is not None:
-        # HF semantics: generate() returns prompt + continuation; the reference decodes
-        # outputs[0] (prompt included) with skip_special_tokens=True (worker/app.py:308)
-        out.text = tokenizer.decode(out.all_ids, skip_special_tokens=True)
+    # HF semantics: generate() returns prompt + continuation; the reference decodes
+    # outputs[0] (prompt included) with skip_special_tokens=True (worker/app.py:308).
+    # Detokenised on first access of ``text``, off the engine's step loop.
+    out.tokenizer = tokenizer
     return out
 
 

@@ -42,6 +42,7 @@ class StageRunner:
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_out: Dict[int, torch.Tensor] = {}
         self._pool = None
+        self.hidden_in = None
         if self.use_graphs:
             self._init_static()
 
@@ -224,6 +225,14 @@ class StageRunner:
         torch.cuda.synchronize(self.device)
 
     # ------------------------------------------------------------------ execution
+    def input_buffer(self, meta: StepMeta) -> Optional[torch.Tensor]:
+        """Where a pipeline receive can put this step's hidden input so the graph reads it
+        in place: the static graph input for captured decode steps (None otherwise)."""
+        if (self.use_graphs and self.hidden_in is not None and meta.kind == DECODE
+                and meta.num_seqs <= self.max_batch):
+            return self.hidden_in[:meta.num_seqs]
+        return None
+
     @staticmethod
     def _feed(ids: torch.Tensor, src: torch.Tensor, feed: torch.Tensor) -> None:
         """Lookahead: ids[i] = feed[src[i]] where src[i] >= 0 (stream-ordered after the step
@@ -245,7 +254,7 @@ class StageRunner:
             self._upload(b)
             if meta.feed_src is not None:
                 self._feed(self._view("ids", S), self._view("src", S), feed)
-            if self.hidden_in is not None:
+            if self.hidden_in is not None and hidden.data_ptr() != self.hidden_in.data_ptr():
                 self.hidden_in[:S].copy_(hidden[:S])
             self.graphs[b].replay()
             return self.graph_out[b][:S]

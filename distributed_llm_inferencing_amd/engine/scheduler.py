@@ -18,6 +18,7 @@ later from prompt + generated tokens).
 """
 from __future__ import annotations
 
+import itertools
 import time
 import zlib
 from collections import deque
@@ -44,9 +45,15 @@ def row_seeds(seq_seeds: np.ndarray, index: np.ndarray) -> np.ndarray:
 
 
 class _MBState:
-    """numpy mirror of one microbatch's running sequences (decode fast path)."""
+    """numpy mirror of one microbatch's running sequences (decode fast path).
+
+    Tokens generated since the mirror was built are kept in ``hist`` (one column per step,
+    every row advances together on the fast path) and appended to the sequences'
+    ``output_ids`` only when a row leaves (finish / preemption) or the mirror is dropped
+    (``flush``): no per-token Python work per step. Finished rows are removed by
+    ``compact`` instead of rebuilding the mirror."""
     __slots__ = ("seqs", "sid", "ctx", "out_cnt", "budget", "last", "temp", "topk", "topp",
-                 "seed", "eos_ok", "stops", "first_pending")
+                 "seed", "eos_ok", "stops", "first_pending", "hist", "k")
 
     def __init__(self, seqs: List[Sequence], eos: Optional[int]):
         self.seqs = list(seqs)
@@ -65,6 +72,36 @@ class _MBState:
                                   bool, n)
         self.stops = [i for i, s in enumerate(seqs) if s.params.stop_token_ids]
         self.first_pending = bool((self.out_cnt == 0).any())
+        left = int((self.budget - self.out_cnt).max()) if n else 0
+        self.hist = np.zeros((n, max(1, min(left, 4096))), dtype=np.int32)
+        self.k = 0
+
+    def record(self, tokens: np.ndarray) -> None:
+        if self.k >= self.hist.shape[1]:
+            self.hist = np.concatenate([self.hist, np.zeros_like(self.hist)], axis=1)
+        self.hist[:, self.k] = tokens
+        self.k += 1
+
+    def flush_rows(self, idx) -> None:
+        """Append the pending tokens of rows ``idx`` to their sequences."""
+        if self.k == 0:
+            return
+        for i in idx:
+            self.seqs[i].output_ids.extend(self.hist[i, :self.k].tolist())
+
+    def flush(self) -> None:
+        self.flush_rows(range(len(self.seqs)))
+        self.hist[:, :self.k] = 0
+        self.k = 0
+
+    def compact(self, keep: np.ndarray) -> None:
+        """Drop rows where ``keep`` is False (their tokens must have been flushed)."""
+        for name in ("sid", "ctx", "out_cnt", "budget", "last", "temp", "topk", "topp", "seed",
+                     "eos_ok", "hist"):
+            setattr(self, name, getattr(self, name)[keep])
+        new_idx = np.cumsum(keep) - 1
+        self.stops = [int(new_idx[i]) for i in self.stops if keep[i]]
+        self.seqs = [s for s, kp in zip(self.seqs, keep.tolist()) if kp]
 
 
 class Scheduler:
@@ -128,6 +165,12 @@ class Scheduler:
         return sum(len(r) for r in self.running)
 
     # ------------------------------------------------------------------ internals
+    def _drop_state(self, mb: int) -> None:
+        st = self._state[mb]
+        if st is not None:
+            st.flush()
+            self._state[mb] = None
+
     def _finish(self, seq: Sequence, reason: str):
         if seq.state == SeqState.FINISHED:
             return
@@ -137,12 +180,15 @@ class Scheduler:
             except ValueError:
                 pass
         elif seq.state == SeqState.RUNNING:
+            self._drop_state(seq.microbatch)
             r = self.running[seq.microbatch]
             try:
                 r.remove(seq)
             except ValueError:
                 pass
-            self._state[seq.microbatch] = None
+        self._mark_finished(seq, reason)
+
+    def _mark_finished(self, seq: Sequence, reason: str):
         seq.state = SeqState.FINISHED
         seq.finish_reason = reason
         seq.finish_time = time.perf_counter()
@@ -164,9 +210,9 @@ class Scheduler:
         r = self.running[mb]
         if not r:
             return False
+        self._drop_state(mb)
         victim = max(r, key=lambda s: s.arrival)
         r.remove(victim)
-        self._state[mb] = None
         self.bm.free(victim.seq_id)
         victim.state = SeqState.WAITING
         victim.num_preemptions += 1
@@ -178,7 +224,8 @@ class Scheduler:
         temp = np.fromiter((s.params.effective_temperature() for s in seqs), np.float32, n)
         topk = np.fromiter((s.params.top_k for s in seqs), np.int32, n)
         topp = np.fromiter((s.params.top_p for s in seqs), np.float32, n)
-        seeds = np.fromiter((row_seed(s.seed, len(s.output_ids)) for s in seqs), np.int64, n)
+        seeds = row_seeds(np.fromiter((s.seed for s in seqs), np.int64, n),
+                          np.fromiter((len(s.output_ids) for s in seqs), np.int64, n))
         return temp, topk, topp, seeds
 
     # ------------------------------------------------------------------ scheduling
@@ -208,35 +255,49 @@ class Scheduler:
         if not self.waiting or (self.M > 1 and not self._least_loaded_ok(mb)):
             return None
         picked: List[Sequence] = []
+        lens_l: List[int] = []
         tokens = 0
         room = self.max_seqs - len(self.running[mb])
-        while self.waiting and len(picked) < room:
-            seq = self.waiting[0]
+        for seq in self.waiting:
+            if len(picked) >= room:
+                break
             n = seq.total_len
             if picked and tokens + n > self.max_prefill_tokens:
                 break
-            if not self.bm.ensure(seq.seq_id, n):
-                break
-            self.waiting.popleft()
             picked.append(seq)
+            lens_l.append(n)
             tokens += n
         if not picked:
             return None
+        # blocks for every picked prompt in one C++ call; stops at the first that does not fit
+        sid = np.fromiter((s.seq_id for s in picked), np.int64, len(picked))
+        lens = np.asarray(lens_l, dtype=np.int32)
+        got = self.bm.ensure_batch(sid, lens)
+        if got == 0:
+            return None
+        if got < len(picked):
+            picked, sid, lens = picked[:got], sid[:got], lens[:got]
+        for _ in range(got):
+            self.waiting.popleft()
+        self._drop_state(mb)
         for s in picked:
             s.state = SeqState.RUNNING
             s.microbatch = mb
             self.running[mb].append(s)
-        self._state[mb] = None
-        lens = np.array([s.total_len for s in picked], dtype=np.int32)
-        ids = np.concatenate([np.asarray(s.all_ids(), dtype=np.int32) for s in picked])
-        pos = np.concatenate([np.arange(n, dtype=np.int32) for n in lens])
-        sid = [s.seq_id for s in picked]
+        T = int(lens.sum())
+        ids = np.fromiter(itertools.chain.from_iterable(
+            (s.prompt_ids + s.output_ids) if s.output_ids else s.prompt_ids for s in picked),
+            np.int32, T)
+        starts = np.zeros(len(picked), np.int32)
+        starts[1:] = np.cumsum(lens)[:-1]
+        pos = (np.arange(T, dtype=np.int32) - np.repeat(starts, lens)).astype(np.int32)
         slots = self.bm.slot_mapping(sid, np.zeros(len(picked), np.int32), lens)
         temp, topk, topp, seeds = self._sampling_arrays(picked)
-        return StepMeta(kind=PREFILL, seq_ids=sid, input_ids=ids, positions=pos,
+        return StepMeta(kind=PREFILL, seq_ids=sid.tolist(), input_ids=ids, positions=pos,
                         slot_mapping=slots, seq_lens=lens, context_lens=lens.copy(),
                         block_tables=np.zeros((len(picked), 0), np.int32), temperature=temp,
-                        top_k=topk, top_p=topp, seeds=seeds, microbatch=mb, step_id=self._step)
+                        top_k=topk, top_p=topp, seeds=seeds, microbatch=mb, step_id=self._step,
+                        seq_ids_arr=sid)
 
     def _mb_state(self, mb: int) -> _MBState:
         st = self._state[mb]
@@ -276,20 +337,13 @@ class Scheduler:
             if idx.size == 0:
                 return None
             sid, ctx = st.sid[idx], ctx_all[idx]
-            # only sequences whose new token starts a fresh block need allocation
-            need = np.nonzero((ctx - 1) % self.bs == 0)[0]
-            ok = True
-            for i in need.tolist():
-                if not self.bm.ensure(int(sid[i]), int(ctx[i])):
-                    ok = False
-                    break
-            if ok:
+            # blocks for the new tokens + their slots + the padded tables: one C++ call
+            slots, tables, widest = self.bm.decode_prepare(sid, ctx, self.table_width)
+            if widest is not None:
                 break
             if not self._preempt(mb):
                 return None
         n = len(sid)
-        slots = self.bm.slot_mapping(sid, ctx - 1, np.ones(n, np.int32))
-        tables = self.bm.fill_tables(sid, self.table_width)
         seeds = row_seeds(st.seed[idx], out_all[idx])
         feed = src[idx]
         meta = StepMeta(kind=DECODE, seq_ids=sid.tolist(), input_ids=st.last[idx],
@@ -297,6 +351,8 @@ class Scheduler:
                         seq_lens=np.ones(n, np.int32), context_lens=ctx,
                         block_tables=tables, temperature=st.temp[idx], top_k=st.topk[idx],
                         top_p=st.topp[idx], seeds=seeds, microbatch=mb, step_id=self._step)
+        meta.table_used = max(1, widest)
+        meta.seq_ids_arr = sid
         if (feed >= 0).any():
             meta.feed_src = feed
         return meta
@@ -308,14 +364,15 @@ class Scheduler:
         mb = meta.microbatch
         st = self._state[mb] if meta.kind == DECODE else None
         if st is not None and len(st.seqs) == len(meta.seq_ids) and \
-                np.array_equal(st.sid, np.asarray(meta.seq_ids, dtype=np.int64)):
-            return self._update_fast(st, tokens)
+                np.array_equal(st.sid, meta.seq_ids_arr if meta.seq_ids_arr is not None
+                               else np.asarray(meta.seq_ids, dtype=np.int64)):
+            return self._update_fast(st, tokens, mb)
+        self._drop_state(mb)
         return self._update_slow(meta, tokens)
 
-    def _update_fast(self, st: _MBState, tokens: np.ndarray) -> List[Sequence]:
+    def _update_fast(self, st: _MBState, tokens: np.ndarray, mb: int) -> List[Sequence]:
         now = time.perf_counter()
-        for s, t in zip(st.seqs, tokens.tolist()):
-            s.output_ids.append(t)
+        st.record(tokens)
         if st.first_pending:
             for i in np.nonzero(st.out_cnt == 0)[0].tolist():
                 st.seqs[i].first_token_time = now
@@ -332,14 +389,23 @@ class Scheduler:
             if int(tokens[i]) in st.seqs[i].params.stop_token_ids:
                 fin_stop[i] = True
         fin_len = fin | (st.ctx >= self.max_model_len)
-        done_idx = np.nonzero(fin_len | fin_stop)[0]
+        done_mask = fin_len | fin_stop
+        done_idx = np.nonzero(done_mask)[0]
         done = []
         if done_idx.size:
+            idx = done_idx.tolist()
+            st.flush_rows(idx)
             seqs = st.seqs
-            for i in done_idx.tolist():
+            for i in idx:
                 s = seqs[i]
-                self._finish(s, "length" if fin_len[i] and not fin_stop[i] else "stop")
+                self._mark_finished(s, "length" if fin_len[i] and not fin_stop[i] else "stop")
                 done.append(s)
+            if done_idx.size == len(seqs):
+                self.running[mb] = []
+                self._state[mb] = None
+            else:
+                st.compact(~done_mask)
+                self.running[mb] = list(st.seqs)
         return done
 
     def _update_slow(self, meta: StepMeta, tokens: np.ndarray) -> List[Sequence]:
@@ -369,7 +435,7 @@ class Scheduler:
                 self._finish(seq, reason)
                 done.append(seq)
         for mb in touched:
-            self._state[mb] = None
+            self._drop_state(mb)
         return done
 
     def pop_finished(self) -> List[Sequence]:

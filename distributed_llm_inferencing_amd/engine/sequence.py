@@ -87,10 +87,18 @@ class RequestOutput:
     latency_s: float
     ttft_s: Optional[float]
     text: Optional[str] = None
+    tokenizer: object = field(default=None, repr=False, compare=False)
 
     @property
     def all_ids(self) -> List[int]:
         return self.prompt_ids + self.output_ids
+
+    def resolve_text(self) -> Optional[str]:
+        """prompt + continuation detokenised (skip_special_tokens), computed on first use
+        (off the engine's step loop)."""
+        if self.text is None and self.tokenizer is not None:
+            self.text = self.tokenizer.decode(self.all_ids, skip_special_tokens=True)
+        return self.text
 
 
 def row_seed(seq_seed: int, index: int) -> int:

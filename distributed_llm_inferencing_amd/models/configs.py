@@ -118,6 +118,9 @@ LLAMA_TINY = ModelConfig(
 LLAMA_TINY128 = replace(LLAMA_TINY, name="llama-tiny128", hidden_size=512, num_heads=4,
                         num_kv_heads=2, head_dim=128, intermediate_size=1024)
 
+# 8 layers: one per stage of an 8-rank pipeline test
+LLAMA_TINY8 = replace(LLAMA_TINY, name="llama-tiny8", num_layers=8)
+
 MIXTRAL_TINY = replace(LLAMA_TINY, name="mixtral-tiny", num_experts=4, top_k_experts=2,
                        intermediate_size=256)
 
@@ -127,7 +130,7 @@ GPT2_TINY = replace(GPT2, name="gpt2-tiny", hidden_size=256, num_layers=2, num_h
 
 _REGISTRY = {c.name: c for c in
              (GPT2, LLAMA3_8B, LLAMA3_70B, MIXTRAL_8X7B, LLAMA_TINY, LLAMA_TINY128,
-              MIXTRAL_TINY, GPT2_TINY)}
+              LLAMA_TINY8, MIXTRAL_TINY, GPT2_TINY)}
 
 _ALIASES = {
     "openai-community/gpt2": "gpt2",

@@ -1,21 +1,28 @@
 """Layer-sharded pipeline-parallel serving: one process per MI355X, stages over RCCL.
 
 This is what the reference's "sharded inference" was meant to be (offline
-layer split, ``metadata.json``, ``/load_shard``; execution never actually coordinated the
-shards) — made real:
+layer split ``shard_model.py:55-109``, ``metadata.json``, ``/load_shard`` at
+``worker/app.py:139-206``, dispatch to shard holders at ``master/dashboard/views.py:318-355``;
+execution never actually coordinated the shards) — made real:
 
-* stage r holds layers [start_r, end_r) (shard/planner.py), its own paged KV pool and its
-  own hipGraph-captured decode step;
-* rank 0 (the head) owns the scheduler, the C++ block allocator and the tokenizer; every
-  step's packed metadata rides with the activations through the ring, so the other stages
-  hold no scheduling state at all;
+* stage r holds layers [start_r, end_r) (shard/planner.py, or the ``shard_<r>/`` files the
+  ``shard-model`` CLI wrote, streamed into HBM by the C++ loader), its own paged KV pool
+  and its own hipGraph-captured decode step;
+* rank 0 (the head) owns the scheduler, the C++ block allocator and the tokenizer; each
+  tick's packed step metadata is published once on the shared-memory control ring
+  (``transport.py``), so the other stages hold no scheduling state at all;
 * M = N + 1 microbatches circulate: while microbatch m is in stage r, stage r-1 runs the
   next one, so all N GPUs are busy in steady state; the tail samples on device and returns
   int32 tokens to the head (C3), which schedules that microbatch's next step a tick after
   they arrived (the extra microbatch keeps the head's host off the critical path);
-* control plane (gloo, host) / data plane (RCCL, stream-ordered): see ``transport.py`` —
-  non-head ranks never synchronise their host with their GPU;
-* sessions: the head drives ticks while it has work, then broadcasts STOP; other ranks
+* every receive lands in a buffer allocated once per engine (decode hidden states straight
+  into the stage runner's static graph input); the tokens the head reads back travel
+  through a ring of M pinned host slots: no tensor is allocated by the transport per tick;
+* requests join a running session at tick boundaries (``run_session(admit=...)``), and
+  finished requests are handed back the tick they finish;
+* control plane (shared memory, host) / data plane (RCCL, stream-ordered): non-head ranks
+  never synchronise their host with their GPU;
+* sessions: the head drives ticks while it has work, then publishes STOP; other ranks
   block waiting for the next session; SHUTDOWN ends them.
 
 ``LocalPipeline`` runs the same partitioned stages and tick schedule in ONE process (all
@@ -24,9 +31,11 @@ GPU or CPU.
 """
 from __future__ import annotations
 
+import json
 import os
 import time
-from typing import Dict, List, Optional, Tuple
+from pathlib import Path
+from typing import Callable, Dict, List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -46,7 +55,7 @@ from ..runtime import BlockManager
 from ..shard.planner import StagePlan, plan_stages
 from ..tokenizer import load_tokenizer
 from ..utils import faults
-from .transport import H_TICK, PipeChannel, init_distributed
+from .transport import H_TICK, PipeChannel, ctrl_slot_bytes, init_distributed
 
 SHUTDOWN = 4
 
@@ -99,9 +108,11 @@ class StageWorker:
     def __init__(self, cfg: ModelConfig, plan: StagePlan, device, num_blocks: int,
                  block_size: int, max_batch: int, table_width: int, seed: int = 0,
                  use_graphs: Optional[bool] = None, params=None, dtype=torch.bfloat16,
-                 vocab_slice: Optional[Tuple[int, int]] = None):
+                 vocab_slice: Optional[Tuple[int, int]] = None, max_tokens: int = 0):
         self.cfg, self.plan = cfg, plan
         self.device = torch.device(device)
+        self.max_batch = max_batch
+        self.max_tokens = max(max_tokens, max_batch)
         if params is None:
             self.model = TransformerLM.random(cfg, plan.start_layer, plan.end_layer, self.device,
                                               dtype=dtype, seed=seed)
@@ -177,27 +188,41 @@ def _stage_capacity_blocks(cfg, plan, block_size, device, kv_fraction, cap_token
                            kv_fraction, cap_tokens=cap_tokens)
 
 
-class _Host:
-    """Tokens on their way to the head's host: a pinned copy + event (sampled on rank 0),
-    an exchange handle (received from the tail), or already a host array."""
+class _TokenRing:
+    """The head's view of each microbatch's sampled ids: M device slots (the tail's tokens
+    land here, or rank 0's own sampler output is parked here) mirrored into M pinned host
+    slots by an async D2H copy + event, enqueued right behind the producing step. Slot
+    = start tick % M: a microbatch's slot is refilled only after the host consumed it."""
 
-    def __init__(self, dev_tokens=None, handle=None, array=None):
-        self.handle, self.array = handle, array
-        if dev_tokens is not None and not dev_tokens.is_cuda:
-            self.array = dev_tokens.numpy()
-        elif dev_tokens is not None:
-            self.host = torch.empty(dev_tokens.shape, dtype=torch.int32, pin_memory=True)
-            self.host.copy_(dev_tokens, non_blocking=True)
-            self.ev = torch.cuda.Event()
-            self.ev.record()
+    def __init__(self, ch: PipeChannel, M: int, max_batch: int):
+        self.M = M
+        self.dev = ch.recv_buffer((M, max_batch), torch.int32)
+        self.cuda = self.dev.is_cuda
+        if self.cuda:
+            self.host = torch.empty((M, max_batch), dtype=torch.int32, pin_memory=True)
+            self.ev = [torch.cuda.Event() for _ in range(M)]
+        self.n = [0] * M
 
-    def get(self, ch) -> np.ndarray:
-        if self.array is not None:
-            return self.array
-        if self.handle is not None:
-            return ch.to_host(self.handle)
-        self.ev.synchronize()
-        return self.host.numpy()
+    def slot(self, start_tick: int, n: int) -> torch.Tensor:
+        return self.dev[start_tick % self.M, :n]
+
+    def landed(self, start_tick: int, n: int, src: Optional[torch.Tensor] = None) -> None:
+        """Tokens of microbatch ``start_tick`` are in (or, with ``src``, copied into) their
+        device slot: start the host copy."""
+        j = start_tick % self.M
+        if src is not None and src.data_ptr() != self.dev[j].data_ptr():
+            self.dev[j, :n].copy_(src[:n].to(self.dev.device), non_blocking=True)
+        self.n[j] = n
+        if self.cuda:
+            self.host[j, :n].copy_(self.dev[j, :n], non_blocking=True)
+            self.ev[j].record()
+
+    def get(self, start_tick: int) -> np.ndarray:
+        j = start_tick % self.M
+        if self.cuda:
+            self.ev[j].synchronize()
+            return self.host[j, :self.n[j]].numpy()
+        return self.dev[j, :self.n[j]].numpy()
 
 
 class PipelineHead:
@@ -205,8 +230,9 @@ class PipelineHead:
 
     Tick k (all ranks exchange once, anti-diagonal: rank r runs the layers of the microbatch
     the head started at tick k - r):
-      consume tokens of the microbatch started at k - M, schedule its next step, broadcast
-      the step's metadata (control plane), post exchange(k), then
+      consume tokens of the microbatch started at k - M, admit newly arrived requests,
+      schedule that microbatch's next step, publish the step's metadata (control plane),
+      post exchange(k), then
         vocab-parallel head: candidates of microbatch k - N from its final hidden (received
           from the tail); merge every rank's candidates of microbatch k - 1 - N and sample;
         tail head (fallback): tokens of microbatch k - N arrive from the tail;
@@ -221,6 +247,16 @@ class PipelineHead:
         self.M = microbatches or num_microbatches(self.N, self.vp)
         assert self.N == 1 or self.M >= self.N + (3 if self.vp else 1), "too few microbatches"
         self.stats = EngineStats()
+        self.host_s = 0.0          # head host time in ticks, excluding transport waits
+        self.ticks = 0
+        self.tick_log = [] if os.environ.get("DLI_PP_TICK_LOG", "0") == "1" else None
+        self.phase_s = {k: 0.0 for k in ("update", "finish", "schedule", "ctrl", "head_ops",
+                                         "compute")}
+        B, D = stage.max_batch, stage.cfg.hidden_size
+        self.tokens = _TokenRing(channel, self.M, B)
+        if self.vp and self.N > 1:
+            self.hf_rx = channel.recv_buffer((B, D))
+            self.cand_rx = channel.recv_buffer((self.N - 1, B, 2 * CAND), torch.int32)
 
     def _account(self, meta: StepMeta):
         self.stats.steps += 1
@@ -230,67 +266,7 @@ class PipelineHead:
         else:
             self.stats.decode_steps += 1
 
-    def run_session(self) -> List[RequestOutput]:
-        N, M, k, ch, st = self.N, self.M, 0, self.ch, self.stage
-        started: Dict[int, Tuple[StepMeta, bool]] = {}   # start tick -> (meta, vocab-parallel)
-        tokens: Dict[int, _Host] = {}
-        prev_out = None                # stage-0 output of tick k-1 (hidden -> rank 1)
-        my_cand = None                 # own candidates of microbatch k-1-N (vocab-parallel)
-        D = self.stage.cfg.hidden_size
-        while True:
-            t0 = time.perf_counter()
-            s = k - M
-            if s in started:
-                m, _ = started.pop(s)
-                self.sched.update(m, tokens.pop(s).get(ch))
-                self.stats.tokens_out += m.num_seqs
-            meta = self.sched.schedule(k % M) if self.sched.has_work() else None
-            if meta is None and not started and not self.sched.has_work():
-                break
-            if N == 1:
-                if meta is not None:
-                    out = st.compute(meta, None)
-                    started[k] = (meta, False)
-                    tokens[k] = _Host(array=out.cpu().numpy())
-                    self._account(meta)
-                k += 1
-                continue
-            vp_k = self.vp and vp_ok(meta)
-            h, p = _ctrl(EMPTY if meta is None else meta.kind, k, meta)
-            h[H_VP] = int(vp_k)
-            ch.broadcast_ctrl(h, p)
-            ret = started.get(k - N)             # its last stage ran at tick k - 1
-            smp = started.get(k - 1 - N)         # its candidates were made at tick k - 1
-            recvs = []
-            if ret is not None:
-                recvs.append(((ret[0].num_seqs, D), ch.dtype, N - 1, 2) if ret[1] else
-                             ((ret[0].num_seqs,), torch.int32, N - 1, 2))
-            if smp is not None and smp[1]:
-                recvs += [((smp[0].num_seqs, 2 * CAND), torch.int32, q, 3) for q in range(1, N)]
-            hd = ch.exchange_many([(prev_out, 1, 1)] if prev_out is not None else [], recvs)
-            ch.reap_ctrl()
-            cand_now = None
-            if ret is not None:
-                if ret[1]:
-                    hf = ch.wait_all(hd)[0]
-                    cand_now = st.candidates(hf)
-                else:
-                    tokens[k - N] = _Host(handle=(hd[0][0], hd[1]))
-            if smp is not None and smp[1]:
-                bufs = ch.wait_all(hd)
-                tok = st.sample_candidates(smp[0], [my_cand] + bufs[-(N - 1):])
-                tokens[k - 1 - N] = _Host(dev_tokens=tok)
-            my_cand = cand_now
-            prev_out = None
-            if meta is not None:
-                prev_out = st.compute(meta, None)
-                started[k] = (meta, vp_k)
-                self._account(meta)
-            self.stats.busy_s += time.perf_counter() - t0
-            k += 1
-        if N > 1:
-            ch.broadcast_ctrl(*_ctrl(STOP, k))
-            ch.flush()
+    def _finished(self) -> List[RequestOutput]:
         outs = []
         for seq in self.sched.pop_finished():
             o = seq_to_output(seq, self.tok)
@@ -299,13 +275,145 @@ class PipelineHead:
             outs.append(o)
         return outs
 
+    def run_session(self, admit: Optional[Callable[[], int]] = None,
+                    on_finished: Optional[Callable[[List[RequestOutput]], None]] = None
+                    ) -> List[RequestOutput]:
+        """Drive ticks until nothing is queued, running or in flight. ``admit`` is called
+        at every tick boundary to add newly arrived requests to the scheduler (continuous
+        admission); ``on_finished`` receives the requests that finished at that tick (else
+        everything is returned at the end)."""
+        N, M, k, ch, st = self.N, self.M, 0, self.ch, self.stage
+        started: Dict[int, Tuple[StepMeta, bool]] = {}   # start tick -> (meta, vocab-parallel)
+        prev_out = None                # stage-0 output of tick k-1 (hidden -> rank 1)
+        my_cand = None                 # own candidates of microbatch k-1-N (vocab-parallel)
+        collected: List[RequestOutput] = []
+        toks = self.tokens
+        ph = self.phase_s
+        pc = time.perf_counter
+        while True:
+            t0 = pc()
+            wait_s = 0.0
+            s = k - M
+            if s in started:
+                m, _ = started.pop(s)
+                arr = toks.get(s)
+                tw = pc()
+                wait_s += tw - t0
+                self.sched.update(m, arr)
+                self.stats.tokens_out += m.num_seqs
+                ph["update"] += pc() - tw
+            t1 = pc()
+            if admit is not None:
+                admit()
+            done = self._finished()
+            if done:
+                if on_finished is not None:
+                    on_finished(done)
+                else:
+                    collected += done
+            t2 = pc()
+            ph["finish"] += t2 - t1
+            meta = self.sched.schedule(k % M) if self.sched.has_work() else None
+            t3 = pc()
+            ph["schedule"] += t3 - t2
+            if meta is None and not started and not self.sched.has_work():
+                break
+            if N == 1:
+                if meta is not None:
+                    out = st.compute(meta, None)
+                    started[k] = (meta, False)
+                    toks.landed(k, meta.num_seqs, src=out)
+                    self._account(meta)
+                k += 1
+                continue
+            vp_k = self.vp and vp_ok(meta)
+            h, p = _ctrl(EMPTY if meta is None else meta.kind, k, meta)
+            h[H_VP] = int(vp_k)
+            ch.broadcast_ctrl(h, p)
+            t4 = pc()
+            ph["ctrl"] += t4 - t3
+            ret = started.get(k - N)             # its last stage ran at tick k - 1
+            smp = started.get(k - 1 - N)         # its candidates were made at tick k - 1
+            recvs = []
+            if ret is not None:
+                S = ret[0].num_seqs
+                recvs.append((self.hf_rx[:S], N - 1, 2) if ret[1] else
+                             (toks.slot(k - N, S), N - 1, 2))
+            if smp is not None and smp[1]:
+                S2 = smp[0].num_seqs
+                recvs += [(self.cand_rx[q - 1, :S2], q, 3) for q in range(1, N)]
+            tw = pc()
+            ch.exchange([(prev_out, 1, 1)] if prev_out is not None else [], recvs)
+            ch.reap_ctrl()
+            t5 = pc()
+            wait_s += t5 - tw
+            cand_now = None
+            if ret is not None:
+                if ret[1]:
+                    cand_now = st.candidates(ch.to_compute(self.hf_rx[:ret[0].num_seqs]))
+                else:
+                    toks.landed(k - N, ret[0].num_seqs)
+            if smp is not None and smp[1]:
+                S2 = smp[0].num_seqs
+                bufs = [ch.to_compute(self.cand_rx[q, :S2]) for q in range(N - 1)]
+                tok = st.sample_candidates(smp[0], [my_cand] + bufs)
+                toks.landed(k - 1 - N, S2, src=tok)
+            my_cand = cand_now
+            prev_out = None
+            t6 = pc()
+            ph["head_ops"] += t6 - t5
+            if meta is not None:
+                prev_out = st.compute(meta, None)
+                started[k] = (meta, vp_k)
+                self._account(meta)
+            now = pc()
+            ph["compute"] += now - t6
+            if self.tick_log is not None:
+                self.tick_log.append((meta.kind if meta is not None else 0, t1 - t0 - wait_s,
+                                      t2 - t1, t3 - t2, t4 - t3, t6 - t5, now - t6))
+            self.host_s += now - t0 - wait_s
+            self.ticks += 1
+            self.stats.busy_s += now - t0
+            k += 1
+        if N > 1:
+            ch.broadcast_ctrl(*_ctrl(STOP, k))
+            ch.flush()
+        done = self._finished()
+        if on_finished is not None and done:
+            on_finished(done)
+        return collected + done
+
     def shutdown(self):
         if self.N > 1:
             self.ch.broadcast_ctrl(*_ctrl(SHUTDOWN, -1))
             self.ch.flush()
 
 
-def serve_session(stage: StageWorker, channel) -> int:
+class _StageBuffers:
+    """Receive buffers of a non-head stage, allocated once: hidden rows from the previous
+    stage (prefill-sized; decode steps land in the runner's static graph input instead) and,
+    with the vocab-parallel head, the tail's final hidden state."""
+
+    def __init__(self, stage: StageWorker, ch: PipeChannel):
+        D = stage.cfg.hidden_size
+        self.rx = ch.recv_buffer((stage.max_tokens, D))
+        self.hf = (ch.recv_buffer((stage.max_batch, D))
+                   if stage.vocab_parallel and not stage.is_last else None)
+        self.direct = ch.nccl or stage.device.type == "cpu"
+
+    def hidden_target(self, stage: StageWorker, meta: StepMeta) -> torch.Tensor:
+        if self.direct:
+            b = stage.runner.input_buffer(meta)
+            if b is not None:
+                return b
+        T = meta.num_tokens
+        if T > self.rx.shape[0]:
+            raise ValueError(f"step of {T} tokens exceeds the stage receive buffer "
+                             f"({self.rx.shape[0]}); raise max_prefill_tokens")
+        return self.rx[:T]
+
+
+def serve_session(stage: StageWorker, channel, bufs: Optional[_StageBuffers] = None) -> int:
     """Non-head rank r: every tick of one head session; returns STOP or SHUTDOWN.
     Tick k: layers of the microbatch started at k - r (control message k - r, received in
     order), with the vocab-parallel head also the candidates of microbatch k - N; the tail
@@ -313,7 +421,7 @@ def serve_session(stage: StageWorker, channel) -> int:
     host never waits on this GPU: receives, replays and sends are all stream-ordered."""
     r, N, k = channel.rank, channel.world, 0
     tail = r == N - 1
-    D = stage.cfg.hidden_size
+    bufs = bufs or _StageBuffers(stage, channel)
     metas: Dict[int, Tuple[StepMeta, bool]] = {}
     prev_out = None                 # my layer output of tick k-1 (hidden / tokens / final hidden)
     prev_vp = False
@@ -343,22 +451,24 @@ def serve_session(stage: StageWorker, channel) -> int:
                 sends.append((prev_out, 0, 2))
         if smp is not None and smp[1] and my_cand is not None:
             sends.append((my_cand, 0, 3))
+        x = None
         if meta is not None:
-            recvs.append(((meta.num_tokens, D), channel.dtype, r - 1, 1))
+            x = bufs.hidden_target(stage, meta)
+            recvs.append((x, r - 1, 1))
+        hf = None
         if ret is not None and ret[1] and not tail:
-            recvs.append(((ret[0].num_seqs, D), channel.dtype, N - 1, 2))
-        hd = channel.exchange_many(sends, recvs)
-        bufs = channel.wait_all(hd) if recvs else []
+            hf = bufs.hf[:ret[0].num_seqs]
+            recvs.append((hf, N - 1, 2))
+        channel.exchange(sends, recvs)
         # candidates first: on the tail they read the final hidden of tick k-1 (prev_out),
         # which this tick's replay overwrites
         cand_now = None
         if ret is not None and ret[1]:
-            hf = prev_out if tail else bufs[-1]
-            cand_now = stage.candidates(hf)
+            cand_now = stage.candidates(prev_out if tail else channel.to_compute(hf))
         my_cand = cand_now
         prev_out, prev_vp = None, False
         if meta is not None:
-            out = stage.compute(meta, bufs[0])
+            out = stage.compute(meta, channel.to_compute(x))
             vp_m = metas[k - r][1]
             if tail and not vp_m and stage.vocab_parallel:
                 out = stage.tokens_full(meta, out)        # a row needs the whole vocabulary
@@ -370,8 +480,49 @@ def serve_session(stage: StageWorker, channel) -> int:
 
 def run_stage_loop(stage: StageWorker, channel) -> None:
     """Non-head ranks: serve sessions until SHUTDOWN."""
-    while serve_session(stage, channel) != SHUTDOWN:
+    bufs = _StageBuffers(stage, channel)
+    while serve_session(stage, channel, bufs) != SHUTDOWN:
         pass
+
+
+# ------------------------------------------------------------------------------ shard files
+def read_shard_dir(shard_dir: str, rank: int, world: int) -> Tuple[ModelConfig, dict, Path]:
+    """(config, metadata, path) of ``<shard_dir>/shard_<rank>`` as written by ``shard-model``
+    (reference layout); the files' partition must have ``world``
+    stages."""
+    d = Path(shard_dir) / f"shard_{rank}"
+    meta = json.loads((d / "metadata.json").read_text())
+    if int(meta.get("num_shards", 1)) != world:
+        raise ValueError(f"{shard_dir} holds {meta.get('num_shards')} shards; the pipeline "
+                         f"has {world} ranks")
+    if int(meta.get("shard_id", rank)) != rank:
+        raise ValueError(f"{d}: metadata.json says shard {meta.get('shard_id')}")
+    cfg = ModelConfig.from_dict(json.loads((d / "config.json").read_text()))
+    return cfg, meta, d
+
+
+def load_stage_params(shard_dir: str, rank: int, world: int, device,
+                      vocab_slice: Optional[Tuple[int, int]] = None) -> Dict[str, torch.Tensor]:
+    """This rank's tensors straight from its shard file into HBM (C++ loader: mmap ->
+    pinned ring -> hipMemcpyAsync). With the vocab-parallel head the rank also reads its
+    row slice of the LM head from the last shard's file (a contiguous byte range)."""
+    from ..runtime import SafetensorsFile
+    _cfg, _meta, d = read_shard_dir(shard_dir, rank, world)
+    f = SafetensorsFile(str(d / "model.safetensors"))
+    try:
+        params = f.load(device=device)
+    finally:
+        f.close()
+    if vocab_slice is not None:
+        tail = Path(shard_dir) / f"shard_{world - 1}" / "model.safetensors"
+        ft = SafetensorsFile(str(tail))
+        try:
+            params["head_slice"] = ft.load_rows("lm_head", *vocab_slice, device=device)
+        finally:
+            ft.close()
+    if torch.device(device).type == "cuda":
+        torch.cuda.synchronize(device)
+    return params
 
 
 # ------------------------------------------------------------------------------ builders
@@ -379,43 +530,64 @@ def build_stage(cfg: ModelConfig, rank: int, world: int, device, max_batch: int,
                 max_model_len: int, block_size: int = 16, kv_fraction: float = 0.85,
                 policy: str = "balanced", seed: int = 0, use_graphs=None,
                 num_blocks: Optional[int] = None, dtype=torch.bfloat16,
-                vocab_parallel: bool = False, microbatches: Optional[int] = None):
-    plans = plan_stages(cfg, world, policy, head_on_all=vocab_parallel)
+                vocab_parallel: bool = False, microbatches: Optional[int] = None,
+                max_tokens: int = 0, shard_dir: Optional[str] = None):
+    if shard_dir is not None:
+        from ..shard.writer import stage_plan_from_metadata
+        plans = [stage_plan_from_metadata(read_shard_dir(shard_dir, i, world)[1])
+                 for i in range(world)]
+    else:
+        plans = plan_stages(cfg, world, policy, head_on_all=vocab_parallel)
     plan = plans[rank]
     table_width = -(-max_model_len // block_size)
     M = microbatches or num_microbatches(world, vocab_parallel)
+    vs = vocab_slices(cfg.vocab_size, world)[rank] if vocab_parallel else None
+    params = (load_stage_params(shard_dir, rank, world, device, vs)
+              if shard_dir is not None else None)
     if num_blocks is None:
+        # every sequence of the M microbatches in flight may reach max_model_len: size the
+        # pool for that (not a fraction of HBM: 288 GB would otherwise all go to KV)
         cap = _stage_capacity_blocks(cfg, plan, block_size, device, kv_fraction,
                                      cap_tokens=max(M * max_batch * max_model_len, 1 << 16))
         t = torch.tensor([cap], dtype=torch.int64,
                          device=device if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MIN)     # block ids are global: same pool size
         num_blocks = int(t.item())
-    vs = vocab_slices(cfg.vocab_size, world)[rank] if vocab_parallel else None
     stage = StageWorker(cfg, plan, device, num_blocks, block_size, max_batch, table_width,
-                        seed=seed, use_graphs=use_graphs, dtype=dtype, vocab_slice=vs)
+                        seed=seed, use_graphs=use_graphs, dtype=dtype, vocab_slice=vs,
+                        max_tokens=max_tokens, params=params)
     return stage, plans, num_blocks, table_width
 
 
 class DistributedPipelineEngine:
-    """User-facing engine on rank 0 of an N-rank pipeline (ranks > 0 call ``serve()``)."""
+    """User-facing engine on rank 0 of an N-rank pipeline (ranks > 0 call ``serve()``).
+    ``shard_dir``: serve the weights the ``shard-model`` CLI exported (one
+    ``shard_<rank>/`` per rank) instead of a random init."""
 
     def __init__(self, model: str, device, max_batch: int = 256, max_model_len: int = 2048,
                  block_size: int = 16, policy: str = "balanced", seed: int = 0,
                  use_graphs=None, max_prefill_tokens: int = 16384, num_blocks=None,
-                 dtype=torch.bfloat16, vocab_parallel: Optional[bool] = None):
+                 dtype=torch.bfloat16, vocab_parallel: Optional[bool] = None,
+                 shard_dir: Optional[str] = None):
         self.rank, self.world = init_distributed(device=torch.device(device)
                                                  if torch.device(device).type == "cuda" else None)
-        self.cfg = get_config(model)
+        if shard_dir is not None:
+            self.cfg = read_shard_dir(shard_dir, self.rank, self.world)[0]
+        else:
+            self.cfg = get_config(model)
         self.device = torch.device(device)
         self.vocab_parallel = (use_vocab_parallel(self.cfg, self.world)
                                if vocab_parallel is None else vocab_parallel)
         self.microbatches = num_microbatches(self.world, self.vocab_parallel)
+        max_model_len = min(max_model_len, self.cfg.max_position)
+        max_tokens = max(max_prefill_tokens, max_model_len, max_batch)
         self.stage, self.plans, nb, tw = build_stage(
             self.cfg, self.rank, self.world, self.device, max_batch, max_model_len, block_size,
             policy=policy, seed=seed, use_graphs=use_graphs, num_blocks=num_blocks, dtype=dtype,
-            vocab_parallel=self.vocab_parallel, microbatches=self.microbatches)
-        self.channel = PipeChannel(self.device, dtype=dtype)
+            vocab_parallel=self.vocab_parallel, microbatches=self.microbatches,
+            max_tokens=max_tokens, shard_dir=shard_dir)
+        self.channel = PipeChannel(self.device, dtype=dtype,
+                                   ctrl_bytes=ctrl_slot_bytes(max_batch, max_tokens, tw))
         self.head = None
         if self.rank == 0:
             bm = BlockManager(nb, block_size)
@@ -423,8 +595,11 @@ class DistributedPipelineEngine:
                               num_microbatches=self.microbatches,
                               eos_token_id=self.cfg.eos_token_id,
                               max_model_len=max_model_len, table_width=tw)
-            self.head = PipelineHead(self.stage, self.channel, sched, load_tokenizer(self.cfg),
-                                     self.microbatches)
+            tok_path = None
+            if shard_dir is not None and (Path(shard_dir) / "tokenizer").exists():
+                tok_path = str(Path(shard_dir) / "tokenizer")
+            self.head = PipelineHead(self.stage, self.channel, sched,
+                                     load_tokenizer(self.cfg, tok_path), self.microbatches)
         self._ids = 0
 
     def warmup(self):
@@ -455,20 +630,24 @@ class DistributedPipelineEngine:
 # ------------------------------------------------------------------------------ loopback
 class LocalPipeline:
     """All N stages in one process (loopback transport): same partitioning, metadata
-    serialisation and microbatch schedule as the distributed ring, executed sequentially."""
+    serialisation and microbatch schedule as the distributed ring, executed sequentially.
+    ``step()`` advances one tick, so a service can admit requests between ticks."""
 
     def __init__(self, model, num_stages: int, device="cpu", max_batch: int = 64,
                  max_model_len: int = 512, block_size: int = 16, num_blocks: int = 256,
                  policy: str = "even", seed: int = 0, use_graphs=None, params=None,
-                 dtype=torch.bfloat16, plans: Optional[List[StagePlan]] = None):
+                 dtype=torch.bfloat16, plans: Optional[List[StagePlan]] = None,
+                 stage_params: Optional[List[Dict[str, torch.Tensor]]] = None, tokenizer=None):
         self.cfg = get_config(model) if isinstance(model, str) else model
         self.N = num_stages
         self.plans = plans or plan_stages(self.cfg, num_stages, policy)
         tw = -(-max_model_len // block_size)
         self.stages = []
-        for p in self.plans:
+        for i, p in enumerate(self.plans):
             sp = None
-            if params is not None:
+            if stage_params is not None:
+                sp = stage_params[i]
+            elif params is not None:
                 sp = {k: v for k, v in params.items() if _param_in_stage(k, p, self.cfg)}
             self.stages.append(StageWorker(self.cfg, p, device, num_blocks, block_size,
                                            max_batch, tw, seed, use_graphs, params=sp,
@@ -476,37 +655,66 @@ class LocalPipeline:
         self.sched = Scheduler(BlockManager(num_blocks, block_size), max_seqs_per_mb=max_batch,
                                num_microbatches=num_stages, eos_token_id=self.cfg.eos_token_id,
                                max_model_len=max_model_len, table_width=tw)
-        self.tok = load_tokenizer(self.cfg)
+        self.tok = tokenizer or load_tokenizer(self.cfg)
+        self.stats = EngineStats()
         self._ids = 0
+        self._k = 0
+        self._inflight: Dict[int, tuple] = {}
+
+    def add_request(self, prompt, params=None, request_id=None) -> str:
+        rid = request_id or f"req-{self._ids}"
+        self._ids += 1
+        ids = self.tok.encode(prompt) if isinstance(prompt, str) else list(prompt)
+        self.sched.add_request(rid, ids, params)
+        return rid
+
+    def has_work(self) -> bool:
+        return self.sched.has_work() or bool(self._inflight)
+
+    def step(self) -> List[RequestOutput]:
+        """One tick: apply the tokens of the microbatch started N ticks ago, schedule the
+        next step of this tick's microbatch and run it through every stage."""
+        k, N = self._k, self.N
+        t0 = time.perf_counter()
+        j = k - N
+        if j in self._inflight:
+            m, toks = self._inflight.pop(j)
+            self.sched.update(m, toks)
+            self.stats.tokens_out += m.num_seqs
+        meta = self.sched.schedule(k % N) if self.sched.has_work() else None
+        if meta is not None:
+            data = None
+            for s in self.stages:
+                # round-trip the wire format exactly as the ring does
+                h, pl = meta.pack()
+                m2 = StepMeta.unpack(h, pl)
+                if not s.model.is_first:
+                    m2.input_ids = None
+                data = s.compute(m2, data)
+            self._inflight[k] = (meta, data.cpu().numpy())
+            self.stats.steps += 1
+            if meta.kind == PREFILL:
+                self.stats.prefill_steps += 1
+            else:
+                self.stats.decode_steps += 1
+            self.stats.busy_s += time.perf_counter() - t0
+        self._k += 1
+        outs = []
+        for s in self.sched.pop_finished():
+            o = seq_to_output(s, self.tok)
+            self.stats.finished += 1
+            self.stats.latencies.append(o.latency_s)
+            outs.append(o)
+        return outs
 
     def generate(self, prompts, params=None) -> List[RequestOutput]:
-        rids = []
-        for p in prompts:
-            rid = f"req-{self._ids}"
-            self._ids += 1
-            ids = self.tok.encode(p) if isinstance(p, str) else list(p)
-            self.sched.add_request(rid, ids, params)
-            rids.append(rid)
-        k = 0
-        inflight: Dict[int, tuple] = {}
-        while self.sched.has_work() or inflight:
-            j = k - self.N
-            if j in inflight:
-                m, toks = inflight.pop(j)
-                self.sched.update(m, toks)
-            meta = self.sched.schedule(k % self.N) if self.sched.has_work() else None
-            if meta is not None:
-                data = None
-                for s in self.stages:
-                    # round-trip the wire format exactly as the ring does
-                    h, pl = meta.pack()
-                    m2 = StepMeta.unpack(h, pl)
-                    if not s.model.is_first:
-                        m2.input_ids = None
-                    data = s.compute(m2, data)
-                inflight[k] = (meta, data.cpu().numpy())
-            k += 1
-        outs = {s.request_id: seq_to_output(s, self.tok) for s in self.sched.pop_finished()}
+        rids = [self.add_request(p, params) for p in prompts]
+        outs: Dict[str, RequestOutput] = {}
+        while self.has_work():
+            for o in self.step():
+                outs[o.request_id] = o
+        for o in self.step():
+            outs[o.request_id] = o
         return [outs[r] for r in rids]
 
 
@@ -532,19 +740,21 @@ def bench_pipeline(args, world: int, rank: int, make_prompts):
         device = torch.device("cpu")
     eng = DistributedPipelineEngine(args.model, device, max_batch=args.batch,
                                     max_model_len=args.max_model_len,
-                                    max_prefill_tokens=max(args.batch * args.prompt_len, 8192))
+                                    max_prefill_tokens=max(args.batch * args.prompt_len, 8192),
+                                    shard_dir=getattr(args, "shard_dir", None))
     world = eng.world
     eng.warmup()
     sp = SamplingParams(max_length=args.max_length, temperature=0.8, top_k=50, top_p=0.95,
                         ignore_eos=True)
-    per_wave = args.batch * eng.microbatches       # M = N + 1 microbatches of --batch requests
+    per_wave = args.batch * eng.microbatches       # M microbatches of --batch requests
+    bufs = None if rank == 0 else _StageBuffers(eng.stage, eng.channel)
 
     def wave(seed):
         if rank == 0:
             outs = eng.generate(make_prompts(per_wave, args.prompt_len, eng.cfg.vocab_size, seed),
                                 sp)
             return sum(len(o.output_ids) for o in outs), [o.latency_s for o in outs]
-        run_one_session(eng)
+        serve_session(eng.stage, eng.channel, bufs)
         return 0, []
 
     for w in range(args.warmup):
@@ -554,6 +764,8 @@ def bench_pipeline(args, world: int, rank: int, make_prompts):
         torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     toks, lats = 0, []
+    if rank == 0:
+        eng.head.host_s, eng.head.ticks = 0.0, 0
     for s in range(args.steps):
         n, l = wave(s)
         toks += n
@@ -566,12 +778,15 @@ def bench_pipeline(args, world: int, rank: int, make_prompts):
     dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     eng.shutdown() if rank == 0 else eng.serve()
     dist.barrier()
+    eng.channel.close()
     dist.destroy_process_group()
     if rank != 0:
         return None
+    snap = eng.head.stats.snapshot()
+    snap["head_host_ms_per_tick"] = round(1e3 * eng.head.host_s / max(1, eng.head.ticks), 4)
+    snap["control_plane"] = eng.channel.ctrl_kind
     return {"tokens": toks, "seconds": float(dt.item()), "latencies": lats,
-            "global_batch": per_wave, "parallelism": f"pp{world}",
-            "engine": eng.head.stats.snapshot()}
+            "global_batch": per_wave, "parallelism": f"pp{world}", "engine": snap}
 
 
 def run_one_session(eng: DistributedPipelineEngine):

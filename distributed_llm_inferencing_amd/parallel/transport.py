@@ -3,26 +3,35 @@
 The reference has NO inter-shard data plane (its "sharded" path runs shard 0 alone,
 ``worker/app.py:334-336``). Here a pipeline step moves over two planes:
 
-* control plane (host): the head's packed ``StepMeta`` for every tick goes to every other
-  stage over a separate **gloo** process group (TCP loopback, CPU tensors) the moment the
-  head schedules it, so a stage's host can stage the metadata upload and enqueue its graph
-  replay long before the activations arrive — no stage ever waits on its GPU to learn what
-  to do next;
+* control plane (host): the head's packed ``StepMeta`` for every tick is written ONCE into a
+  shared-memory broadcast ring (``csrc/runtime/shm_ring.cpp``, all stages of a pipeline
+  live on one 8-GPU node) the moment the head schedules it; every stage reads it from the
+  same pages, so a stage's host stages the metadata upload and enqueues its graph replay
+  long before the activations arrive — no stage ever waits on its GPU to learn what to do
+  next, and the head's cost per tick is one memcpy + one release store whatever N is.
+  (Carrying the metadata inside the activation message instead would make every stage's
+  host wait for its receive to land before it could even launch: a host<->GPU round trip
+  per hop per tick.) A gloo fallback (``DLI_PP_CTRL=gloo``) serves ranks on different
+  hosts;
 * data plane (device): hidden states stage r -> r+1 and sampled token ids tail -> head go by
   RCCL point-to-point over xGMI (``torch.distributed`` backend "nccl" == RCCL on ROCm), one
   grouped send/recv per rank per tick, ordered on the GPU streams: the receive is a stream
-  dependency of the consumer's graph replay, never a host wait. On CPU (tests) the data
-  plane is gloo as well.
+  dependency of the consumer's graph replay, never a host wait. Receives land in buffers
+  allocated once per engine (a decode step's hidden state goes straight into the stage
+  runner's static graph input); sends read the producer's output in place (the next replay
+  that would overwrite it is stream-ordered behind the send). On CPU (tests) the data plane
+  is gloo as well.
 
 Every stage learns the activation shape of tick k from tick k's metadata (rows = tokens of
 the step, cols = hidden size), so the data plane carries no headers at all.
 """
 from __future__ import annotations
 
+import itertools
 import os
-from collections import deque
+import socket
 from datetime import timedelta
-from typing import Optional, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -32,8 +41,19 @@ from ..engine.batch import HEADER_LEN
 from ..utils import faults
 from ..utils.tracing import trace_range
 
-# header word indices (int64 units) beyond StepMeta's own first 8
+# header word indices (int64 units) beyond StepMeta's own first 9
 H_TICK = 12
+_HDR_BYTES = HEADER_LEN * 8
+_ring_ids = itertools.count()
+
+
+def ctrl_slot_bytes(max_seqs: int, max_tokens: int, table_width: int) -> int:
+    """Upper bound of one packed StepMeta message (header + int32 payload, see
+    ``StepMeta.pack``): seq ids, 3 per-token arrays, 2 per-seq lengths, the block table,
+    3 sampling words and a 2-word seed per sequence."""
+    S, T = int(max_seqs), int(max(max_tokens, max_seqs))
+    words = S + 3 * T + 2 * S + S * int(table_width) + 3 * S + 2 * S
+    return _HDR_BYTES + 4 * words + 64
 
 
 class PipeChannel:
@@ -48,7 +68,8 @@ class PipeChannel:
     streams that HIP may alias onto the same hardware queue (GPU_MAX_HW_QUEUES=4), putting
     a spinning receive in front of a send."""
 
-    def __init__(self, device: torch.device, dtype=torch.bfloat16, max_pending: int = 8):
+    def __init__(self, device: torch.device, dtype=torch.bfloat16,
+                 ctrl_bytes: int = 1 << 20, ctrl: Optional[str] = None):
         self.rank = dist.get_rank()
         self.world = dist.get_world_size()
         self.device = torch.device(device)
@@ -58,12 +79,16 @@ class PipeChannel:
         # the control plane between sessions: no timeout that could fire while idle.
         self.ctrl_group = dist.new_group(backend="gloo", timeout=timedelta(days=365))
         self.data_device = self.device if self.nccl else torch.device("cpu")
-        self._inflight = deque()
-        self._ctrl_sends = deque()
-        self.max_pending = max_pending
-        self.side_stream = (torch.cuda.Stream(self.device)
-                            if self.nccl and self.device.type == "cuda" else None)
+        self._ctrl_sends: List = []
+        self.ring = None
+        self.ctrl_kind = "none"
+        self.ctrl_bytes = int(ctrl_bytes)
+        self._msg = np.zeros(self.ctrl_bytes, dtype=np.uint8)       # head's staging buffer
+        self._hdr_rx = torch.empty(HEADER_LEN, dtype=torch.int64)    # gloo fallback
+        self._pay_rx = torch.empty(self.ctrl_bytes // 4, dtype=torch.int32)
+        self.exchanges = 0
         if self.world > 1:
+            self._init_ctrl(ctrl or os.environ.get("DLI_PP_CTRL", "auto"))
             # every rank joins one grouped ring exchange up front, so whatever point-to-point
             # communicator state RCCL builds lazily is built with all ranks present (the
             # session's first exchanges involve only some ranks)
@@ -75,6 +100,33 @@ class PipeChannel:
             if int(r.item()) != self.prev:
                 raise RuntimeError(f"pipeline ring check failed on rank {self.rank}")
 
+    # ------------------------------------------------------------------ setup
+    def _init_ctrl(self, mode: str) -> None:
+        hosts = [None] * self.world
+        dist.all_gather_object(hosts, socket.gethostname(), group=self.ctrl_group)
+        use_shm = mode == "shm" or (mode == "auto" and len(set(hosts)) == 1)
+        name = None
+        if use_shm and self.rank == 0:
+            from ..runtime import ShmRing
+            name = (f"/dli_pp_{os.environ.get('MASTER_PORT', '0')}_{os.getpid()}_"
+                    f"{next(_ring_ids)}")
+            try:
+                # 4N + 16 slots: the head runs at most ~N + 3 ticks ahead of the tail
+                self.ring = ShmRing.create(name, 4 * self.world + 16, self.ctrl_bytes,
+                                           self.world - 1)
+            except OSError:
+                name = None
+        box = [name if self.rank == 0 else None]
+        dist.broadcast_object_list(box, src=0, group=self.ctrl_group)
+        name = box[0]
+        if name is not None and self.rank > 0:
+            from ..runtime import ShmRing
+            self.ring = ShmRing.open(name, self.rank - 1)
+        dist.barrier(group=self.ctrl_group)
+        if name is not None and self.rank == 0:
+            self.ring.unlink()           # mapped by every rank now: nothing left in /dev/shm
+        self.ctrl_kind = "shm" if name is not None else "gloo"
+
     @property
     def next(self) -> int:
         return (self.rank + 1) % self.world
@@ -85,124 +137,114 @@ class PipeChannel:
 
     # ------------------------------------------------------------------ control plane
     def broadcast_ctrl(self, header: np.ndarray, payload: np.ndarray) -> None:
-        """Head -> every other stage (asynchronous; buffers kept until delivered)."""
+        """Head -> every other stage; never waits for a consumer unless the ring is full."""
         if faults.active():
             faults.check("transport.exchange", tick=int(header[H_TICK]))
-        h = torch.from_numpy(np.ascontiguousarray(header, dtype=np.int64).copy())
-        h[4] = int(payload.shape[0])
-        p = torch.from_numpy(np.ascontiguousarray(payload, dtype=np.int32).copy())
+        header[4] = int(payload.shape[0])
         with trace_range("pp.ctrl"):
+            if self.ring is not None:
+                nb = _HDR_BYTES + 4 * int(payload.shape[0])
+                if nb > self.ctrl_bytes:
+                    raise ValueError(f"step metadata of {nb} B exceeds the control slot "
+                                     f"({self.ctrl_bytes} B)")
+                m = self._msg
+                m[:_HDR_BYTES].view(np.int64)[:] = header
+                m[_HDR_BYTES:nb].view(np.int32)[:] = payload
+                self.ring.publish(m[:nb])
+                return
+            h = torch.from_numpy(np.ascontiguousarray(header, dtype=np.int64).copy())
+            p = torch.from_numpy(np.ascontiguousarray(payload, dtype=np.int32).copy())
             for r in range(1, self.world):
                 self._ctrl_sends.append((dist.isend(h, r, group=self.ctrl_group), h))
                 if p.numel():
                     self._ctrl_sends.append((dist.isend(p, r, group=self.ctrl_group), p))
-        # never block here: stage r consumes the message of tick j only after the head has
-        # posted its data exchange of tick j (and stage r-1 has run), so a blocking drain
-        # BEFORE this tick's exchange can deadlock a deep ring (8 stages: ~2 x 28 messages
-        # are legitimately in flight). The head drains in reap_ctrl() after its exchange.
-        self._reap(blocking_above=None)
+            # never block here: stage r consumes the message of tick j only after the head
+            # has posted its data exchange of tick j, so a blocking drain BEFORE this tick's
+            # exchange can deadlock a deep ring. The head drains in reap_ctrl().
+            self._reap(blocking_above=None)
 
     def _reap(self, blocking_above):
         q = self._ctrl_sends
-        while q and q[0][0].is_completed():
-            q.popleft()[0].wait()          # completed: returns at once, releases the Work
+        i = 0
+        while i < len(q) and q[i][0].is_completed():
+            q[i][0].wait()
+            i += 1
+        del q[:i]
         if blocking_above is not None:
             while len(q) > blocking_above:
-                w, _ = q.popleft()
-                w.wait()
+                q.pop(0)[0].wait()
 
     def reap_ctrl(self) -> None:
-        """Head, after posting this tick's data exchange: release delivered control messages
-        and bound the backlog (safe to block now: every stage can consume the messages of
-        ticks <= the one just posted)."""
-        self._reap(blocking_above=64 * self.world)
+        """Head (gloo control plane), after posting this tick's data exchange: release
+        delivered messages and bound the backlog."""
+        if self._ctrl_sends:
+            self._reap(blocking_above=64 * self.world)
 
     def recv_ctrl(self) -> Tuple[np.ndarray, np.ndarray]:
-        h = torch.empty(HEADER_LEN, dtype=torch.int64)
+        """Next control message: (header int64[16], payload int32[n]). The arrays are views
+        of a reused buffer, valid until the next call."""
+        if self.ring is not None:
+            m = self.ring.consume()
+            return m[:_HDR_BYTES].view(np.int64), m[_HDR_BYTES:].view(np.int32)
+        h = self._hdr_rx
         dist.recv(h, 0, group=self.ctrl_group)
         n = int(h[4])
-        p = torch.empty(n, dtype=torch.int32)
+        p = self._pay_rx[:n]
         if n:
             dist.recv(p, 0, group=self.ctrl_group)
         return h.numpy(), p.numpy()
 
     # ------------------------------------------------------------------ data plane
-    def exchange_many(self, sends, recvs):
-        """Post this tick's grouped exchange. ``sends`` = [(tensor, peer, tag)] (snapshotted:
-        graph outputs are static buffers), ``recvs`` = [(shape, dtype, peer, tag)]. Tags
-        keep several messages between one pair apart (gloo matches per (peer, tag); RCCL
-        ignores them). Returns (recv buffers, record) for ``wait_all``, or None."""
-        ops, keep, bufs = [], [], []
+    def recv_buffer(self, shape: Sequence[int], dtype=None) -> torch.Tensor:
+        """A receive buffer allocated ONCE (engine setup) on the data-plane device."""
+        return torch.empty(tuple(shape), dtype=dtype or self.dtype, device=self.data_device)
+
+    def exchange(self, sends, recvs) -> None:
+        """This tick's grouped exchange, completed before anything later on this rank reads
+        a receive buffer or overwrites a sent tensor.
+
+        ``sends`` = [(tensor, peer, tag)] sent in place; ``recvs`` = [(buffer, peer, tag)]
+        with buffers from ``recv_buffer`` (views allowed). Tags keep several messages between
+        one pair apart (gloo matches per (peer, tag); RCCL ignores them).
+
+        RCCL: every Work is waited on the CURRENT stream — a stream dependency, not a host
+        wait — so the next kernels on this stream (the consumer replay, or the replay that
+        rewrites a sent static output) run after the transfer. gloo: a host wait."""
+        ops = []
         with trace_range("pp.exchange"):
             for t, peer, tag in sends:
                 if t is None or t.numel() == 0:
                     continue
-                snap = t.clone() if self.nccl else t.to("cpu")
-                snap = snap.contiguous()
-                keep.append(snap)
-                ops.append(dist.P2POp(dist.isend, snap, peer, tag=tag))
-            for shape, dt, peer, tag in recvs:
-                buf = torch.empty(shape, dtype=dt, device=self.data_device)
-                bufs.append(buf)
+                if not self.nccl and t.device.type != "cpu":
+                    t = t.to("cpu")          # same-device gloo rehearsal only
+                ops.append(dist.P2POp(dist.isend, t.contiguous(), peer, tag=tag))
+            for buf, peer, tag in recvs:
+                if buf.numel() == 0:
+                    continue
                 ops.append(dist.P2POp(dist.irecv, buf, peer, tag=tag))
             if not ops:
-                return None
+                return
             works = dist.batch_isend_irecv(ops)
-        rec = [works, keep, False]        # [works, snapshots, waited]
-        self._inflight.append(rec)
-        while len(self._inflight) > self.max_pending:
-            self._finish(self._inflight.popleft())
-        return bufs, rec
-
-    def exchange(self, send: Optional[torch.Tensor], recv_shape: Optional[tuple],
-                 recv_dtype=None):
-        """Ring-only form: {send -> next, receive <- prev} (tag 1)."""
-        r = self.exchange_many([(send, self.next, 1)] if send is not None else [],
-                               [(recv_shape, recv_dtype or self.dtype, self.prev, 1)]
-                               if recv_shape is not None else [])
-        if r is None:
-            return None
-        bufs, rec = r
-        return (bufs[0] if bufs else None), rec
-
-    def wait_all(self, handle):
-        """Receive buffers of an exchange (on RCCL a stream dependency, not a host wait)."""
-        bufs, rec = handle
-        self._finish(rec)
-        return [b if b.device == self.device else b.to(self.device) for b in bufs]
-
-    def _finish(self, rec) -> None:
-        # a gloo Work must be waited exactly once (a second wait on a completed receive
-        # blocks forever); an RCCL wait is a dependency of the CURRENT stream and idempotent,
-        # so it is always issued (the caller's stream may not have waited yet)
-        if self.nccl or not rec[2]:
-            for w in rec[0]:
+            for w in works:
                 w.wait()
-            rec[2] = True
+        self.exchanges += 1
 
-    def wait(self, handle) -> torch.Tensor:
-        """Input of this tick: on RCCL a stream dependency of the replay, not a host wait."""
-        buf, rec = handle
-        self._finish(rec)
-        return buf if buf.device == self.device else buf.to(self.device)
-
-    def to_host(self, handle) -> np.ndarray:
-        """Head: the tail's sampled ids on the host, synchronised on a side stream so the
-        compute stream (already running the next replay) is never blocked."""
-        buf, rec = handle
-        if self.side_stream is not None:
-            with torch.cuda.stream(self.side_stream):
-                self._finish(rec)
-                return buf.cpu().numpy()
-        self._finish(rec)
-        return buf.numpy()
+    def to_compute(self, buf: torch.Tensor) -> torch.Tensor:
+        """A received buffer as the compute device sees it (a copy only when gloo carries
+        the data plane of a GPU rank: the same-device rehearsal)."""
+        return buf if buf.device == self.device else buf.to(self.device, non_blocking=True)
 
     def flush(self) -> None:
-        while self._inflight:
-            self._finish(self._inflight.popleft())
         while self._ctrl_sends:
-            w, _ = self._ctrl_sends.popleft()
+            w, _ = self._ctrl_sends.pop(0)
             w.wait()
+
+    def close(self) -> None:
+        if self.ring is not None:
+            if self.rank == 0:
+                self.ring.close()
+            self.ring.destroy()
+            self.ring = None
 
 
 def init_distributed(backend: Optional[str] = None, device: Optional[torch.device] = None):
@@ -212,7 +254,8 @@ def init_distributed(backend: Optional[str] = None, device: Optional[torch.devic
     (``DLI_PP_TIMEOUT_S``, default 600 s), so a stage that dies mid-session turns a blocked
     exchange into an error: RCCL's watchdog aborts the communicator when the timeout fires
     (torch's ``TORCH_NCCL_ASYNC_ERROR_HANDLING`` default), gloo raises as soon as the dead
-    peer's sockets close. The head then fails its pending requests and reports unhealthy
+    peer's sockets close; the shared-memory control ring notices a dead producer / consumer
+    process. The head then fails its pending requests and reports unhealthy
     (``worker/service.PipelineService``); the master's failure detector routes new requests
     to the remaining replicas."""
     if dist.is_initialized():

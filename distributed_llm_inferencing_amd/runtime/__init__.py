@@ -2,7 +2,9 @@
 
 * ``BlockManager`` — paged-KV block allocator + batched block-table / slot-mapping builders
 * ``SafetensorsFile`` — mmap'd safetensors reader with a pinned-staging ring feeding
-  ``hipMemcpyAsync`` (GPU) or plain memcpy (CPU)
+  ``hipMemcpyAsync`` (GPU) or plain memcpy (CPU); whole tensors or row ranges
+* ``ShmRing`` — single-producer / multi-consumer broadcast ring in POSIX shared memory (the
+  pipeline's per-tick control plane between the processes of one node)
 """
 from __future__ import annotations
 
@@ -31,6 +33,8 @@ _SIGS = {
     "dli_bm_table": ([_P, _LL, _P, _I], _I),
     "dli_bm_fill_tables": ([_P, _P, _I, _P, _I], _I),
     "dli_bm_slot_mapping": ([_P, _P, _P, _P, _I, _P], _I),
+    "dli_bm_decode_prepare": ([_P, _P, _P, _I, _P, _P, _I], _I),
+    "dli_bm_ensure_batch": ([_P, _P, _P, _I], _I),
     "dli_st_open": ([ctypes.c_char_p], _P),
     "dli_st_close": ([_P], None),
     "dli_st_count": ([_P], _I),
@@ -38,6 +42,18 @@ _SIGS = {
     "dli_st_find": ([_P, ctypes.c_char_p], _I),
     "dli_st_copy_to_host": ([_P, _I, _P], _I),
     "dli_st_load_to_device": ([_P, _P, _P, _I, _P], _LL),
+    "dli_st_load_range": ([_P, _I, _LL, _LL, _P, _P, _I], _LL),
+    "dli_ring_create": ([ctypes.c_char_p, _LL, _LL, _I], _P),
+    "dli_ring_open": ([ctypes.c_char_p, _I], _P),
+    "dli_ring_unlink": ([_P], _I),
+    "dli_ring_slot_bytes": ([_P], _LL),
+    "dli_ring_publish": ([_P, _P, _LL, ctypes.c_double], _I),
+    "dli_ring_consume": ([_P, _P, _LL, ctypes.c_double], _LL),
+    "dli_ring_peek_len": ([_P, ctypes.c_double], _LL),
+    "dli_ring_published": ([_P], _LL),
+    "dli_ring_min_consumed": ([_P], _LL),
+    "dli_ring_close": ([_P], None),
+    "dli_ring_destroy": ([_P], None),
 }
 
 
@@ -86,6 +102,13 @@ class BlockManager:
     def ensure(self, seq_id: int, total_tokens: int) -> bool:
         return lib().dli_bm_ensure(self._h, seq_id, total_tokens) >= 0
 
+    def ensure_batch(self, seq_ids: np.ndarray, totals: np.ndarray) -> int:
+        """``ensure`` for each (seq, total) in order, stopping at the first that does not
+        fit; returns how many succeeded."""
+        ids = np.ascontiguousarray(seq_ids, dtype=np.int64)
+        t = np.ascontiguousarray(totals, dtype=np.int32)
+        return lib().dli_bm_ensure_batch(self._h, _np_ptr(ids), _np_ptr(t), ids.shape[0])
+
     def free(self, seq_id: int) -> int:
         return lib().dli_bm_free(self._h, seq_id)
 
@@ -102,6 +125,23 @@ class BlockManager:
         if r < 0:
             raise RuntimeError("block table wider than max_blocks")
         return out
+
+    def decode_prepare(self, seq_ids: np.ndarray, ctx: np.ndarray, max_blocks: int):
+        """One decode step's KV metadata (grow tables, new-token slots, padded tables) in
+        one call. Returns (slots [n], tables [n, max_blocks], widest table), or
+        (-1, i, None) when sequence i could not get a block."""
+        ids = np.ascontiguousarray(seq_ids, dtype=np.int64)
+        c = np.ascontiguousarray(ctx, dtype=np.int32)
+        n = ids.shape[0]
+        slots = np.empty(n, dtype=np.int32)
+        tables = np.empty((n, max(1, max_blocks)), dtype=np.int32)
+        r = lib().dli_bm_decode_prepare(self._h, _np_ptr(ids), _np_ptr(c), n, _np_ptr(slots),
+                                        _np_ptr(tables), tables.shape[1])
+        if r == -(n + 1):
+            raise RuntimeError("block table wider than max_blocks")
+        if r < 0:
+            return -1, -r - 1, None
+        return slots, tables, r
 
     def slot_mapping(self, seq_ids, starts, counts) -> np.ndarray:
         ids = np.asarray(seq_ids, dtype=np.int64)
@@ -170,3 +210,102 @@ class SafetensorsFile:
                                              ctypes.c_void_p(out[n].data_ptr())) != 0:
                     raise RuntimeError(f"host load failed for {n}")
         return out
+
+    def load_rows(self, name: str, lo: int, hi: int, device="cpu") -> torch.Tensor:
+        """Rows [lo, hi) of a row-major tensor (e.g. one rank's vocabulary slice of the LM
+        head) without reading the rest of it: a contiguous byte range of the file."""
+        dt, shape, nbytes = self.meta[name]
+        if not shape or not (0 <= lo <= hi <= shape[0]):
+            raise ValueError(f"rows [{lo}, {hi}) outside {name} {shape}")
+        row = nbytes // shape[0]
+        dev = torch.device(device)
+        out = torch.empty((hi - lo, *shape[1:]), dtype=_DT[dt], device=dev)
+        if hi == lo:
+            return out
+        stream = torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else None
+        r = lib().dli_st_load_range(self._h, self._index[name], lo * row, (hi - lo) * row,
+                                    ctypes.c_void_p(out.data_ptr()), stream,
+                                    1 if dev.type == "cuda" else 0)
+        if r < 0:
+            raise RuntimeError(f"row load failed for {name} ({r})")
+        return out
+
+
+class ShmRing:
+    """Broadcast ring in POSIX shared memory (``csrc/runtime/shm_ring.cpp``): one producer
+    publishes byte messages, every consumer reads each of them in order. ``create`` on the
+    producer, ``open(index)`` on consumer ``index``; waits back off to sleeps and fail
+    (``TimeoutError``) when the peer process is gone or ``timeout_s`` passes."""
+
+    def __init__(self, handle, name: str, producer: bool):
+        self._h, self.name, self.producer = handle, name, producer
+        self.slot_bytes = int(lib().dli_ring_slot_bytes(handle))
+        self._buf = np.empty(self.slot_bytes, dtype=np.uint8)
+
+    @classmethod
+    def create(cls, name: str, slots: int, slot_bytes: int, consumers: int) -> "ShmRing":
+        h = lib().dli_ring_create(name.encode(), int(slots), int(slot_bytes), int(consumers))
+        if not h:
+            raise OSError(f"cannot create shared-memory ring {name}")
+        return cls(h, name, True)
+
+    @classmethod
+    def open(cls, name: str, index: int, timeout_s: float = 120.0) -> "ShmRing":
+        import time
+        t0 = time.monotonic()
+        while True:
+            h = lib().dli_ring_open(name.encode(), int(index))
+            if h:
+                return cls(h, name, False)
+            if time.monotonic() - t0 > timeout_s:
+                raise OSError(f"cannot open shared-memory ring {name}")
+            time.sleep(0.01)
+
+    def unlink(self):
+        lib().dli_ring_unlink(self._h)
+
+    def publish(self, data: np.ndarray, timeout_s: float = 600.0) -> None:
+        a = np.ascontiguousarray(data)
+        r = lib().dli_ring_publish(self._h, _np_ptr(a), a.nbytes, float(timeout_s))
+        if r == -1:
+            raise ValueError(f"message of {a.nbytes} B exceeds ring slot {self.slot_bytes} B")
+        if r == -2:
+            raise TimeoutError("control ring: a consumer stopped reading (dead or hung)")
+        if r == -3:
+            raise EOFError("control ring closed")
+
+    def consume(self, timeout_s: float = 0.0) -> np.ndarray:
+        """Next message as a uint8 view of an internal buffer (valid until the next call).
+        ``timeout_s`` = 0 waits as long as the producer process is alive."""
+        n = lib().dli_ring_consume(self._h, _np_ptr(self._buf), self._buf.nbytes,
+                                   float(timeout_s))
+        if n == -2:
+            raise TimeoutError("control ring: producer gone or timeout")
+        if n == -3:
+            raise EOFError("control ring closed")
+        if n < 0:
+            raise RuntimeError(f"control ring consume failed ({n})")
+        return self._buf[:n]
+
+    @property
+    def published(self) -> int:
+        return int(lib().dli_ring_published(self._h))
+
+    @property
+    def min_consumed(self) -> int:
+        return int(lib().dli_ring_min_consumed(self._h))
+
+    def close(self):
+        if self._h:
+            lib().dli_ring_close(self._h)
+
+    def destroy(self):
+        h, self._h = self._h, None
+        if h and _lib is not None:
+            _lib.dli_ring_destroy(h)
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:  # noqa: BLE001
+            pass

@@ -309,7 +309,7 @@ def create_worker_app(settings: Optional[Settings] = None, device: Optional[str]
                 out = st.services[name].generate(prompt, params, timeout=timeout + 30)
             if out.finish_reason == "timeout":
                 raise TimeoutError("Inference generation timed out")
-            return jsonify({"status": "success", "result": out.text,
+            return jsonify({"status": "success", "result": out.resolve_text(),
                             "execution_time": time.time() - t0,
                             "output_tokens": len(out.output_ids),
                             "finish_reason": out.finish_reason})
