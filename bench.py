@@ -147,6 +147,8 @@ def main():
     ap.add_argument("--prompt-len", type=int, default=32)
     ap.add_argument("--max-length", type=int, default=100)
     ap.add_argument("--max-model-len", type=int, default=512)
+    ap.add_argument("--shard-dir", default=None,
+                    help="N>1 pp: load each stage from <dir>/shard_<rank>/ (shard-model output)")
     ap.add_argument("--mode", default="auto", choices=["auto", "pp", "ep", "tp", "dp"],
                     help="N>1: pp = layer-sharded pipeline (dense, default), ep = expert "
                          "parallel (MoE), tp = tensor-parallel ablation, dp = independent "

@@ -116,6 +116,22 @@ int dli_bm_free(void* h, long long seq) {
   return n;
 }
 
+// dli_bm_free for seqs[0..n); returns the blocks released.
+int dli_bm_free_batch(void* h, const long long* seqs, int n) {
+  auto* m = H(h);
+  std::lock_guard<std::mutex> g(m->mu);
+  int total = 0;
+  for (int i = 0; i < n; ++i) {
+    auto it = m->tables.find(seqs[i]);
+    if (it == m->tables.end()) continue;
+    total += (int)it->second.size();
+    for (auto it2 = it->second.rbegin(); it2 != it->second.rend(); ++it2)
+      m->free_list.push_back(*it2);
+    m->tables.erase(it);
+  }
+  return total;
+}
+
 int dli_bm_table(void* h, long long seq, int* out, int max_blocks) {
   auto* m = H(h);
   std::lock_guard<std::mutex> g(m->mu);

@@ -9,8 +9,10 @@ launcher for an 8-GPU MI355X box.
     serve-node      --gpus N [--base-port 5000] [--master URL]
                     one worker process per GPU (HIP_VISIBLE_DEVICES=i, port base+i), each
                     registered with the master as a node
-    serve-pipeline  --model M [--port 5000]             (under torchrun) N-rank layer-sharded
-                    pipeline; rank 0 serves the worker API and reports the stages as shards
+    serve-pipeline  --model M [--port 5000] [--shard-dir D]
+                    (under torchrun) N-rank layer-sharded pipeline; rank 0 serves the worker
+                    API and reports the stages as shards; --shard-dir serves the files
+                    `shard-model` exported (rank r <- D/shard_<r>/)
     serve-cluster   --model M --gpus 8 --dp K [--base-port 5000] [--master URL]
                     K data-parallel replicas, each a pipeline of gpus/K stages (SURVEY.md
                     §2.5 "DP replicas"); every replica head registers as a node and the
@@ -76,6 +78,9 @@ def _serve_pipeline(argv):
     ap.add_argument("--max-batch", type=int, default=256)
     ap.add_argument("--max-model-len", type=int, default=2048)
     ap.add_argument("--policy", default="balanced")
+    ap.add_argument("--shard-dir", default=None,
+                    help="serve the weights `shard-model` exported: rank r loads "
+                         "<dir>/shard_<r>/model.safetensors (layers from its metadata.json)")
     ap.add_argument("--no-shard-report", action="store_true",
                     help="DP replica: serve the model as a plain node (no shard rows)")
     a = ap.parse_args(argv)
@@ -89,7 +94,8 @@ def _serve_pipeline(argv):
     if torch.cuda.is_available():
         torch.cuda.set_device(local)
     eng = DistributedPipelineEngine(a.model, dev, max_batch=a.max_batch,
-                                    max_model_len=a.max_model_len, policy=a.policy)
+                                    max_model_len=a.max_model_len, policy=a.policy,
+                                    shard_dir=a.shard_dir)
     eng.warmup()
     if eng.rank != 0:
         eng.serve()
@@ -102,7 +108,9 @@ def _serve_pipeline(argv):
     st.pipeline_service = PipelineService(eng, name=a.model)
     st.tokenizers[a.model] = eng.head.tok
     st.pipeline_shards = [] if a.no_shard_report else [
-        {"model_name": a.model, "shard_id": p.shard_id, "path": f"rank{p.shard_id}",
+        {"model_name": a.model, "shard_id": p.shard_id,
+         "path": (os.path.join(a.shard_dir, f"shard_{p.shard_id}") if a.shard_dir
+                  else f"rank{p.shard_id}"),
          "metadata": p.to_metadata(a.model, len(eng.plans), eng.cfg.num_layers)}
         for p in eng.plans]
     app = create_worker_app(s, state=st)

@@ -42,6 +42,11 @@ class StepMeta:
     table_used: Optional[int] = None
     # seq_ids as int64 numpy (set by the decode scheduler; saves list -> array conversions)
     seq_ids_arr: Optional[np.ndarray] = None
+    # the payload already packed by the C++ scheduler core (decode fast path), its
+    # un-trimmed table width, and the core's identity for the matching update
+    packed_payload: Optional[np.ndarray] = None
+    table_width_full: int = 0
+    core: Optional[tuple] = None
 
     @property
     def num_seqs(self) -> int:
@@ -54,6 +59,13 @@ class StepMeta:
     # ---- wire format: header (int64) + payload (int32) ------------------------------------
     def pack(self) -> (np.ndarray, np.ndarray):
         S, T = self.num_seqs, self.num_tokens
+        if self.packed_payload is not None:
+            header = np.zeros(HEADER_LEN, dtype=np.int64)
+            header[:7] = [self.kind, S, T, int(self.table_used), self.packed_payload.shape[0],
+                          self.microbatch, self.step_id]
+            header[7] = 1
+            header[8] = max(int(self.table_width_full), int(self.table_used))
+            return header, self.packed_payload
         tables = self.block_tables
         width = 0 if tables is None else int(tables.shape[1])
         if tables is not None and tables.shape[1] > 1:

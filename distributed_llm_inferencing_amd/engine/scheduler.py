@@ -104,11 +104,44 @@ class _MBState:
         self.seqs = [s for s, kp in zip(self.seqs, keep.tolist()) if kp]
 
 
+class _MBCore:
+    """The same mirror in C++ (``runtime.DecodeCore``): the decode fast path of the pipeline
+    head, where one tick's scheduling + token application must cost tens of microseconds.
+    Used when no lookahead is involved and no row has stop tokens."""
+    __slots__ = ("seqs", "core", "first_rows")
+
+    def __init__(self, seqs: List[Sequence], eos: Optional[int], max_model_len: int):
+        from ..runtime import DecodeCore
+        self.seqs = list(seqs)
+        n = len(seqs)
+        out_cnt = np.fromiter((len(s.output_ids) for s in seqs), np.int32, n)
+        budget = np.fromiter((s.params.budget(s.prompt_len) for s in seqs), np.int32, n)
+        self.first_rows = np.nonzero(out_cnt == 0)[0].tolist()
+        left = int((budget - out_cnt).max()) if n else 1
+        self.core = DecodeCore(
+            np.fromiter((s.seq_id for s in seqs), np.int64, n),
+            np.fromiter((s.total_len for s in seqs), np.int32, n), out_cnt, budget,
+            np.fromiter(((s.output_ids[-1] if s.output_ids else s.prompt_ids[-1])
+                         for s in seqs), np.int32, n),
+            np.fromiter((s.params.effective_temperature() for s in seqs), np.float32, n),
+            np.fromiter((s.params.top_k for s in seqs), np.int32, n),
+            np.fromiter((s.params.top_p for s in seqs), np.float32, n),
+            np.fromiter((s.seed for s in seqs), np.int64, n),
+            np.fromiter((eos is not None and not s.params.ignore_eos for s in seqs), bool, n),
+            eos, max_model_len, max(1, min(left, 4096)))
+
+    def flush(self) -> None:
+        h = self.core.history()
+        if h.shape[1]:
+            for s, row in zip(self.seqs, h.tolist()):
+                s.output_ids.extend(row)
+
+
 class Scheduler:
     def __init__(self, block_manager: BlockManager, max_seqs_per_mb: int = 256,
                  max_prefill_tokens: int = 16384, num_microbatches: int = 1,
                  eos_token_id: Optional[int] = None, max_model_len: int = 4096,
-                 table_width: Optional[int] = None):
+                 table_width: Optional[int] = None, native_decode: bool = False):
         self.bm = block_manager
         self.bs = block_manager.block_size
         self.max_seqs = max_seqs_per_mb
@@ -123,6 +156,8 @@ class Scheduler:
         self._state: List[Optional[_MBState]] = [None] * self.M
         self.seqs: Dict[int, Sequence] = {}
         self.finished: List[Sequence] = []
+        # decode fast path in C++ (runtime.DecodeCore) for microbatches without stop tokens
+        self.native_decode = native_decode
         self._next_id = 0
         self._step = 0
         self._deadlines = 0
@@ -188,11 +223,12 @@ class Scheduler:
                 pass
         self._mark_finished(seq, reason)
 
-    def _mark_finished(self, seq: Sequence, reason: str):
+    def _mark_finished(self, seq: Sequence, reason: str, free: bool = True):
         seq.state = SeqState.FINISHED
         seq.finish_reason = reason
         seq.finish_time = time.perf_counter()
-        self.bm.free(seq.seq_id)
+        if free:
+            self.bm.free(seq.seq_id)
         if seq.params.timeout_s is not None:
             self._deadlines -= 1
         self.finished.append(seq)
@@ -299,10 +335,16 @@ class Scheduler:
                         top_k=topk, top_p=topp, seeds=seeds, microbatch=mb, step_id=self._step,
                         seq_ids_arr=sid)
 
-    def _mb_state(self, mb: int) -> _MBState:
+    def _mb_state(self, mb: int, native: bool = False):
         st = self._state[mb]
+        if st is not None and native != isinstance(st, _MBCore):
+            self._drop_state(mb)
+            st = None
         if st is None:
-            st = _MBState(self.running[mb], self.eos)
+            if native:
+                st = _MBCore(self.running[mb], self.eos, self.max_model_len)
+            else:
+                st = _MBState(self.running[mb], self.eos)
             self._state[mb] = st
         return st
 
@@ -320,9 +362,51 @@ class Scheduler:
         hit = sk[pos] == st.sid
         return hit.astype(np.int32), np.where(hit, order[pos], -1).astype(np.int32)
 
+    def _native_ok(self, mb: int, inflight: Optional[StepMeta]) -> bool:
+        if not self.native_decode or inflight is not None:
+            return False
+        st = self._state[mb]
+        if isinstance(st, _MBCore):
+            return True
+        return not any(s.params.stop_token_ids for s in self.running[mb])
+
+    def _decode_native(self, mb: int) -> Optional[StepMeta]:
+        while True:
+            st = self._mb_state(mb, native=True)
+            S = len(st.seqs)
+            if S == 0:
+                return None
+            payload, cols = st.core.schedule(self.bm, self.table_width)
+            if payload is not None:
+                break
+            if not self._preempt(mb):
+                return None
+        o = [0]
+
+        def take(n, dt=None):
+            v = payload[o[0]:o[0] + n]
+            o[0] += n
+            return v if dt is None else v.view(dt)
+        sid = take(S)
+        ids, pos, slots, lens, ctx = take(S), take(S), take(S), take(S), take(S)
+        tables = take(S * cols).reshape(S, cols)
+        temp, topk, topp = take(S, np.float32), take(S), take(S, np.float32)
+        seeds = take(2 * S, np.int64)
+        meta = StepMeta(kind=DECODE, seq_ids=sid, input_ids=ids, positions=pos,
+                        slot_mapping=slots, seq_lens=lens, context_lens=ctx, block_tables=tables,
+                        temperature=temp, top_k=topk, top_p=topp, seeds=seeds, microbatch=mb,
+                        step_id=self._step)
+        meta.table_used = cols
+        meta.packed_payload = payload
+        meta.table_width_full = self.table_width
+        meta.core = (st, st.core.steps, S)
+        return meta
+
     def _decode(self, mb: int, inflight: Optional[StepMeta] = None) -> Optional[StepMeta]:
         if not self.running[mb]:
             return None
+        if self._native_ok(mb, inflight):
+            return self._decode_native(mb)
         while True:
             st = self._mb_state(mb)
             if len(st.seqs) == 0:
@@ -362,6 +446,12 @@ class Scheduler:
         """Apply sampled tokens of a finished step; returns sequences that finished."""
         tokens = np.asarray(tokens, dtype=np.int32).reshape(-1)
         mb = meta.microbatch
+        core = getattr(meta, "core", None)
+        if core is not None:
+            st, steps, S = core
+            if (st is self._state[mb] and st.core.steps == steps and st.core.rows == S
+                    and tokens.shape[0] == S):
+                return self._update_native(st, tokens, mb)
         st = self._state[mb] if meta.kind == DECODE else None
         if st is not None and len(st.seqs) == len(meta.seq_ids) and \
                 np.array_equal(st.sid, meta.seq_ids_arr if meta.seq_ids_arr is not None
@@ -405,6 +495,37 @@ class Scheduler:
                 self._state[mb] = None
             else:
                 st.compact(~done_mask)
+                self.running[mb] = list(st.seqs)
+        return done
+
+    def _update_native(self, st: _MBCore, tokens: np.ndarray, mb: int) -> List[Sequence]:
+        done_idx, stop = st.core.update(tokens)
+        if st.first_rows:
+            now = time.perf_counter()
+            for i in st.first_rows:
+                st.seqs[i].first_token_time = now
+            st.first_rows = []
+        done = []
+        if done_idx.shape[0]:
+            seqs = st.seqs
+            idx = done_idx.tolist()
+            if len(idx) > 8:          # many rows finish together: one history copy
+                hist = st.core.history()[done_idx].tolist()
+            else:
+                hist = [st.core.row_history(i) for i in idx]
+            for i, sf, h in zip(idx, stop.tolist(), hist):
+                s = seqs[i]
+                s.output_ids.extend(h)
+                self._mark_finished(s, "stop" if sf else "length", free=False)
+                done.append(s)
+            self.bm.free_batch(np.fromiter((q.seq_id for q in done), np.int64, len(done)))
+            if len(idx) == len(seqs):
+                self.running[mb] = []
+                self._state[mb] = None
+            else:
+                st.core.compact(done_idx)
+                dropped = set(idx)
+                st.seqs = [q for i, q in enumerate(seqs) if i not in dropped]
                 self.running[mb] = list(st.seqs)
         return done
 

@@ -250,6 +250,8 @@ class PipelineHead:
         self.host_s = 0.0          # head host time in ticks, excluding transport waits
         self.ticks = 0
         self.tick_log = [] if os.environ.get("DLI_PP_TICK_LOG", "0") == "1" else None
+        # host seconds / ticks by step kind (EMPTY / PREFILL / DECODE)
+        self.host_by_kind = {EMPTY: [0.0, 0], PREFILL: [0.0, 0], DECODE: [0.0, 0]}
         self.phase_s = {k: 0.0 for k in ("update", "finish", "schedule", "ctrl", "head_ops",
                                          "compute")}
         B, D = stage.max_batch, stage.cfg.hidden_size
@@ -368,10 +370,14 @@ class PipelineHead:
                 self._account(meta)
             now = pc()
             ph["compute"] += now - t6
+            hs = now - t0 - wait_s
+            kk = self.host_by_kind[meta.kind if meta is not None else EMPTY]
+            kk[0] += hs
+            kk[1] += 1
             if self.tick_log is not None:
-                self.tick_log.append((meta.kind if meta is not None else 0, t1 - t0 - wait_s,
+                self.tick_log.append((meta.kind if meta is not None else 0, hs,
                                       t2 - t1, t3 - t2, t4 - t3, t6 - t5, now - t6))
-            self.host_s += now - t0 - wait_s
+            self.host_s += hs
             self.ticks += 1
             self.stats.busy_s += now - t0
             k += 1
@@ -594,7 +600,8 @@ class DistributedPipelineEngine:
             sched = Scheduler(bm, max_seqs_per_mb=max_batch, max_prefill_tokens=max_prefill_tokens,
                               num_microbatches=self.microbatches,
                               eos_token_id=self.cfg.eos_token_id,
-                              max_model_len=max_model_len, table_width=tw)
+                              max_model_len=max_model_len, table_width=tw,
+                              native_decode=os.environ.get("DLI_NATIVE_SCHED", "1") == "1")
             tok_path = None
             if shard_dir is not None and (Path(shard_dir) / "tokenizer").exists():
                 tok_path = str(Path(shard_dir) / "tokenizer")
@@ -654,7 +661,8 @@ class LocalPipeline:
                                            dtype=dtype))
         self.sched = Scheduler(BlockManager(num_blocks, block_size), max_seqs_per_mb=max_batch,
                                num_microbatches=num_stages, eos_token_id=self.cfg.eos_token_id,
-                               max_model_len=max_model_len, table_width=tw)
+                               max_model_len=max_model_len, table_width=tw,
+                               native_decode=os.environ.get("DLI_NATIVE_SCHED", "1") == "1")
         self.tok = tokenizer or load_tokenizer(self.cfg)
         self.stats = EngineStats()
         self._ids = 0
@@ -766,6 +774,7 @@ def bench_pipeline(args, world: int, rank: int, make_prompts):
     toks, lats = 0, []
     if rank == 0:
         eng.head.host_s, eng.head.ticks = 0.0, 0
+        eng.head.host_by_kind = {k: [0.0, 0] for k in eng.head.host_by_kind}
     for s in range(args.steps):
         n, l = wave(s)
         toks += n
@@ -784,6 +793,8 @@ def bench_pipeline(args, world: int, rank: int, make_prompts):
         return None
     snap = eng.head.stats.snapshot()
     snap["head_host_ms_per_tick"] = round(1e3 * eng.head.host_s / max(1, eng.head.ticks), 4)
+    hd = eng.head.host_by_kind[DECODE]
+    snap["head_host_ms_per_decode_tick"] = round(1e3 * hd[0] / max(1, hd[1]), 4)
     snap["control_plane"] = eng.channel.ctrl_kind
     return {"tokens": toks, "seconds": float(dt.item()), "latencies": lats,
             "global_batch": per_wave, "parallelism": f"pp{world}", "engine": snap}

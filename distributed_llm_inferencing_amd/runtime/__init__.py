@@ -1,6 +1,8 @@
 """Bindings for the host C++ runtime (``lib/libdli_runtime.so``, sources in csrc/runtime):
 
 * ``BlockManager`` — paged-KV block allocator + batched block-table / slot-mapping builders
+* ``DecodeCore`` — one microbatch's running sequences + the decode fast path of the
+  continuous-batching scheduler (schedule -> packed step metadata, apply sampled tokens)
 * ``SafetensorsFile`` — mmap'd safetensors reader with a pinned-staging ring feeding
   ``hipMemcpyAsync`` (GPU) or plain memcpy (CPU); whole tensors or row ranges
 * ``ShmRing`` — single-producer / multi-consumer broadcast ring in POSIX shared memory (the
@@ -11,7 +13,7 @@ from __future__ import annotations
 import ctypes
 import threading
 from pathlib import Path
-from typing import Dict, List, Sequence
+from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 import torch
@@ -30,11 +32,22 @@ _SIGS = {
     "dli_bm_blocks_needed": ([_P, _LL, _LL], _I),
     "dli_bm_ensure": ([_P, _LL, _LL], _I),
     "dli_bm_free": ([_P, _LL], _I),
+    "dli_bm_free_batch": ([_P, _P, _I], _I),
     "dli_bm_table": ([_P, _LL, _P, _I], _I),
     "dli_bm_fill_tables": ([_P, _P, _I, _P, _I], _I),
     "dli_bm_slot_mapping": ([_P, _P, _P, _P, _I, _P], _I),
     "dli_bm_decode_prepare": ([_P, _P, _P, _I, _P, _P, _I], _I),
     "dli_bm_ensure_batch": ([_P, _P, _P, _I], _I),
+    "dli_mb_create": ([_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I], _P),
+    "dli_mb_destroy": ([_P], None),
+    "dli_mb_rows": ([_P], _I),
+    "dli_mb_steps": ([_P], _I),
+    "dli_mb_payload_words": ([_P, _I], _LL),
+    "dli_mb_schedule": ([_P, _P, _I, _P, _LL, _P], _LL),
+    "dli_mb_update": ([_P, _P, _I, _P, _P], _I),
+    "dli_mb_row_history": ([_P, _I, _P], _I),
+    "dli_mb_history": ([_P, _P], _I),
+    "dli_mb_compact": ([_P, _P, _I], _I),
     "dli_st_open": ([ctypes.c_char_p], _P),
     "dli_st_close": ([_P], None),
     "dli_st_count": ([_P], _I),
@@ -59,6 +72,8 @@ _SIGS = {
 
 def lib():
     global _lib
+    if _lib is not None:
+        return _lib
     with _lock:
         if _lib is None:
             if not LIB_PATH.exists():
@@ -73,8 +88,8 @@ def lib():
     return _lib
 
 
-def _np_ptr(a: np.ndarray):
-    return a.ctypes.data_as(ctypes.c_void_p)
+def _np_ptr(a: np.ndarray) -> int:
+    return a.ctypes.data              # plain int: ctypes converts it for c_void_p arguments
 
 
 class BlockManager:
@@ -111,6 +126,10 @@ class BlockManager:
 
     def free(self, seq_id: int) -> int:
         return lib().dli_bm_free(self._h, seq_id)
+
+    def free_batch(self, seq_ids: np.ndarray) -> int:
+        ids = np.ascontiguousarray(seq_ids, dtype=np.int64)
+        return lib().dli_bm_free_batch(self._h, _np_ptr(ids), ids.shape[0])
 
     def table(self, seq_id: int) -> List[int]:
         cap = max(1, self.num_blocks)
@@ -153,6 +172,81 @@ class BlockManager:
         if r < 0:
             raise RuntimeError("slot mapping beyond allocated blocks")
         return out
+
+
+class DecodeCore:
+    """C++ mirror of one microbatch's running sequences (``csrc/runtime/decode_core.cpp``).
+    ``schedule`` returns the packed decode-step payload (StepMeta wire format) and its table
+    width, ``update`` applies one token per row and returns (finished rows, EOS flags)."""
+
+    def __init__(self, sid, ctx, out_cnt, budget, last, temp, topk, topp, seed, eos_ok,
+                 eos: Optional[int], max_model_len: int, hist_cap: int):
+        a = [np.ascontiguousarray(sid, np.int64), np.ascontiguousarray(ctx, np.int32),
+             np.ascontiguousarray(out_cnt, np.int32), np.ascontiguousarray(budget, np.int32),
+             np.ascontiguousarray(last, np.int32), np.ascontiguousarray(temp, np.float32),
+             np.ascontiguousarray(topk, np.int32), np.ascontiguousarray(topp, np.float32),
+             np.ascontiguousarray(seed, np.int64), np.ascontiguousarray(eos_ok, np.uint8)]
+        n = a[0].shape[0]
+        self._h = lib().dli_mb_create(n, *[_np_ptr(x) for x in a],
+                                      -1 if eos is None else int(eos), int(max_model_len),
+                                      int(hist_cap))
+        if not self._h:
+            raise ValueError("invalid microbatch")
+        self._cols = ctypes.c_int()
+        self._done = np.empty(max(1, n), np.int32)
+        self._stop = np.empty(max(1, n), np.int32)
+
+    def __del__(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h and _lib is not None:
+            _lib.dli_mb_destroy(h)
+
+    @property
+    def rows(self) -> int:
+        return lib().dli_mb_rows(self._h)
+
+    @property
+    def steps(self) -> int:
+        return lib().dli_mb_steps(self._h)
+
+    def schedule(self, bm: "BlockManager", table_width: int):
+        """(payload int32, table columns) or (None, failing row) when a row could not get a
+        KV block."""
+        L = lib()
+        words = L.dli_mb_payload_words(self._h, table_width)
+        out = np.empty(max(1, words), np.int32)
+        r = L.dli_mb_schedule(self._h, bm._h, int(table_width), _np_ptr(out), out.shape[0],
+                              ctypes.byref(self._cols))
+        n = self.rows
+        if r == -(n + 1):
+            raise RuntimeError("decode metadata: block table wider than the table width")
+        if r < 0:
+            return None, int(-r - 1)
+        return out[:r], self._cols.value
+
+    def update(self, tokens: np.ndarray):
+        t = np.ascontiguousarray(tokens, np.int32)
+        nd = lib().dli_mb_update(self._h, _np_ptr(t), t.shape[0], _np_ptr(self._done),
+                                 _np_ptr(self._stop))
+        if nd < 0:
+            raise ValueError(f"{t.shape[0]} tokens for a microbatch of {self.rows}")
+        return self._done[:nd], self._stop[:nd]
+
+    def row_history(self, row: int) -> List[int]:
+        out = np.empty(max(1, self.steps), np.int32)
+        k = lib().dli_mb_row_history(self._h, int(row), _np_ptr(out))
+        return out[:k].tolist()
+
+    def history(self) -> np.ndarray:
+        n, k = self.rows, self.steps
+        out = np.empty((n, k), np.int32)
+        if n and k:
+            lib().dli_mb_history(self._h, _np_ptr(out))
+        return out
+
+    def compact(self, drop: np.ndarray) -> int:
+        d = np.ascontiguousarray(drop, np.int32)
+        return lib().dli_mb_compact(self._h, _np_ptr(d), d.shape[0])
 
 
 _DT = {"BF16": torch.bfloat16, "F16": torch.float16, "F32": torch.float32, "I32": torch.int32,

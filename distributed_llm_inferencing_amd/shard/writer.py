@@ -87,6 +87,41 @@ def load_shard(shard_path: str, device="cpu") -> Tuple[ModelConfig, dict, Dict[s
     return cfg, meta, params
 
 
+def load_cached_model(cache_dir: str, model_name: str, device="cpu"):
+    """Whole-model weights from the model cache, or None when the cache holds none:
+    ``<cache>/<model>/model.safetensors`` + ``config.json``, or every ``shard_<i>/`` of an
+    export (merged). Returns (config, params on `device`, tokenizer dir or None)."""
+    root = model_dir(cache_dir, model_name)
+    if not root.is_dir():
+        return None
+    tok = str(root / "tokenizer") if (root / "tokenizer").is_dir() else None
+    if (root / "model.safetensors").exists() and (root / "config.json").exists():
+        from ..runtime import SafetensorsFile
+        cfg = ModelConfig.from_dict(json.loads((root / "config.json").read_text()))
+        f = SafetensorsFile(str(root / "model.safetensors"))
+        try:
+            params = f.load(device=device)
+        finally:
+            f.close()
+        return cfg, params, tok
+    shards = sorted((d for d in root.glob("shard_*") if (d / "model.safetensors").exists()),
+                    key=lambda d: int(d.name.split("_")[1]))
+    if not shards:
+        return None
+    cfg, params, covered = None, {}, 0
+    for d in shards:
+        c, meta, p = load_shard(str(d), device=device)
+        if int(meta["start_layer"]) != covered:
+            raise ValueError(f"{root}: shard {d.name} starts at layer {meta['start_layer']}, "
+                             f"expected {covered}")
+        covered = int(meta["end_layer"]) + 1
+        cfg = c
+        params.update(p)
+    if covered != cfg.num_layers:
+        raise ValueError(f"{root}: shards cover {covered} of {cfg.num_layers} layers")
+    return cfg, params, tok
+
+
 def stage_plan_from_metadata(meta: dict) -> StagePlan:
     s, e = int(meta["start_layer"]), int(meta["end_layer"]) + 1
     return StagePlan(int(meta["shard_id"]), s, e, int(meta.get("weight_bytes", 0)), 0.0,

@@ -81,18 +81,33 @@ class WorkerState:
         self.services: Dict[str, object] = {}           # model_name -> service
         self.tokenizers: Dict[str, object] = {}
         self.shards: Dict[str, Dict[int, dict]] = {}     # model -> shard_id -> record
-        self.shard_pipes: Dict[tuple, object] = {}
+        self.shard_pipes: Dict[tuple, object] = {}     # (model, shard ids) -> EngineService
+        self.weights_source: Dict[str, str] = {}
         self.lock = threading.RLock()
         os.makedirs(settings.model_cache_dir, exist_ok=True)
 
     # ------------------------------------------------------------------ models
     def load_model(self, name: str):
+        """Reference: ``from_pretrained(name, cache_dir=MODEL_CACHE_DIR)`` then ``.to(DEVICE)``
+        (worker/app.py:117-124). Here: weights from ``MODEL_CACHE_DIR/<name>/`` when present
+        (a ``model.safetensors`` + ``config.json``, or the ``shard_<i>/`` directories the
+        ``shard-model`` CLI writes), streamed into HBM by the C++ loader; otherwise the
+        architecture's deterministic random init (no checkpoints are fetchable here)."""
         from ..engine.llm_engine import LLMEngine
+        from ..shard.writer import load_cached_model
         with self.lock:
             if name in self.services or name == getattr(self, "pipeline_model", None):
                 return False            # a pipeline head serves its model across all stages
-            cfg = get_config(name)
-            eng = LLMEngine(cfg, device=str(self.device), **self.engine_kwargs)
+            cached = load_cached_model(self.settings.model_cache_dir, name, self.device)
+            if cached is not None:
+                cfg, params, tok_dir = cached
+                eng = LLMEngine(cfg, device=str(self.device), params=params,
+                                tokenizer_path=tok_dir, **self.engine_kwargs)
+                self.weights_source[name] = "cache"
+            else:
+                cfg = get_config(name)
+                eng = LLMEngine(cfg, device=str(self.device), **self.engine_kwargs)
+                self.weights_source[name] = "random-init"
             if eng.device.type == "cuda":
                 eng.warmup()          # capture decode graphs (+ GEMM autotune) before serving
             self.services[name] = EngineService(eng, name=name.replace("/", "_"))
@@ -107,7 +122,7 @@ class WorkerState:
             self.tokenizers.pop(name, None)
             self.shards.pop(name, None)
             for k in [k for k in self.shard_pipes if k[0] == name]:
-                self.shard_pipes.pop(k)
+                self.shard_pipes.pop(k).close()
             if self.device.type == "cuda":
                 torch.cuda.empty_cache()
 
@@ -133,7 +148,10 @@ class WorkerState:
             return True
 
     def shard_pipeline(self, name: str, shard_ids):
-        """A loopback pipeline over the listed loaded shards; they must cover every layer."""
+        """A loopback pipeline over the listed loaded shards (they must cover every layer),
+        behind its own engine thread: concurrent ``shard_ids`` requests are admitted between
+        ticks and batched together (the reference ran ``shard_ids[0]`` alone, one request at
+        a time: worker/app.py:332-372)."""
         from ..parallel.pipeline import LocalPipeline
         key = (name, tuple(sorted(shard_ids)))
         with self.lock:
@@ -164,9 +182,10 @@ class WorkerState:
             pipe = LocalPipeline(cfg, len(plans), device=self.device, max_batch=kw["max_batch"],
                                  max_model_len=kw["max_model_len"],
                                  num_blocks=kw["num_blocks"] or 4096, params=params,
-                                 plans=plans)
-            self.shard_pipes[key] = pipe
-            return pipe
+                                 plans=plans, tokenizer=self.tokenizers.get(name))
+            svc = EngineService(pipe, name=f"{name.replace('/', '_')}-shards")
+            self.shard_pipes[key] = svc
+            return svc
 
     def resources(self) -> dict:
         gpu_frac, extra = 0.0, {}
@@ -296,9 +315,8 @@ def create_worker_app(settings: Optional[Settings] = None, device: Optional[str]
                 # stage of this model runs on this rank's pipeline, with or without shard_ids
                 out = svc.generate(prompt, params, timeout=timeout + 30)
             elif shard_ids:
-                pipe = st.shard_pipeline(name, [int(s) for s in shard_ids])
-                with st.lock:
-                    out = pipe.generate([prompt], params)[0]
+                svc = st.shard_pipeline(name, [int(s) for s in shard_ids])
+                out = svc.generate(prompt, params, timeout=timeout + 30)
             else:
                 if name not in st.services:
                     try:

@@ -91,8 +91,8 @@ class EngineService:
 
 
 class PipelineService:
-    """Same interface, backed by the rank-0 head of a DistributedPipelineEngine: requests
-    are batched into ring sessions.
+    """Same interface, backed by the rank-0 head of a DistributedPipelineEngine: a ring
+    session runs while there is work, and requests join it at tick boundaries.
 
     A session that raises (a stage died, a link failed, the data-plane timeout fired) leaves
     the ring unusable: every pending and later request fails at once with that error, and
@@ -107,6 +107,8 @@ class PipelineService:
         self._ids = 0
         self._lock = threading.Lock()
         self.error: Optional[BaseException] = None
+        self._futs = {}
+        self.sessions = 0
         self._t = threading.Thread(target=self._run, name=f"dli-pipe-{name}", daemon=True)
         self._t.start()
 
@@ -132,38 +134,48 @@ class PipelineService:
     def generate(self, prompt, params=None, timeout=None):
         return self.submit(prompt, params).result(timeout=timeout)
 
+    def _admit(self) -> int:
+        """Tick boundary: move every queued request into the running head scheduler."""
+        n = 0
+        while True:
+            try:
+                rid, prompt, params, fut = self._inbox.get_nowait()
+            except queue.Empty:
+                return n
+            try:
+                self.engine.add_request(prompt, params, request_id=rid)
+                self._futs[rid] = fut
+                n += 1
+            except Exception as e:  # noqa: BLE001
+                fut.set_exception(e)
+
+    def _resolve(self, outs) -> None:
+        for o in outs:
+            f = self._futs.pop(o.request_id, None)
+            if f is not None and not f.done():
+                f.set_result(o)
+
     def _run(self):
         head = self.engine.head
         while not self._stop.is_set():
             try:
-                first = self._inbox.get(timeout=0.05)
+                item = self._inbox.get(timeout=0.05)
             except queue.Empty:
                 continue
-            batch = [first]
-            while True:
-                try:
-                    batch.append(self._inbox.get_nowait())
-                except queue.Empty:
-                    break
-            futs = {}
-            for rid, prompt, params, fut in batch:
-                try:
-                    self.engine.add_request(prompt, params, request_id=rid)
-                    futs[rid] = fut
-                except Exception as e:  # noqa: BLE001
-                    fut.set_exception(e)
+            self._inbox.put(item)            # admitted by the session's first tick
             try:
-                outs = head.run_session()
+                # continuous admission: requests that arrive while the ring is running join
+                # it at the next tick; each finished request is answered the tick it finishes
+                head.run_session(admit=self._admit, on_finished=self._resolve)
+                self.sessions += 1
             except BaseException as e:  # noqa: BLE001 — the ring is broken: fail fast, for good
                 self.error = e
-                for f in futs.values():
-                    f.set_exception(e)
+                for f in self._futs.values():
+                    if not f.done():
+                        f.set_exception(e)
+                self._futs.clear()
                 self._fail_pending()
                 return
-            for o in outs:
-                f = futs.pop(o.request_id, None)
-                if f is not None:
-                    f.set_result(o)
 
     def stats(self) -> dict:
         s = self.engine.head.stats.snapshot()

@@ -1,0 +1,211 @@
+"""Serving the sharded pipeline (CPU, gloo):
+
+* an 8-rank ring serves the per-stage files the ``shard-model`` CLI wrote (each rank
+  streams ``shard_<rank>/model.safetensors`` through the C++ loader; with the vocab-parallel
+  head every rank reads its row slice of the LM head from the last shard), token-identical
+  to the single-stage engine (reference: shard_model.py:94-109 -> worker/app.py:139-206 ->
+  master/dashboard/views.py:318-355, which never actually ran more than shard 0);
+* continuous admission: requests submitted while a ring session is running join it at the
+  next tick and finish before the first session's stragglers (one session in total);
+* the worker's ``shard_ids`` path batches concurrent requests (shared decode steps);
+* ``/load_model`` reads weights from MODEL_CACHE_DIR (reference worker/app.py:117-124).
+"""
+import os
+import socket
+import threading
+import time
+
+import torch
+import torch.multiprocessing as mp
+
+from distributed_llm_inferencing_amd.engine import SamplingParams
+from distributed_llm_inferencing_amd.engine.llm_engine import LLMEngine
+
+PROMPTS = [[5, 6, 7, 8], [9, 10, 11], [1, 2, 3, 4, 5, 6, 7], [100, 200], [7] * 9, [3, 4]]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _spawn(target, world, *args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q, *args)) for r in range(world)]
+    for p in procs:
+        p.start()
+    return q, procs
+
+
+def _join(procs):
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+
+
+# ----------------------------------------------------------------------------- shard files
+def _shard_worker(rank, world, port, q, shard_root):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), DLI_PP_VOCAB_PARALLEL="auto")
+    torch.set_num_threads(1)
+    import torch.distributed as dist
+    from distributed_llm_inferencing_amd.parallel.pipeline import DistributedPipelineEngine
+    eng = DistributedPipelineEngine("ignored", "cpu", max_batch=8, max_model_len=64,
+                                    num_blocks=256, dtype=torch.float32, shard_dir=shard_root)
+    if rank == 0:
+        sp = SamplingParams(max_length=20, do_sample=False, ignore_eos=True)
+        sp2 = SamplingParams(max_length=20, seed=3, ignore_eos=True)
+        res = ([o.all_ids for o in eng.generate(PROMPTS, sp)],
+               [o.all_ids for o in eng.generate(PROMPTS, sp2)],
+               eng.vocab_parallel, [(p.start_layer, p.end_layer) for p in eng.plans],
+               eng.channel.ctrl_kind)
+        eng.shutdown()
+        q.put(res)
+    else:
+        eng.serve()
+    dist.barrier()
+    eng.channel.close()
+    dist.destroy_process_group()
+
+
+def test_gloo_ring_serves_shard_files(tmp_path):
+    from distributed_llm_inferencing_amd.shard.writer import export_shards, model_dir
+    export_shards("llama-tiny8", 8, str(tmp_path), dtype=torch.float32, log=lambda *a: None)
+    root = str(model_dir(str(tmp_path), "llama-tiny8"))
+    q, procs = _spawn(_shard_worker, 8, root)
+    greedy, sampled, vp, plans, ctrl = q.get(timeout=300)
+    _join(procs)
+    assert vp and ctrl == "shm"
+    assert plans == [(i, i + 1) for i in range(8)]          # the files' partition, not ours
+    ref = LLMEngine("llama-tiny8", device="cpu", dtype=torch.float32, max_batch=8,
+                    max_model_len=64, num_blocks=64)
+    assert greedy == [o.all_ids for o in ref.generate(
+        PROMPTS, SamplingParams(max_length=20, do_sample=False, ignore_eos=True))]
+    assert sampled == [o.all_ids for o in ref.generate(
+        PROMPTS, SamplingParams(max_length=20, seed=3, ignore_eos=True))]
+
+
+# ----------------------------------------------------------------------------- admission
+def _admit_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    import torch.distributed as dist
+    from distributed_llm_inferencing_amd.parallel.pipeline import DistributedPipelineEngine
+    from distributed_llm_inferencing_amd.worker.service import PipelineService
+    eng = DistributedPipelineEngine("llama-tiny", "cpu", max_batch=8, max_model_len=128,
+                                    num_blocks=256, dtype=torch.float32)
+    if rank != 0:
+        eng.serve()
+    else:
+        svc = PipelineService(eng, name="pp")
+        long_sp = SamplingParams(max_length=90, do_sample=False, ignore_eos=True)
+        short_sp = SamplingParams(max_length=12, do_sample=False, ignore_eos=True)
+        done = {}
+
+        def track(key, fut):
+            fut.add_done_callback(lambda f: done.setdefault(key, (time.perf_counter(),
+                                                                  f.result())))
+        for i, p in enumerate(PROMPTS[:4]):
+            track(("long", i), svc.submit(p, long_sp))
+        while eng.head.stats.decode_steps < 10:           # the session is running
+            time.sleep(0.005)
+        for i, p in enumerate(PROMPTS[4:]):
+            track(("short", i), svc.submit(p, short_sp))
+        while len(done) < 6:
+            time.sleep(0.01)
+        while svc.sessions < 1:
+            time.sleep(0.01)
+        time.sleep(0.2)
+        res = {k: (t, o.all_ids) for k, (t, o) in done.items()}
+        q.put((res, svc.sessions))
+        svc.close()
+        eng.shutdown()
+    dist.barrier()
+    eng.channel.close()
+    dist.destroy_process_group()
+
+
+def test_pipeline_service_admits_requests_into_running_session():
+    q, procs = _spawn(_admit_worker, 2)
+    res, sessions = q.get(timeout=300)
+    _join(procs)
+    assert sessions == 1                                   # the late requests joined it
+    last_long = max(t for (kind, _), (t, _) in res.items() if kind == "long")
+    assert all(t < last_long for (kind, _), (t, _) in res.items() if kind == "short")
+    ref = LLMEngine("llama-tiny", device="cpu", dtype=torch.float32, max_batch=8,
+                    max_model_len=128, num_blocks=128)
+    longs = [o.all_ids for o in ref.generate(PROMPTS[:4], SamplingParams(
+        max_length=90, do_sample=False, ignore_eos=True))]
+    shorts = [o.all_ids for o in ref.generate(PROMPTS[4:], SamplingParams(
+        max_length=12, do_sample=False, ignore_eos=True))]
+    assert [res[("long", i)][1] for i in range(4)] == longs
+    assert [res[("short", i)][1] for i in range(2)] == shorts
+
+
+# ----------------------------------------------------------------------------- worker paths
+def _settings(tmp_path):
+    from distributed_llm_inferencing_amd.config import Settings
+    s = Settings()
+    s.master_db = str(tmp_path / "db.sqlite3")
+    s.model_cache_dir = str(tmp_path / "cache")
+    return s
+
+
+SMALL = dict(max_batch=8, max_model_len=128, num_blocks=256)
+
+
+def test_worker_sharded_requests_share_decode_steps(tmp_path):
+    from distributed_llm_inferencing_amd.shard.writer import export_shards
+    from distributed_llm_inferencing_amd.worker.server import create_worker_app
+    app = create_worker_app(_settings(tmp_path), device="cpu", engine_kwargs=SMALL)
+    c = app.test_client()
+    paths = export_shards("llama-tiny", 2, str(tmp_path / "shards"), log=lambda *a: None)
+    for i, p in enumerate(paths):
+        assert c.post("/load_shard", json={"model_name": "llama-tiny", "shard_id": i,
+                                           "shard_path": str(p)}).status_code == 200
+    out = [None] * 6
+
+    def call(i):
+        out[i] = c.post("/inference", json={"model_name": "llama-tiny", "prompt": f"req {i}",
+                                            "max_length": 30, "shard_ids": [0, 1],
+                                            "temperature": 0})
+    ts = [threading.Thread(target=call, args=(i,)) for i in range(6)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    assert all(r.status_code == 200 for r in out), [r.get_json() for r in out]
+    svc = app.extensions["dli_worker"].shard_pipes[("llama-tiny", (0, 1))]
+    st = svc.engine.stats
+    assert st.finished == 6
+    # 6 requests x ~24 new tokens each: serialized would be ~6 x 24 decode steps
+    assert st.decode_steps < 3 * 24, st.decode_steps
+    single = c.post("/inference", json={"model_name": "llama-tiny", "prompt": "req 0",
+                                        "max_length": 30, "temperature": 0}).get_json()
+    assert out[0].get_json()["result"] == single["result"]
+
+
+def test_load_model_reads_model_cache(tmp_path):
+    from distributed_llm_inferencing_amd.shard.writer import export_shards
+    from distributed_llm_inferencing_amd.worker.server import create_worker_app
+    s = _settings(tmp_path)
+    # a cache entry with weights that differ from the random init (seed 7)
+    export_shards("llama-tiny", 2, s.model_cache_dir, seed=7, dtype=torch.float32,
+                  log=lambda *a: None)
+    app = create_worker_app(s, device="cpu", engine_kwargs=SMALL)
+    c = app.test_client()
+    assert c.post("/load_model", json={"model_name": "llama-tiny"}).status_code == 200
+    st = app.extensions["dli_worker"]
+    assert st.weights_source["llama-tiny"] == "cache"
+    body = {"model_name": "llama-tiny", "prompt": "abc", "max_length": 16, "temperature": 0}
+    got = c.post("/inference", json=body).get_json()["result"]
+    ref = LLMEngine("llama-tiny", device="cpu", dtype=torch.float32, seed=7, max_batch=8,
+                    max_model_len=128, num_blocks=64)
+    want = ref.generate(["abc"], SamplingParams(max_length=16, temperature=0))[0]
+    assert got == want.resolve_text()
+    rnd = LLMEngine("llama-tiny", device="cpu", dtype=torch.float32, seed=0, max_batch=8,
+                    max_model_len=128, num_blocks=64)
+    assert rnd.generate(["abc"], SamplingParams(max_length=16, temperature=0))[0].all_ids \
+        != want.all_ids                                   # really not the default init
