@@ -6,37 +6,50 @@
 // The expert MLPs themselves run as grouped GEMMs (gemm.hip, grid.z = expert).
 #include "common.h"
 
-__global__ void moe_route_kernel(float* __restrict__ topk_w, int* __restrict__ topk_ids,
-                                 const u16* __restrict__ logits, int T, int E, int k) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= T) return;
-  float p[64];
-  float mx = -INFINITY;
-  for (int e = 0; e < E; ++e) { p[e] = bf2f(logits[(long)t * E + e]); mx = fmaxf(mx, p[e]); }
-  float s = 0.f;
-  for (int e = 0; e < E; ++e) { p[e] = __expf(p[e] - mx); s += p[e]; }
-  float wsum = 0.f;
+// One wave per token, lane e holds expert e (E <= 64): softmax max / sum and each of the k
+// argmax rounds are wave-wide shuffle reductions, so no per-thread logits array (the former
+// float p[64] per thread spilled to scratch).
+__global__ void __launch_bounds__(256) moe_route_kernel(float* __restrict__ topk_w,
+                                                        int* __restrict__ topk_ids,
+                                                        const u16* __restrict__ logits, int T,
+                                                        int E, int k) {
+  const int lane = threadIdx.x & 63;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= T) return;                                  // wave-uniform
+  const float x = lane < E ? bf2f(logits[(long)t * E + lane]) : -INFINITY;
+  const float mx = wave_max(x);
+  float p = lane < E ? __expf(x - mx) : 0.f;
+  const float s = wave_sum(p);
+  float mine = 0.f, wsum = 0.f;                        // lane j keeps the j-th pick's weight
   for (int j = 0; j < k; ++j) {
-    int best = 0; float bv = -1.f;
-    for (int e = 0; e < E; ++e) if (p[e] > bv) { bv = p[e]; best = e; }
-    topk_ids[t * k + j] = best;
-    topk_w[t * k + j] = bv / s;
-    wsum += bv / s;
-    p[best] = -2.f;
+    float bv = lane < E ? p : -3.f;
+    int bi = lane;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {                 // argmax, lowest index on ties (HF)
+      const float ov = __shfl_xor(bv, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+    }
+    const float w = bv / s;
+    wsum += w;
+    if (lane == j) { mine = w; topk_ids[t * k + j] = bi; }
+    if (lane == bi) p = -2.f;                          // taken
   }
-  for (int j = 0; j < k; ++j) topk_w[t * k + j] /= wsum;
+  if (lane < k) topk_w[t * k + lane] = mine / wsum;
 }
 
 extern "C" int dli_moe_route(float* topk_w, int* topk_ids, const void* logits, int T, int E, int k,
                              hipStream_t st) {
   if (T <= 0) return 0;
   if (E > 64 || k > E) return (int)hipErrorInvalidValue;
-  moe_route_kernel<<<(T + 255) / 256, 256, 0, st>>>(topk_w, topk_ids, (const u16*)logits, T, E, k);
+  moe_route_kernel<<<(T + 3) / 4, 256, 0, st>>>(topk_w, topk_ids, (const u16*)logits, T, E, k);
   DLI_RETURN_LAUNCH();
 }
 
-// Single workgroup. ids: [n] expert ids (n = T*k); experts outside [e0, e0+E_local) are dropped
-// (pos = -1). offsets: [E_local + 1]; pos: [n]; src: [n] (token of each permuted row).
+// Single workgroup of 1024 threads (n = T*k routed slots: counting and placement are
+// block-strided, LDS atomics; the expert-offset scan is one wave's shuffle scan). ids: [n]
+// expert ids; experts outside [e0, e0+E_local) are dropped (pos = -1). offsets:
+// [E_local + 1]; pos: [n]; src: [n] (token of each permuted row).
 __global__ void __launch_bounds__(1024) moe_align_kernel(int* __restrict__ offsets,
                                                          int* __restrict__ pos,
                                                          int* __restrict__ src,
@@ -51,11 +64,27 @@ __global__ void __launch_bounds__(1024) moe_align_kernel(int* __restrict__ offse
     if (e >= 0 && e < E_local) atomicAdd(&cnt[e], 1);
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < 64) {                              // exclusive scan by the first wave
+    const int lane = threadIdx.x;
     int run = 0;
-    for (int e = 0; e < E_local; ++e) { off[e] = run; run += cnt[e]; cnt[e] = 0; }
-    off[E_local] = run;
-    for (int e = 0; e <= E_local; ++e) offsets[e] = off[e];
+    for (int base = 0; base < E_local; base += 64) {
+      const int e = base + lane;
+      const int c = e < E_local ? cnt[e] : 0;
+      int incl = c;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+      }
+      if (e < E_local) off[e] = run + incl - c;
+      run += __shfl(incl, 63, 64);
+    }
+    if (lane == 0) off[E_local] = run;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e <= E_local; e += blockDim.x) {
+    offsets[e] = off[e];
+    if (e < E_local) cnt[e] = 0;
   }
   __syncthreads();
   for (int i = threadIdx.x; i < n; i += blockDim.x) {

@@ -367,3 +367,74 @@ extern "C" int dli_sample(int* out_tokens, const float* logits, long row_stride,
                                            top_p, seeds);
   DLI_RETURN_LAUNCH();
 }
+
+// ---------------------------------------------------------------------------------------
+// Per-row top-c of fp32 logits (the vocab-parallel LM head's candidates,
+// parallel/pipeline.py): one 512-thread workgroup per row.
+//   1. radix select over the row in global memory (4 passes of 8-bit digits on order-
+//      preserving keys): tau = key of the c-th largest element, n_gt = count above tau;
+//   2. ordered compaction: thread t owns a contiguous slice of the row, so a block scan of
+//      per-thread counts writes the winners (every key > tau, then the first c - n_gt keys
+//      == tau in index order) already in ascending index order — the order the candidate
+//      merge on rank 0 requires (ranks concatenate ascending vocab slices).
+// Replaces torch.topk + torch.sort + gather on the pipeline's hot path.
+__global__ void __launch_bounds__(SMP_THREADS) topk_rows_kernel(
+    float* __restrict__ out_v, int* __restrict__ out_i, const float* __restrict__ x,
+    long row_stride, int V, int c, int id_offset) {
+  __shared__ uint32_t hist[256];
+  __shared__ float sv[16];
+  __shared__ uint32_t s_sel[3];
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const float* xr = x + (long)row * row_stride;
+  uint32_t prefix = 0, pmask = 0, k_rem = (uint32_t)c;
+  for (int pass = 0; pass < 4; ++pass) {
+    const int shift = 24 - 8 * pass;
+    for (int i = tid; i < 256; i += blockDim.x) hist[i] = 0;
+    __syncthreads();
+    row_scan(xr, V, [&](float v, int) {
+      const uint32_t k = f2key(v);
+      if ((k & pmask) == prefix) atomicAdd(&hist[(k >> shift) & 255u], 1u);
+    });
+    __syncthreads();
+    find_digit(hist, k_rem, sv, s_sel);
+    __syncthreads();
+    k_rem -= s_sel[1];
+    prefix |= s_sel[0] << shift;
+    pmask |= 255u << shift;
+    __syncthreads();
+  }
+  const uint32_t tau = prefix;                 // c-th largest key; k_rem of its ties are taken
+  // ---- ordered compaction over contiguous per-thread slices
+  const int per = (V + SMP_THREADS - 1) / SMP_THREADS;
+  const int lo = min(V, tid * per), hi = min(V, lo + per);
+  uint32_t n_gt = 0, n_eq = 0;
+  for (int e = lo; e < hi; ++e) {
+    const uint32_t k = f2key(xr[e]);
+    n_gt += k > tau;
+    n_eq += k == tau;
+  }
+  const float gt_incl = block_scan((float)n_gt, sv);        // exact: counts < 2^24
+  __syncthreads();
+  const float eq_incl = block_scan((float)n_eq, sv);
+  uint32_t eq_before = (uint32_t)eq_incl - n_eq;            // ties in earlier slices
+  uint32_t before = (uint32_t)gt_incl - n_gt + min(eq_before, k_rem);
+  for (int e = lo; e < hi && before < (uint32_t)c; ++e) {
+    const float v = xr[e];
+    const uint32_t k = f2key(v);
+    bool take = k > tau;
+    if (k == tau) { take = eq_before < k_rem; ++eq_before; }
+    if (take) {
+      out_v[(long)row * c + before] = v;
+      out_i[(long)row * c + before] = e + id_offset;
+      ++before;
+    }
+  }
+}
+
+extern "C" int dli_topk_rows(float* out_v, int* out_i, const float* x, long row_stride, int rows,
+                             int V, int c, int id_offset, hipStream_t st) {
+  if (rows <= 0) return 0;
+  if (c < 1 || c > V || V > (1 << 24)) return (int)hipErrorInvalidValue;
+  topk_rows_kernel<<<rows, SMP_THREADS, 0, st>>>(out_v, out_i, x, row_stride, V, c, id_offset);
+  DLI_RETURN_LAUNCH();
+}

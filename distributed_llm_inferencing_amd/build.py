@@ -5,9 +5,15 @@ repo snapshot; they are git-ignored):
 
 * ``lib/libdli_kernels.so`` — every HIP/CDNA4 kernel in ``csrc/kernels`` behind a plain
   ``extern "C"`` ABI (called through ctypes with torch's current HIP stream).
-* ``lib/libdli_runtime.so`` — the host-side C++ runtime in ``csrc/runtime`` (paged-KV
-  block allocator, continuous-batching scheduler core, safetensors weight loader with
-  pinned staging + hipMemcpyAsync, byte tokenizer).
+* ``lib/libdli_runtime.so`` — the host-side C++ runtime in ``csrc/runtime``: paged-KV block
+  allocator + batched block-table / slot builders (``block_manager.cpp``), the decode fast
+  path of the continuous-batching scheduler (``decode_core.cpp``), the safetensors weight
+  loader with pinned staging + hipMemcpyAsync (``safetensors_loader.cpp``) and the
+  pipeline's shared-memory control ring (``shm_ring.cpp``).
+
+Each library is stamped with a digest of its sources + flags (``<lib>.sha1``); the loaders
+(``ops/_native.py``, ``runtime/__init__.py``) rebuild a library whose stamp does not match
+the tree, or refuse to load it when no toolchain is present — never a stale binary.
 
 Both link ``libamdhip64.so.7``; at run time the copy torch already loaded is reused
 (same SONAME), so kernels launched here and torch's own kernels share one HIP runtime.
@@ -83,14 +89,40 @@ def _link(objs, out: Path, extra=()):
     os.replace(tmp, out)
 
 
-def _build_group(srcs, headers, flags, out: Path, jobs: int, extra=()):
+def _group_sources(kind: str):
+    if kind == "kernels":
+        return (sorted((CSRC / "kernels").glob("*.hip")), sorted((CSRC / "kernels").glob("*.h")),
+                KERNEL_FLAGS)
+    return (sorted((CSRC / "runtime").glob("*.cpp")), sorted((CSRC / "runtime").glob("*.h")),
+            RUNTIME_FLAGS)
+
+
+def source_digest(kind: str) -> str:
+    """Digest of one library's sources + headers + flags (``kernels`` or ``runtime``)."""
+    srcs, hdrs, flags = _group_sources(kind)
+    return _digest([*srcs, *hdrs], flags)
+
+
+def stamp_path(lib: Path) -> Path:
+    return lib.with_name(lib.name + ".sha1")
+
+
+def is_current(kind: str, lib: Path) -> bool:
+    st = stamp_path(lib)
+    return lib.exists() and st.exists() and st.read_text().strip() == source_digest(kind)
+
+
+def _build_group(srcs, headers, flags, out: Path, jobs: int, extra=(), kind=None):
     objs_dir = OBJDIR / out.stem
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         futs = [ex.submit(_compile, s, objs_dir / (s.stem + ".o"), flags, headers) for s in srcs]
         objs = [f.result() for f in futs]
     newest = max(o.stat().st_mtime for o in objs)
-    if not out.exists() or out.stat().st_mtime < newest:
+    if kind is not None and not is_current(kind, out) or not out.exists() \
+            or out.stat().st_mtime < newest:
         _link(objs, out, extra)
+    if kind is not None:
+        stamp_path(out).write_text(source_digest(kind))
     return out
 
 
@@ -98,15 +130,14 @@ def build(force: bool = False, jobs: int = 0, verbose: bool = True) -> dict:
     jobs = jobs or min(8, os.cpu_count() or 4)
     if force and OBJDIR.exists():
         shutil.rmtree(OBJDIR)
-    k_srcs = sorted((CSRC / "kernels").glob("*.hip"))
-    k_hdrs = sorted((CSRC / "kernels").glob("*.h"))
-    r_srcs = sorted((CSRC / "runtime").glob("*.cpp"))
-    r_hdrs = sorted((CSRC / "runtime").glob("*.h"))
+    k_srcs, k_hdrs, _ = _group_sources("kernels")
+    r_srcs, r_hdrs, _ = _group_sources("runtime")
     out = {}
-    out["kernels"] = _build_group(k_srcs, k_hdrs, KERNEL_FLAGS, LIBDIR / "libdli_kernels.so", jobs)
+    out["kernels"] = _build_group(k_srcs, k_hdrs, KERNEL_FLAGS, LIBDIR / "libdli_kernels.so", jobs,
+                                  kind="kernels")
     if r_srcs:
         out["runtime"] = _build_group(r_srcs, r_hdrs, RUNTIME_FLAGS, LIBDIR / "libdli_runtime.so",
-                                      jobs, extra=("-lpthread",))
+                                      jobs, extra=("-lpthread",), kind="runtime")
     if verbose:
         for k, v in out.items():
             print(f"[dli.build] {k}: {v} ({v.stat().st_size // 1024} KiB)")

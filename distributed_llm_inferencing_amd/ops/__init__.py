@@ -344,12 +344,17 @@ def head_candidates(h, w_slice, offset: int, c: int):
     token a top-k <= c sampler can pick."""
     if not _use_native(h):
         v, i = R.head_candidates(h, w_slice, offset, c)
-    else:
-        lg = linear(h, w_slice, epi="f32")
-        v, i = torch.topk(lg, min(c, lg.shape[1]), dim=-1)
-        i = (i + offset).to(torch.int32)
-    i, perm = torch.sort(i, dim=-1)
-    return v.gather(1, perm), i
+        i, perm = torch.sort(i, dim=-1)
+        return v.gather(1, perm), i
+    lg = linear(h, w_slice, epi="f32")
+    S, V = lg.shape
+    c = min(c, V)
+    v = torch.empty(S, c, dtype=torch.float32, device=h.device)
+    i = torch.empty(S, c, dtype=torch.int32, device=h.device)
+    # HIP top-c per row, written in ascending id order (sampling.hip topk_rows_kernel)
+    _native_call("dli_topk_rows", _p(v), _p(i), _p(lg), lg.stride(0), S, V, c, int(offset),
+                 _st())
+    return v, i
 
 
 # ----------------------------------------------------------------------------- MoE

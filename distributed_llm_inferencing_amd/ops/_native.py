@@ -42,6 +42,7 @@ _SIGS = {
     "dli_decode_attention_workspace_bytes": [I, I, I, I],
     "dli_prefill_attention": [P, I, P, I, P, I, I, I, I, I, F, P],
     "dli_sample": [P, P, L, I, I, P, P, P, P, P],
+    "dli_topk_rows": [P, P, P, L, I, I, I, I, P],
     "dli_gemm": [P, I, P, I, P, I, I, I, I, I, I, I, P, P, P, I, P],
     "dli_splitk_add_rmsnorm": [P, P, P, I, I, I, P, F, P],
     "dli_splitk_rope_cache": [P, P, I, I, I, P, P, P, P, P, I, I, I, I, I, P],
@@ -52,16 +53,32 @@ _SIGS = {
 }
 
 
+def ensure_current(lib_path: Path, kind: str) -> None:
+    """Build a missing library, rebuild a stale one (its source-digest stamp does not match
+    the tree), and refuse a stale one when no toolchain can rebuild it."""
+    from .. import build as _build
+    if _build.is_current(kind, lib_path):
+        return
+    try:
+        _build._hipcc()
+    except RuntimeError:
+        if lib_path.exists():
+            raise RuntimeError(f"{lib_path} is stale (sources changed since it was built; "
+                               f"stamp {_build.stamp_path(lib_path).name}) and hipcc is not "
+                               "available to rebuild it")
+        raise
+    _build.build(verbose=False)
+    if not _build.is_current(kind, lib_path):
+        raise RuntimeError(f"{lib_path} still does not match its sources after a rebuild")
+
+
 def _load():
     global _lib, _load_error
     with _lock:
         if _lib is not None or _load_error is not None:
             return _lib
         try:
-            if not LIB_PATH.exists():
-                # build in place when a toolchain is present (CPU containers, fresh boxes)
-                from .. import build as _build
-                _build.build(verbose=False)
+            ensure_current(LIB_PATH, "kernels")
             lib = ctypes.CDLL(str(LIB_PATH))
             for name, args in _SIGS.items():
                 fn = getattr(lib, name)

@@ -76,9 +76,8 @@ def lib():
         return _lib
     with _lock:
         if _lib is None:
-            if not LIB_PATH.exists():
-                from .. import build as _build
-                _build.build(verbose=False)
+            from ..ops._native import ensure_current
+            ensure_current(LIB_PATH, "runtime")
             L = ctypes.CDLL(str(LIB_PATH))
             for name, (args, res) in _SIGS.items():
                 fn = getattr(L, name)

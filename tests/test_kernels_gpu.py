@@ -391,3 +391,60 @@ def test_feed_ids(gpu):
     ref = torch.where(src >= 0, feed[src.clamp(min=0).long()], ids)
     ops.feed_ids(ids, src, feed)
     assert torch.equal(ids, ref)
+
+
+@pytest.mark.parametrize("T,E,k", [(5, 64, 2), (129, 16, 4), (64, 8, 8)])
+def test_moe_route_wide(gpu, T, E, k):
+    """Wave-per-token router at the E <= 64 limit, k up to E (HF: lowest index on ties)."""
+    torch.manual_seed(9)
+    rl = rnd(T, E, dev=gpu)
+    rl[0] = 0                                   # all-tie row: experts 0..k-1, weights 1/k
+    w, ids = ops.moe_route(rl, k)
+    rw, rids = R.router_topk(rl, k)
+    assert torch.equal(ids[1:].long().sort(-1).values, rids[1:].long().sort(-1).values)
+    assert ids[0].tolist() == list(range(k))
+    close(w.sort(-1).values, rw.sort(-1).values, rtol=1e-3, atol=1e-3)
+    assert torch.allclose(w.sum(-1), torch.ones(T, device=gpu), atol=1e-5)
+
+
+@pytest.mark.parametrize("S,V,c", [(37, 16032, 64), (5, 4008, 64), (3, 64, 64), (9, 50257, 50)])
+def test_topk_rows_kernel(gpu, S, V, c):
+    """HIP per-row top-c (vocab-parallel head candidates) vs torch.topk: same value multiset,
+    ids ascending and offset, every value above the c-th largest present, ties broken to the
+    lowest index; exercised on continuous and heavily tied rows."""
+    from distributed_llm_inferencing_amd.ops import _native
+    torch.manual_seed(3)
+    off = 1000
+    for tied in (False, True):
+        x = torch.randn(S, V, device=gpu)
+        if tied:
+            x = (x * 2).round() / 2                 # few distinct values: many ties at the cut
+        v = torch.empty(S, c, device=gpu)
+        i = torch.empty(S, c, dtype=torch.int32, device=gpu)
+        _native.call("dli_topk_rows", v.data_ptr(), i.data_ptr(), x.data_ptr(), x.stride(0), S,
+                     V, c, off, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        ref = torch.topk(x, c, dim=-1).values
+        assert torch.equal(v.sort(-1, descending=True).values, ref)
+        assert bool((i[:, 1:] > i[:, :-1]).all())                  # ascending ids
+        loc = (i - off).long()
+        assert torch.equal(x.gather(1, loc), v)                     # ids point at values
+        kth = ref[:, -1:]
+        assert torch.equal((x > kth).sum(-1), (v > kth).sum(-1))    # all strictly larger
+        for r in range(S):                                          # ties: lowest indices
+            eq = (x[r] == kth[r]).nonzero().flatten()
+            need = int((v[r] == kth[r]).sum())
+            assert torch.equal(loc[r][v[r] == kth[r]], eq[:need])
+
+
+def test_head_candidates_native_matches_reference(gpu):
+    torch.manual_seed(4)
+    h = rnd(19, 256, dev=gpu)
+    w = rnd(3000, 256, dev=gpu, scale=0.1)
+    v, i = ops.head_candidates(h, w, 5000, 64)
+    lg = ops.linear(h, w, epi="f32")                   # same logits the op ranks
+    rv, ri = torch.topk(lg, 64, dim=-1)
+    ri, perm = torch.sort((ri + 5000).to(torch.int32), dim=-1)
+    assert torch.equal(i, ri)
+    assert torch.equal(v, rv.gather(1, perm))
+    close(v, R.linear(h, w, out_dtype=torch.float32).gather(1, (i - 5000).long()))
