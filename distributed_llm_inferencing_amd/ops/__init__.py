@@ -20,7 +20,7 @@ _native_call = N.call
 _p = N.ptr
 _FUSED_OFF = __import__("os").environ.get("DLI_NO_FUSED_REDUCE", "0") == "1"   # A/B switch
 # rows per expert from which eager (prefill) MoE GEMMs go to hipBLASLt per expert
-_MOE_BLAS_ROWS = int(__import__("os").environ.get("DLI_MOE_BLAS_ROWS", "1024"))
+_MOE_PREFILL_ROWS = int(__import__("os").environ.get("DLI_MOE_PREFILL_ROWS", "1024"))
 
 
 def _use_native(t: torch.Tensor) -> bool:
@@ -387,18 +387,21 @@ def moe_mlp(x, w_gu, w_down, topk_w, topk_ids, expert_offset: int = 0):
     xp = torch.empty(max(n, 1), D, dtype=x.dtype, device=dev)
     _native_call("dli_moe_gather", _p(xp), _p(x), _p(src), n, D, _p(offsets[E_local:]), _st())
     act = torch.empty(max(n, 1), F2 // 2, dtype=x.dtype, device=dev)
-    if n >= _MOE_BLAS_ROWS * E_local and not torch.cuda.is_current_stream_capturing():
-        # prefill-sized expert GEMMs (thousands of rows per expert) are compute-bound:
-        # hipBLASLt per expert beats our grouped 256x128 tile (0.73 PF) by ~1.5x; needs the
-        # expert offsets on the host (one sync per MoE layer, eager prefill only)
+    if n >= _MOE_PREFILL_ROWS * E_local and not torch.cuda.is_current_stream_capturing():
+        # prefill-sized expert GEMMs (thousands of rows per expert) are compute-bound: the
+        # grouped 8-phase 256x256 kernel (tile 22, grid.z = expert) with the fused SiLU*up
+        # epilogue. The largest expert's row count bounds the grid (one host read of the
+        # offsets per MoE layer, eager prefill only) instead of n, which would launch ~8x
+        # more (empty) row tiles per expert.
         offs = offsets.tolist()
+        rows_max = max(b - a for a, b in zip(offs[:-1], offs[1:]))
         y = torch.empty(max(n, 1), D, dtype=x.dtype, device=dev)
-        for e in range(E_local):
-            a, b = offs[e], offs[e + 1]
-            if b > a:
-                g = torch.matmul(xp[a:b], w_gu[e].t())
-                _native_call("dli_silu_mul", _p(act[a:b]), _p(g), b - a, F2 // 2, _st())
-                torch.matmul(act[a:b], w_down[e].t(), out=y[a:b])
+        if rows_max > 0:
+            p8 = G.GemmPlan("dli", 22, 1)
+            _gemm_native(xp, w_gu, "silu_mul", out=act, groups=E_local, group_off=offsets,
+                         rows_per_group=rows_max, plan=p8)
+            _gemm_native(act, w_down, "none", out=y, groups=E_local, group_off=offsets,
+                         rows_per_group=rows_max, plan=p8)
         out = torch.empty_like(x)
         _native_call("dli_moe_combine", _p(out), _p(y), _p(topk_w), _p(pos), T, k, D, _st())
         return out

@@ -6,10 +6,10 @@ The projection GEMMs of a decode step are skinny (M = batch) and of a prefill st
 * a tile from {64x64, 64x128, 128x128, 128x256, 256x128} sized to M,
 * a split-K factor so the grid covers the 256 CUs (cdna_hip_programming.md §5 'Projection
   GEMM at M = 256': choose SPLITK so that tiles * SPLITK ~ 0.5-1x the CU count),
-* the backend. Fused epilogues (SiLU*mul, bias+GELU, fp32 logits) always run on our kernel.
-  Plain bf16 GEMMs may run on hipBLASLt (torch.matmul) if the autotuner measured it
-  faster on this shape (autotune at graph capture, on by default; ``DLI_GEMM_AUTOTUNE=0``
-  disables it), or if forced with ``DLI_GEMM_BACKEND``.
+* the backend: always our MFMA kernels (decode tiles autotuned at graph capture, on by
+  default; ``DLI_GEMM_AUTOTUNE=0`` disables it; prefill on the 8-phase 256x256 kernel).
+  hipBLASLt (torch.matmul) remains reachable only as an explicit ablation
+  (``DLI_GEMM_BACKEND=hipblaslt``, ``DLI_GEMM_PREFILL_BLAS=1``, ``DLI_GEMM_DECODE_BLAS=1``).
 
 Split-K partial slabs live in a grow-only per-device workspace; engines warm every shape
 up before hipGraph capture so no allocation happens inside a capture.
@@ -83,12 +83,17 @@ LARGE_M = int(os.environ.get("DLI_GEMM_LARGE_M", "1024"))
 
 
 def _heuristic(M: int, N: int, K: int, epi: str) -> GemmPlan:
-    """Fitted to profiles/r1_gemm/gemm_bench.json (MI355X, random bf16 operands):
-    skinny decode GEMMs (M <= 512) run on our kernel, 1.1-1.9x faster than hipBLASLt there;
-    fat prefill GEMMs (M >= LARGE_M) on hipBLASLt, which is 1.6-1.9x faster than our 128^2
-    2-stage structure at M >= 2048 (fused epilogues then run as a separate pass)."""
-    if M >= LARGE_M and os.environ.get("DLI_GEMM_NO_BLAS", "0") != "1":
-        return GemmPlan("hipblaslt", 2, 1)
+    """Fitted to profiles/r1_gemm/gemm_bench.json and profiles/r1_gemm8p/ (MI355X, random
+    bf16 operands): skinny decode GEMMs (M <= 512) on the 2/3-stage tiles below (autotuned
+    at capture); fat prefill GEMMs (M >= LARGE_M) on the 256x256 8-phase ping-pong kernel
+    (tile 22) with its fused epilogue (SiLU*up, bias+GELU, fp32) — no library GEMM on the
+    hot path. ``DLI_GEMM_PREFILL_BLAS=1`` routes plain prefill GEMMs to hipBLASLt instead
+    (ablation only)."""
+    if M >= LARGE_M:
+        if (os.environ.get("DLI_GEMM_PREFILL_BLAS", "0") == "1" and epi in ("none", "splitk")
+                and os.environ.get("DLI_GEMM_NO_BLAS", "0") != "1"):
+            return GemmPlan("hipblaslt", 2, 1)
+        return GemmPlan("dli", 22, 1)
     if M <= 128:
         tile = 0 if N <= 8192 else 1
     elif M <= 256:
@@ -290,7 +295,7 @@ def candidate_plans(M: int, N: int, K: int, epi: str):
     # DLI_GEMM_DECODE_BLAS=1: measured in-situ at M = 512 our kernels (8-wave 256x256 gate/up
     # with fused SiLU, 3-stage 128-row tiles) run the decode layer as fast as the library mix
     # (249.5 vs 257 us per layer, profiles/r1_final/), so the decode hot path stays entirely
-    # on hand-written MFMA kernels. Prefill-sized plain GEMMs (M >= LARGE_M) use hipBLASLt.
+    # on hand-written MFMA kernels.
     if (epi in ("none", "splitk", "silu_mul", "f32")
             and os.environ.get("DLI_GEMM_DECODE_BLAS", "0") == "1"
             and os.environ.get("DLI_GEMM_NO_BLAS") != "1"):

@@ -319,6 +319,27 @@ def test_sampling_fallback_path_adversarial(gpu):
 
 
 @pytest.mark.parametrize("epi", ["none", "silu_mul"])
+def test_grouped_8phase_rows_bound(gpu, epi):
+    """Grouped tile 22 with M = the largest group's rows (the MoE prefill launch) over groups
+    of 0 / 300 / 1029 / 513 rows: row tiles past a group's end are skipped, partial ones
+    clamped."""
+    torch.manual_seed(14)
+    sizes = [0, 300, 1029, 513]
+    E, N, K = len(sizes), 512, 640
+    x = rnd(sum(sizes), K, dev=gpu)
+    w = rnd(E, N, K, dev=gpu, scale=0.05)
+    off = torch.tensor([0] + list(__import__("itertools").accumulate(sizes)), dtype=torch.int32,
+                       device=gpu)
+    refs = []
+    for e in range(E):
+        y = R.linear(x[off[e]:off[e + 1]], w[e])
+        refs.append(R.silu_mul(y.float().to(BF)) if epi == "silu_mul" else y)
+    out = ops._gemm_native(x, w, epi, plan=G.GemmPlan("dli", 22, 1), groups=E, group_off=off,
+                           rows_per_group=max(sizes))
+    close(out, torch.cat(refs), rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("epi", ["none", "silu_mul"])
 def test_grouped_gemm_all_tiles_and_splitk(gpu, epi):
     """Grouped (MoE) GEMM over uneven groups (one empty, one past a 128-row tile) for every
     tile id and split-K factor, against per-group fp32 references."""
@@ -345,10 +366,10 @@ def test_grouped_gemm_all_tiles_and_splitk(gpu, epi):
             close(out, ref, rtol=2e-2, atol=2e-2)
 
 
-def test_moe_mlp_prefill_blas_path(gpu, monkeypatch):
-    """Prefill-sized MoE (rows per expert above the threshold) takes the per-expert
-    hipBLASLt path; same result as the reference."""
-    monkeypatch.setattr(ops, "_MOE_BLAS_ROWS", 16)
+def test_moe_mlp_prefill_grouped_8phase_path(gpu, monkeypatch):
+    """Prefill-sized MoE (rows per expert above the threshold) takes the grouped 8-phase
+    path (grid bounded by the largest expert's rows); same result as the reference."""
+    monkeypatch.setattr(ops, "_MOE_PREFILL_ROWS", 16)
     torch.manual_seed(13)
     T, E, k, D, F = 200, 4, 2, 256, 512
     x = rnd(T, D, dev=gpu)

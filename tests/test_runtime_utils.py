@@ -241,3 +241,19 @@ def test_decode_core_matches_python_scheduler():
     m_c, out_c = run(True)
     assert out_c == out_py
     assert m_c == m_py
+
+
+def test_prefill_gemm_plan_is_own_kernel(monkeypatch):
+    """Prefill-sized GEMMs plan onto the 8-phase MFMA kernel (tile 22), never hipBLASLt,
+    unless the ablation switch asks for the library."""
+    from distributed_llm_inferencing_amd.ops import gemm as G
+    G.clear_plans()
+    for epi in ("none", "silu_mul", "splitk", "f32"):
+        p = G.plan(16384, 6144, 4096, epi)
+        assert p.backend == "dli" and p.tile == 22 and p.splits == 1, (epi, p)
+    assert all(p.backend == "dli" for p in G.candidate_plans(512, 4096, 4096, "none"))
+    G.clear_plans()
+    monkeypatch.setenv("DLI_GEMM_PREFILL_BLAS", "1")
+    assert G.plan(16384, 6144, 4096, "none").backend == "hipblaslt"
+    assert G.plan(16384, 28672, 4096, "silu_mul").backend == "dli"
+    G.clear_plans()
