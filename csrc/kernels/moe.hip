@@ -161,3 +161,51 @@ extern "C" int dli_moe_combine(void* out, const void* y, const float* w, const i
                                                                  T, k, dim);
   DLI_RETURN_LAUNCH();
 }
+
+// Expert-parallel dispatch pack (parallel/expert.py): every (token t, pick j) row goes to
+// the bucket of the rank that holds its expert:
+//   dest = id / e_per,  pos[t*k + j] = base[dest] + atomicAdd(&fill[dest], 1),
+//   send_x[pos] = x[t], send_e[pos] = id (global expert id; unused rows keep -1).
+// Decode: base[d] = d * C with C = T * min(k, e_per), which bounds a bucket exactly (a
+// token's top-k experts are distinct), so no row is dropped and the all-to-all sizes are
+// known on the host without reading the routing. Prefill: base = exclusive prefix of the
+// exact per-destination counts. Slot order within a bucket is arbitrary; results do not
+// depend on it (the expert GEMM treats rows independently, the combine sums each token's
+// picks in j order). One 256-thread workgroup per (t, j): lane 0 claims the slot, the block
+// copies the row with 16-B vectors.
+__global__ void __launch_bounds__(256) ep_pack_kernel(u16* __restrict__ send_x,
+                                                      int* __restrict__ send_e,
+                                                      int* __restrict__ pos,
+                                                      int* __restrict__ fill,
+                                                      const int* __restrict__ base,
+                                                      const u16* __restrict__ x,
+                                                      const int* __restrict__ ids, int k, int D,
+                                                      int e_per) {
+  __shared__ int s_pos;
+  const int r = blockIdx.x;                      // = t * k + j
+  const int t = r / k;
+  if (threadIdx.x == 0) {
+    const int id = ids[r];
+    const int dest = id / e_per;
+    const int p = base[dest] + atomicAdd(&fill[dest], 1);
+    pos[r] = p;
+    send_e[p] = id;
+    s_pos = p;
+  }
+  __syncthreads();
+  const int p = s_pos;
+  const int chunks = D >> 3;
+  for (int c = threadIdx.x; c < chunks; c += blockDim.x)
+    *reinterpret_cast<uint4*>(send_x + (long)p * D + c * 8) =
+        *reinterpret_cast<const uint4*>(x + (long)t * D + c * 8);
+}
+
+extern "C" int dli_ep_pack(void* send_x, int* send_e, int* pos, int* fill, const int* base,
+                           const void* x, const int* ids, int T, int k, int D, int e_per,
+                           hipStream_t st) {
+  if (T <= 0) return 0;
+  if (D % 8 || e_per <= 0) return (int)hipErrorInvalidValue;
+  ep_pack_kernel<<<T * k, 256, 0, st>>>((u16*)send_x, send_e, pos, fill, base, (const u16*)x,
+                                         ids, k, D, e_per);
+  DLI_RETURN_LAUNCH();
+}

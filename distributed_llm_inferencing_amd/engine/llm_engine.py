@@ -152,12 +152,23 @@ class LLMEngine:
         step BEFORE the in-flight step's tokens reach the host, then applies those tokens:
         the host's sync, scheduler update and metadata upload overlap the GPU's work instead
         of leaving it idle between steps (measured ~8 % idle at batch 512 without)."""
-        prev = self._inflight
         t0 = time.perf_counter()
-        meta = None
+        return self.finish_step(self.plan_step(), t0)
+
+    def plan_step(self):
+        """Schedule this iteration's step (against the in-flight one under lookahead);
+        None when there is nothing to launch. Lockstep users (expert parallelism) read its
+        size before every rank launches."""
         with self.timer.phase("schedule"):
-            if self.scheduler.has_work():
-                meta = self.scheduler.schedule(0, inflight=prev[0] if prev else None)
+            if not self.scheduler.has_work():
+                return None
+            prev = self._inflight
+            return self.scheduler.schedule(0, inflight=prev[0] if prev else None)
+
+    def finish_step(self, meta, t0: Optional[float] = None) -> List[RequestOutput]:
+        """Launch ``meta`` (if any), then apply the tokens of the step that completes now."""
+        t0 = time.perf_counter() if t0 is None else t0
+        prev = self._inflight
         launched = None
         if meta is not None:
             kind = "prefill" if meta.kind == 1 else "decode"

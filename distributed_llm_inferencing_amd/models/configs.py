@@ -124,13 +124,16 @@ LLAMA_TINY8 = replace(LLAMA_TINY, name="llama-tiny8", num_layers=8)
 MIXTRAL_TINY = replace(LLAMA_TINY, name="mixtral-tiny", num_experts=4, top_k_experts=2,
                        intermediate_size=256)
 
+# 8 experts: one per rank of an 8-rank expert-parallel test
+MIXTRAL_TINY8E = replace(MIXTRAL_TINY, name="mixtral-tiny8e", num_experts=8)
+
 GPT2_TINY = replace(GPT2, name="gpt2-tiny", hidden_size=256, num_layers=2, num_heads=4,
                     num_kv_heads=4, head_dim=64, intermediate_size=1024, vocab_size=1024,
                     max_position=256, bos_token_id=1023, eos_token_id=1023)
 
 _REGISTRY = {c.name: c for c in
              (GPT2, LLAMA3_8B, LLAMA3_70B, MIXTRAL_8X7B, LLAMA_TINY, LLAMA_TINY128,
-              LLAMA_TINY8, MIXTRAL_TINY, GPT2_TINY)}
+              LLAMA_TINY8, MIXTRAL_TINY, MIXTRAL_TINY8E, GPT2_TINY)}
 
 _ALIASES = {
     "openai-community/gpt2": "gpt2",

@@ -415,6 +415,53 @@ def moe_mlp(x, w_gu, w_down, topk_w, topk_ids, expert_offset: int = 0):
     return out
 
 
+def ep_pack(x, topk_ids, e_per: int, base, send_rows: int):
+    """Expert-parallel dispatch: (token, pick) rows into per-destination-rank buckets
+    starting at ``base[dest]`` (int32 [N] on the device). Returns (send_x [send_rows, D],
+    send_e int32 [send_rows] global expert id or -1, pos int32 [T, k] row of each pick)."""
+    T, D = x.shape
+    k = topk_ids.shape[1]
+    dev = x.device
+    send_x = torch.empty(max(send_rows, 1), D, dtype=x.dtype, device=dev)[:send_rows]
+    send_e = torch.full((send_rows,), -1, dtype=torch.int32, device=dev)
+    pos = torch.empty(T, k, dtype=torch.int32, device=dev)
+    if not _use_native(x):
+        # deterministic reference: slots in (token, pick) order
+        fill = [0] * base.shape[0]
+        bl = base.tolist()
+        ids = topk_ids.tolist()
+        for t in range(T):
+            for j in range(k):
+                d = ids[t][j] // e_per
+                p = bl[d] + fill[d]
+                fill[d] += 1
+                pos[t, j] = p
+                send_e[p] = ids[t][j]
+                send_x[p] = x[t]
+        return send_x, send_e, pos
+    fill = torch.zeros(base.shape[0], dtype=torch.int32, device=dev)
+    _native_call("dli_ep_pack", _p(send_x), _p(send_e), _p(pos), _p(fill), _p(base), _p(x),
+                 _p(topk_ids), T, k, D, e_per, _st())
+    return send_x, send_e, pos
+
+
+def moe_combine(y, topk_w, pos):
+    """out[t] = sum_j topk_w[t, j] * y[pos[t, j]] (fp32 sum in j order, bf16 out); pos < 0
+    rows contribute nothing."""
+    T, k = pos.shape
+    D = y.shape[1]
+    if not _use_native(y):
+        out = torch.zeros(T, D, dtype=torch.float32, device=y.device)
+        for j in range(k):
+            pj = pos[:, j].long()
+            ok = pj >= 0
+            out[ok] += topk_w[ok, j:j + 1].float() * y[pj[ok]].float()
+        return out.to(y.dtype)
+    out = torch.empty(T, D, dtype=y.dtype, device=y.device)
+    _native_call("dli_moe_combine", _p(out), _p(y), _p(topk_w), _p(pos), T, k, D, _st())
+    return out
+
+
 # ----------------------------------------------------------------------------- misc
 def native_library_path():
     return N.loaded_path()

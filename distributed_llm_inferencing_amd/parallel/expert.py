@@ -1,27 +1,35 @@
 """Expert parallelism for Mixtral: experts mapped to GPU ranks, all-to-all over xGMI
-(BASELINE.json config 5; SURVEY.md §2.4 C4, §2.5 "Expert parallel").
+(BASELINE.json config 5; SURVEY.md §2.4 C4, §2.5 "Expert parallel"; the reference has no
+MoE at all — its compute is HF ``generate`` at ``worker/app.py:297-305``).
 
 Layout: data-parallel attention + expert-parallel MoE. Every rank holds the full attention
 / norm / embedding weights and its own requests + paged KV; rank r holds experts
-[r*E/N, (r+1)*E/N). Per MoE layer:
+[r*E/N, (r+1)*E/N). Per MoE layer, all on device:
 
-    route (softmax -> top-2 -> renormalise, local)
-    dispatch: (token, slot) rows sorted by destination rank -> all_to_all_single
-    local grouped-GEMM expert MLPs (HIP kernels) on the rows received
-    combine: all_to_all_single back -> weighted sum per token
+    route (softmax -> top-2 -> renormalise)                  moe_route kernel
+    dispatch pack: (token, pick) rows into per-rank buckets  ep_pack kernel
+    all_to_all_single (rows + their expert ids)              RCCL, all 7 xGMI links at once
+    local expert MLPs on the rows received                   moe_align/gather + grouped GEMM
+    all_to_all_single back, weighted sum per token           moe_combine kernel
 
-On the fully connected 8-GPU xGMI mesh each rank pair has its own link, so the all-to-all
-runs on all 7 links at once. Split sizes are exchanged per layer (one tiny all-to-all of
-counts) so the payload is exact (no capacity padding / no dropped tokens).
+Decode steps use FIXED-CAPACITY buckets: a token's top-k experts are distinct, so a rank
+sends at most min(k, E/N) rows per token to any peer; with every rank's token count T_p of
+the step known, bucket sizes are exact bounds (no dropped tokens, identical results) and
+nothing about the routing is read on the host. The T_p come from the ONE per-step lockstep
+exchange every rank makes anyway (do we still have work? how many tokens?): O(1) host syncs
+per decode step, none per layer. Prefill steps (T in the thousands) would move mostly
+padding at that bound, so they exchange exact per-destination counts per layer (one host
+read per layer; prefill is compute-bound).
 
-Ranks step in lockstep (each step runs the same 32 MoE exchanges on every rank; a rank with
-no local work still joins with zero rows).
+Ranks step in lockstep: every rank launches one forward per step (a rank without work runs
+an empty one that still joins every exchange); lookahead scheduling stays on (a rank's
+next step is planned against its in-flight one before the lockstep exchange).
 """
 from __future__ import annotations
 
 import os
 import time
-from typing import Optional
+from typing import List, Optional
 
 import torch
 import torch.distributed as dist
@@ -31,6 +39,9 @@ from ..engine.llm_engine import LLMEngine
 from ..models.configs import get_config
 from ..models.model import TransformerLM
 from ..models import weights as W
+
+# a step whose largest per-rank token count exceeds this exchanges exact counts per layer
+EP_BOUND_MAX_TOKENS = int(os.environ.get("DLI_EP_BOUND_MAX_TOKENS", "1024"))
 
 
 class ExpertParallelMoE:
@@ -45,11 +56,22 @@ class ExpertParallelMoE:
         self.E, self.k = num_experts, top_k
         self.e_per = num_experts // self.world
         self.e0 = self.rank * self.e_per
+        self.per_token = min(top_k, self.e_per)        # rows per token to any one rank
         self.bytes_sent = 0
         self.exchanges = 0
+        self.host_reads = 0                            # routing-dependent host syncs
+        self.peer_tokens: Optional[List[int]] = None   # T of every rank for this step
+        self._bases = {}
 
     def expert_range(self):
         return (self.e0, self.e0 + self.e_per)
+
+    def begin_step(self, peer_tokens: List[int]) -> None:
+        """Every rank's token count for the forward about to run (same list everywhere)."""
+        self.peer_tokens = [int(t) for t in peer_tokens]
+
+    def _cdev(self, dev):
+        return dev if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
 
     def _a2a(self, out, inp, out_splits, in_splits):
         dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
@@ -58,53 +80,67 @@ class ExpertParallelMoE:
         T, D = h.shape
         dev = h.device
         k, N = self.k, self.world
+        if self.peer_tokens is None or len(self.peer_tokens) != N or \
+                self.peer_tokens[self.rank] != T:
+            raise RuntimeError("ExpertParallelMoE: begin_step() must announce this step's "
+                               "token counts before the forward")
         if T > 0:
             router_logits = ops.linear(h, lp["router"])
             topk_w, topk_ids = ops.moe_route(router_logits, k)
-            flat_ids = topk_ids.reshape(-1).long()
-            dest = flat_ids // self.e_per
-            order = torch.argsort(dest, stable=True)
-            send_counts = torch.bincount(dest, minlength=N)
         else:
             topk_w = torch.zeros(0, k, dtype=torch.float32, device=dev)
-            flat_ids = torch.zeros(0, dtype=torch.long, device=dev)
-            order = torch.zeros(0, dtype=torch.long, device=dev)
-            send_counts = torch.zeros(N, dtype=torch.long, device=dev)
-        cdev = dev if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
-        sc = send_counts.to(cdev)
-        rc = torch.empty_like(sc)
-        dist.all_to_all_single(rc, sc, group=self.group)
-        in_splits = sc.tolist()
-        out_splits = rc.tolist()
-        R = int(sum(out_splits))
-        # dispatch rows (token embedding + its global expert id)
-        src_tok = order // k
-        send_x = h.index_select(0, src_tok) if T > 0 else h.new_zeros(0, D)
-        send_e = flat_ids.index_select(0, order).to(torch.int32) if T > 0 else \
-            torch.zeros(0, dtype=torch.int32, device=dev)
-        recv_x = torch.empty(R, D, dtype=h.dtype, device=cdev)
-        recv_e = torch.empty(R, dtype=torch.int32, device=cdev)
-        self._a2a(recv_x, send_x.to(cdev), out_splits, in_splits)
-        self._a2a(recv_e, send_e.to(cdev), out_splits, in_splits)
+            topk_ids = torch.zeros(0, k, dtype=torch.int32, device=dev)
+        bound = max(self.peer_tokens) <= EP_BOUND_MAX_TOKENS
+        if bound:
+            # fixed-capacity buckets: C_p = T_p * min(k, E/N) rows from rank p to each rank
+            C = T * self.per_token
+            in_splits = [C] * N
+            out_splits = [t * self.per_token for t in self.peer_tokens]
+            key = (C, str(dev))
+            base = self._bases.get(key)
+            if base is None:
+                base = torch.arange(N, dtype=torch.int32, device=dev) * C
+                self._bases[key] = base
+        else:
+            # exact per-destination counts (prefill): one host read per layer
+            if T > 0:
+                dest = topk_ids.reshape(-1).long() // self.e_per
+                sc = torch.bincount(dest, minlength=N).to(torch.int32)
+            else:
+                sc = torch.zeros(N, dtype=torch.int32, device=dev)
+            cd = self._cdev(dev)
+            rc = torch.empty(N, dtype=torch.int32, device=cd)
+            dist.all_to_all_single(rc, sc.to(cd), group=self.group)
+            both = torch.cat([sc.to(cd), rc]).tolist()
+            self.host_reads += 1
+            in_splits, out_splits = both[:N], both[N:]
+            base = torch.zeros(N, dtype=torch.int32, device=dev)
+            if N > 1:
+                base[1:] = torch.cumsum(sc, 0)[:-1].to(torch.int32)
+        send_rows, recv_rows = sum(in_splits), sum(out_splits)
+        send_x, send_e, pos = ops.ep_pack(h, topk_ids, self.e_per, base, send_rows)
+        cd = self._cdev(dev)
+        recv_x = torch.empty(recv_rows, D, dtype=h.dtype, device=cd)
+        recv_e = torch.empty(recv_rows, dtype=torch.int32, device=cd)
+        self._a2a(recv_x, send_x.to(cd), out_splits, in_splits)
+        self._a2a(recv_e, send_e.to(cd), out_splits, in_splits)
         recv_x, recv_e = recv_x.to(dev), recv_e.to(dev)
-        # local experts: one expert per received row (top-1 with weight 1)
-        if R > 0:
+        # local experts: one expert per received row (weight 1); padding rows (id -1) fall
+        # outside the local range, are skipped by the align and come back as zeros
+        if recv_rows > 0:
             y = ops.moe_mlp(recv_x, lp["w_gu"], lp["w_down"],
-                            torch.ones(R, 1, dtype=torch.float32, device=dev),
-                            recv_e.view(R, 1), self.e0)
+                            torch.ones(recv_rows, 1, dtype=torch.float32, device=dev),
+                            recv_e.view(recv_rows, 1), self.e0)
         else:
             y = recv_x.new_zeros(0, D)
-        back = torch.empty(T * k, D, dtype=h.dtype, device=cdev)
-        self._a2a(back, y.to(cdev), in_splits, out_splits)
+        back = torch.empty(send_rows, D, dtype=h.dtype, device=cd)
+        self._a2a(back, y.to(cd), in_splits, out_splits)
         back = back.to(dev)
         self.exchanges += 1
-        self.bytes_sent += (T * k + R) * D * h.element_size()
+        self.bytes_sent += (send_rows + recv_rows) * D * h.element_size()
         if T == 0:
             return h.new_zeros(0, D)
-        contrib = torch.empty_like(back)
-        contrib.index_copy_(0, order, back)
-        out = (contrib.view(T, k, D).float() * topk_w.view(T, k, 1)).sum(1)
-        return out.to(h.dtype)
+        return ops.moe_combine(back, topk_w, pos)
 
 
 class ExpertParallelEngine:
@@ -113,7 +149,7 @@ class ExpertParallelEngine:
 
     def __init__(self, model: str, device, max_batch: int = 256, max_model_len: int = 2048,
                  seed: int = 0, num_blocks: Optional[int] = None, dtype=torch.bfloat16,
-                 max_prefill_tokens: int = 16384):
+                 max_prefill_tokens: int = 16384, lookahead: Optional[bool] = None):
         from .transport import init_distributed
         dev = torch.device(device)
         self.rank, self.world = init_distributed(device=dev if dev.type == "cuda" else None)
@@ -135,31 +171,51 @@ class ExpertParallelEngine:
         self.engine = LLMEngine(cfg, device=str(dev), dtype=dtype, max_batch=max_batch,
                                 max_model_len=max_model_len, num_blocks=num_blocks,
                                 use_graphs=False, lm=lm,
-                                max_prefill_tokens=max_prefill_tokens,
-                                lookahead=False)   # every forward joins the ranks' all-to-alls
+                                max_prefill_tokens=max_prefill_tokens, lookahead=lookahead)
         self.device = dev
+        self.steps = 0
+        self.lockstep_syncs = 0
 
-    def _any_work(self) -> bool:
+    def _exchange(self, work: bool, tokens: int) -> List[List[int]]:
+        """The per-step lockstep exchange: (has work, tokens of the next forward) of every
+        rank — the one host sync of a decode step."""
         cdev = self.device if dist.get_backend() == "nccl" else torch.device("cpu")
-        t = torch.tensor([1 if self.engine.has_work() else 0], dtype=torch.int32, device=cdev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return bool(t.item())
+        mine = torch.tensor([1 if work else 0, tokens], dtype=torch.int64, device=cdev)
+        allv = [torch.empty_like(mine) for _ in range(self.world)]
+        dist.all_gather(allv, mine)
+        self.lockstep_syncs += 1
+        return torch.stack(allv).tolist()
 
-    def _idle_step(self):
+    def _idle_forward(self):
         """Join every MoE exchange of one forward with zero local rows."""
         D = self.cfg.hidden_size
-        h = torch.zeros(0, D, dtype=torch.bfloat16, device=self.device)
+        h = torch.zeros(0, D, dtype=self.engine.model.params["embed"].dtype, device=self.device)
         for i in range(self.cfg.num_layers):
             self.moe(h, self.engine.model.layers[i], i)
 
+    def step(self):
+        """One lockstep iteration: plan this rank's step, exchange (work, tokens) with every
+        rank, then launch the forward (an empty one when this rank has none) and apply the
+        tokens of the step that completes. Returns (outputs, any rank had work)."""
+        eng = self.engine
+        meta = eng.plan_step()
+        work = meta is not None or eng.has_work()
+        info = self._exchange(work, 0 if meta is None else meta.num_tokens)
+        if not any(w for w, _ in info):
+            return eng.finish_step(None), False
+        self.moe.begin_step([t for _, t in info])
+        if meta is None:
+            self._idle_forward()
+        self.steps += 1
+        return eng.finish_step(meta), True
+
     def run_until_idle(self):
         outs = []
-        while self._any_work():
-            if self.engine.has_work():
-                outs.extend(self.engine.step())
-            else:
-                self._idle_step()
-        outs.extend(self.engine.step())
+        while True:
+            o, more = self.step()
+            outs.extend(o)
+            if not more:
+                break
         return outs
 
     def generate(self, prompts, params=None):

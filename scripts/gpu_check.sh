@@ -46,6 +46,7 @@ for s in "$@"; do
         step ab_notune 600 env DLI_GEMM_AUTOTUNE=0 python bench.py --steps 2 --warmup 1
         step ab_fused2 600 python bench.py --steps 2 --warmup 1 ;;
     mixtral1) step mixtral1 900 python bench.py --model mixtral-8x7b --steps 1 --warmup 1 --batch 128 ;;
+    ep4) step ep4 900 env DLI_DIST_BACKEND=gloo DLI_SAME_DEVICE=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29539 bench.py --model mixtral-8x7b --gpus 4 --steps 1 --warmup 1 --batch 32 ;;
     ep2) step ep2 900 env DLI_DIST_BACKEND=gloo DLI_SAME_DEVICE=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29535 bench.py --model mixtral-8x7b --gpus 2 --steps 1 --warmup 1 --batch 32 ;;
     llama70) step llama70 1100 python bench.py --model llama3-70b --steps 1 --warmup 1 --batch 64 ;;
     bench_small) step bench_small 600 python bench.py --steps 2 --warmup 1 --batch 64 ;;

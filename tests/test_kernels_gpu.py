@@ -469,3 +469,29 @@ def test_head_candidates_native_matches_reference(gpu):
     assert torch.equal(i, ri)
     assert torch.equal(v, rv.gather(1, perm))
     close(v, R.linear(h, w, out_dtype=torch.float32).gather(1, (i - 5000).long()))
+
+
+def test_ep_pack_and_combine(gpu):
+    """Expert-parallel dispatch pack (fixed-capacity buckets) and the weighted combine:
+    every (token, pick) row lands in its destination's bucket with its expert id, unused
+    rows keep -1, and combining the returned rows equals the fp32 reference sum."""
+    torch.manual_seed(15)
+    T, k, D, N, e_per = 300, 2, 512, 4, 2
+    x = rnd(T, D, dev=gpu)
+    _w, ids = R.router_topk(rnd(T, N * e_per, dev=gpu), k)
+    ids = ids.to(torch.int32)
+    C = T * min(k, e_per)
+    base = torch.arange(N, dtype=torch.int32, device=gpu) * C
+    sx, se, pos = ops.ep_pack(x, ids, e_per, base, N * C)
+    torch.cuda.synchronize()
+    p = pos.long()
+    assert torch.equal(se[p.flatten()], ids.flatten())
+    assert torch.equal(sx[p.flatten()], x.repeat_interleave(k, 0))
+    dest = (ids.long() // e_per)
+    assert bool(((p >= dest * C) & (p < dest * C + C)).all())          # inside its bucket
+    assert int((se >= 0).sum()) == T * k and len(set(p.flatten().tolist())) == T * k
+    y = rnd(N * C, D, dev=gpu)
+    w = torch.rand(T, k, device=gpu)
+    out = ops.moe_combine(y, w, pos)
+    ref = (y[p].float() * w.unsqueeze(-1)).sum(1)
+    close(out, ref, rtol=1e-2, atol=1e-2)
