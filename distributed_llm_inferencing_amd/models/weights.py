@@ -108,7 +108,11 @@ def slice_experts(name: str, t: torch.Tensor, expert_range: Optional[tuple]) -> 
         return t
     if t.dim() != 3:
         return t
-    return t[expert_range[0]:expert_range[1]].contiguous()
+    if expert_range[0] == 0 and expert_range[1] == t.shape[0]:
+        return t
+    # a copy: a leading-dim slice is already contiguous, so .contiguous() would return a
+    # view that keeps every expert's storage alive (each EP rank held all 8 experts)
+    return t[expert_range[0]:expert_range[1]].clone()
 
 
 def _name_hash(name: str) -> int:

@@ -257,3 +257,14 @@ def test_prefill_gemm_plan_is_own_kernel(monkeypatch):
     assert G.plan(16384, 6144, 4096, "none").backend == "hipblaslt"
     assert G.plan(16384, 28672, 4096, "silu_mul").backend == "dli"
     G.clear_plans()
+
+
+def test_slice_experts_releases_other_experts():
+    """An EP rank keeps only its experts' storage (a view would pin all of them)."""
+    import torch
+    from distributed_llm_inferencing_amd.models import weights as W
+    t = torch.randn(8, 16, 4)
+    s = W.slice_experts("layers.0.w_gu", t, (2, 4))
+    assert s.shape[0] == 2 and torch.equal(s, t[2:4])
+    assert s.untyped_storage().nbytes() == 2 * 16 * 4 * 4
+    assert W.slice_experts("layers.0.attn_norm", t, (2, 4)) is t
