@@ -50,6 +50,11 @@ class Dispatcher:
         self._threads: List[threading.Thread] = []
         self.max_length = MAX_LENGTH
         self.processed = 0
+        # (node id, model) confirmed loaded: skip the /load_model round trip before every
+        # /inference (the reference posts it each time, views.py:397-401; the worker also
+        # auto-loads on /inference, app.py:278-282). Dropped on any error from that node.
+        self._loaded: set = set()
+        self.load_calls = 0
 
     # ------------------------------------------------------------------ lifecycle
     def start(self):
@@ -152,17 +157,21 @@ class Dispatcher:
         t0 = time.perf_counter()
         try:
             faults.check("dispatch.post")
-            if shard_ids is None:
+            if shard_ids is None and (node["id"], model) not in self._loaded:
+                self.load_calls += 1
                 r = self._post(node, "/load_model", {"model_name": model}, HTTP_LOAD_TIMEOUT)
                 if r.status_code != 200:
                     self.store.mark_failed(rid, f"Failed to load model: {r.text}")
                     return False, None
+                with self._lock:
+                    self._loaded.add((node["id"], model))
             payload = {"model_name": model, "prompt": prompt, "max_length": self.max_length,
                        "timeout": WORKER_TIMEOUT}
             if shard_ids is not None:
                 payload["shard_ids"] = sorted(shard_ids)
             r = self._post(node, "/inference", payload, HTTP_INFER_TIMEOUT)
         except (requests.RequestException, faults.InjectedFault) as e:
+            self._forget(node["id"])
             return False, f"Connection error: {e}"
         if r.status_code == 200:
             data = r.json()
@@ -172,5 +181,10 @@ class Dispatcher:
                 return True, None
             self.store.mark_failed(rid, data.get("message", "Unknown error"))
             return False, None
+        self._forget(node["id"])
         self.store.mark_failed(rid, f"Node returned status code {r.status_code}: {r.text}")
         return False, None
+
+    def _forget(self, node_id: int) -> None:
+        with self._lock:
+            self._loaded = {k for k in self._loaded if k[0] != node_id}

@@ -328,7 +328,15 @@ def main(argv=None):
     ap = argparse.ArgumentParser("dli serve-master")
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--port", type=int, default=8000)
+    ap.add_argument("--server", default="werkzeug", choices=["werkzeug", "uvicorn"],
+                    help="werkzeug: threaded WSGI server (a thread per connection); uvicorn: "
+                         "its WSGI interface over the module-level app (control/wsgi.py)")
     a = ap.parse_args(argv)
+    if a.server == "uvicorn":
+        import uvicorn
+        uvicorn.run("distributed_llm_inferencing_amd.control.wsgi:application",
+                    interface="wsgi", host=a.host, port=a.port, log_level="warning")
+        return
     from ..utils.log import setup_logging
     setup_logging("master")
     app = create_master_app()

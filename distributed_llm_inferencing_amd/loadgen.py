@@ -108,13 +108,18 @@ def main(argv=None):
     ap.add_argument("--rate", type=float, default=0.0, help="open loop (requests/s) if > 0")
     ap.add_argument("--prompt-words", type=int, default=24)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--poll", type=float, default=0.05, help="status poll interval (s)")
+    ap.add_argument("--tokens-per-request", type=int, default=0,
+                    help="report output tokens/s (requests generate a fixed count)")
     a = ap.parse_args(argv)
     rng = random.Random(a.seed)
     prompts = [make_prompt(rng, a.prompt_words) for _ in range(a.requests)]
-    lg = LoadGen(a.master, a.model)
+    lg = LoadGen(a.master, a.model, poll_s=a.poll)
     wall = lg.open_loop(prompts, a.rate, a.seed) if a.rate > 0 else \
         lg.closed_loop(prompts, a.concurrency)
-    print(json.dumps(lg.report(wall)), flush=True)
+    rep = lg.report(wall, a.tokens_per_request or None)
+    rep.update(concurrency=a.concurrency, rate=a.rate, poll_s=a.poll)
+    print(json.dumps(rep), flush=True)
     return 0
 
 

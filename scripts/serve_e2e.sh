@@ -1,13 +1,21 @@
 #!/bin/bash
-# End-to-end serving on one MI355X through the public API: master (Flask, sqlite, dispatcher
-# pool) + one GPU worker (continuous batching over HTTP requests) + the load generator.
-# Usage: bash scripts/serve_e2e.sh [requests] [concurrency] [max_batch]
+# End-to-end serving on one MI355X through the public API (BASELINE.json config 2: master
+# dispatch -> one Llama-3-8B worker): master (Flask, sqlite store, request queue,
+# dispatcher pool) + one GPU worker (continuous batching over HTTP requests) + the load
+# generator submitting form-encoded requests exactly as the reference UI does and polling
+# /api/inference/status/<id>/. Reference request shape: max_length 100 incl. the prompt,
+# T=0.8 / top-k 50 / top-p 0.95 (the dispatcher's defaults, views.py:351).
+#
+# Phases: warm-up (graphs already captured by --preload), closed loop at concurrency C
+# (N requests), then concurrency 1 (latency of a lone request through every hop).
+# Usage: bash scripts/serve_e2e.sh [requests] [concurrency] [max_batch] [server]
 set -u
-N=${1:-1024}; C=${2:-512}; B=${3:-512}
+N=${1:-1024}; C=${2:-512}; B=${3:-512}; SRV=${4:-werkzeug}
 mkdir -p gpurun_out/logs
 export MASTER_DB=/tmp/dli_e2e_$$.sqlite3 DLI_LOG_DIR=gpurun_out/logs DISPATCH_WORKERS=$C
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-python -m distributed_llm_inferencing_amd.cli serve-master --port 8000 > gpurun_out/e2e_master.log 2>&1 &
+python -m distributed_llm_inferencing_amd.cli serve-master --port 8000 --server $SRV \
+    > gpurun_out/e2e_master.log 2>&1 &
 MPID=$!
 python -m distributed_llm_inferencing_amd.cli serve-worker --port 5000 --gpu 0 --max-batch $B \
     --preload llama3-8b > gpurun_out/e2e_worker.log 2>&1 &
@@ -22,12 +30,16 @@ rc=1
 if [ $ok = 1 ]; then
   curl -s -X POST -d hostname=gpu0 -d ip_address=127.0.0.1 -d port=5000 \
       http://127.0.0.1:8000/api/nodes/add/ > gpurun_out/e2e_addnode.json
-  timeout -k 10 900 python -m distributed_llm_inferencing_amd.loadgen \
-      --master http://127.0.0.1:8000 --model llama3-8b --requests $N --concurrency $C \
-      > gpurun_out/e2e_loadgen.json
+  LG="python -m distributed_llm_inferencing_amd.loadgen --master http://127.0.0.1:8000 --model llama3-8b --prompt-words 5"
+  # warm-up wave (same shape)
+  timeout -k 10 600 $LG --requests $C --concurrency $C --seed 99 > gpurun_out/e2e_warmup.json && \
+  curl -s http://127.0.0.1:5000/metrics > gpurun_out/e2e_metrics_before.json && \
+  timeout -k 10 900 $LG --requests $N --concurrency $C > gpurun_out/e2e_loadgen_c$C.json && \
+  curl -s http://127.0.0.1:5000/metrics > gpurun_out/e2e_metrics_after.json && \
+  timeout -k 10 600 $LG --requests 16 --concurrency 1 --poll 0.01 > gpurun_out/e2e_loadgen_c1.json
   rc=$?
-  cat gpurun_out/e2e_loadgen.json
-  curl -s http://127.0.0.1:5000/metrics > gpurun_out/e2e_worker_metrics.json
+  cat gpurun_out/e2e_loadgen_c$C.json gpurun_out/e2e_loadgen_c1.json
+  curl -s http://127.0.0.1:8000/metrics > gpurun_out/e2e_master_metrics.json
 else
   echo "worker did not become healthy"; tail -20 gpurun_out/e2e_worker.log
 fi

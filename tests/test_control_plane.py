@@ -214,10 +214,43 @@ def test_end_to_end_dispatch_over_http(tmp_path, master):
         assert st["result"].startswith("Hello") and st["completed_at"]
         recent = c.get("/api/inference/recent/").get_json()["requests"]
         assert recent[0]["id"] == rid
+        # further requests to the same node skip the /load_model round trip
+        rids = [c.post("/api/inference/submit/", data={"model_name": "gpt2-tiny",
+                                                       "prompt": f"Hi {i}"}).get_json()[
+            "request_id"] for i in range(3)]
+        deadline = time.time() + 120
+        while time.time() < deadline and any(
+                c.get(f"/api/inference/status/{r}/").get_json()["status"] not in
+                ("completed", "failed") for r in rids):
+            time.sleep(0.1)
+        assert all(c.get(f"/api/inference/status/{r}/").get_json()["status"] == "completed"
+                   for r in rids)
+        assert master.extensions["dli"].dispatcher.load_calls == 1
         m = c.get("/metrics").get_json()
-        assert m["requests"]["completed"] == 1
+        assert m["requests"]["completed"] == 4
     finally:
         w.close()
+
+
+def test_master_module_level_wsgi_app(tmp_path, monkeypatch):
+    """control/wsgi.py exposes ``application`` (reference master/master/wsgi.py) built from
+    the environment; it serves the reference routes."""
+    import importlib
+    import sys
+    monkeypatch.setenv("MASTER_DB", str(tmp_path / "w.sqlite3"))
+    monkeypatch.setenv("MODEL_CACHE_DIR", str(tmp_path / "cache"))
+    monkeypatch.setenv("DLI_LOG_DIR", str(tmp_path / "logs"))
+    sys.modules.pop("distributed_llm_inferencing_amd.control.wsgi", None)
+    mod = importlib.import_module("distributed_llm_inferencing_amd.control.wsgi")
+    try:
+        c = mod.application.test_client()
+        assert c.get("/").status_code == 200
+        assert c.get("/api/nodes/status/").get_json() == {"nodes": []}
+        r = c.post("/api/inference/submit/", data={"model_name": "gpt2", "prompt": "x"})
+        assert r.get_json()["status"] == "success"
+    finally:
+        mod.application.extensions["dli"].shutdown()
+        sys.modules.pop("distributed_llm_inferencing_amd.control.wsgi", None)
 
 
 def test_failover_and_no_nodes(tmp_path, master):
