@@ -44,6 +44,13 @@ class Dispatcher:
         self.max_attempts = max_attempts
         self.on_node_error = on_node_error
         self.http = session or requests.Session()
+        if session is None:
+            # one pooled keep-alive connection per consumer thread (urllib3 keeps 10 per
+            # host by default: the rest were opened and discarded per request)
+            ad = requests.adapters.HTTPAdapter(pool_connections=16,
+                                               pool_maxsize=max(16, num_workers))
+            self.http.mount("http://", ad)
+            self.http.mount("https://", ad)
         self.inflight: Dict[int, int] = defaultdict(int)
         self._lock = threading.Lock()
         self._stop = threading.Event()

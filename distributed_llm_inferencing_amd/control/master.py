@@ -252,7 +252,11 @@ def create_master_app(settings: Optional[Settings] = None, store: Optional[Store
     @app.get("/api/inference/status/<int:request_id>/")
     def inference_status(request_id):
         try:
-            r = store.get_request(request_id)
+            # optional long poll (?wait=<s>, <= 60): answer when the request completes or
+            # fails, or after the wait — one call per request instead of a polling storm;
+            # without it the route answers at once, as the reference's does
+            wait = min(float(request.args.get("wait", 0) or 0), 60.0)
+            r = store.wait_final(request_id, wait) if wait > 0 else store.get_request(request_id)
             return jsonify({"id": r["id"], "status": r["status"], "model_name": r["model_name"],
                             "prompt": r["prompt"], "result": r["result"], "error": r["error"],
                             "created_at": r["created_at"], "completed_at": r["completed_at"]})

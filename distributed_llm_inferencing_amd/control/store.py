@@ -81,6 +81,7 @@ class Store:
     def __init__(self, path: str = ":memory:"):
         self.path = path
         self._lock = threading.RLock()
+        self._final = threading.Condition()      # signalled when a request completes / fails
         self._local = threading.local()
         self._shared = None
         if path == ":memory:":
@@ -216,10 +217,30 @@ class Store:
     def mark_completed(self, rid: int, result: str, execution_time: Optional[float] = None):
         self._exec("UPDATE inference_request SET status='completed', result=?, completed_at=?, "
                    "execution_time=? WHERE id=?", (result, now_iso(), execution_time, rid))
+        self._notify_final()
 
     def mark_failed(self, rid: int, error: str):
         self._exec("UPDATE inference_request SET status='failed', error=?, completed_at=? "
                    "WHERE id=?", (error, now_iso(), rid))
+        self._notify_final()
+
+    def _notify_final(self):
+        with self._final:
+            self._final.notify_all()
+
+    def wait_final(self, rid: int, timeout_s: float) -> Dict[str, Any]:
+        """The request's row once it is completed / failed, or as it stands after
+        ``timeout_s`` (long-poll support for the status API). Woken by this process's
+        dispatcher; rows finished by another process are seen within 0.1 s."""
+        import time as _t
+        deadline = _t.monotonic() + max(0.0, timeout_s)
+        while True:
+            r = self.get_request(rid)
+            left = deadline - _t.monotonic()
+            if r["status"] in ("completed", "failed") or left <= 0:
+                return r
+            with self._final:
+                self._final.wait(min(left, 0.1))
 
     def requeue(self, rid: int):
         self._exec("UPDATE inference_request SET status='pending', node_id=NULL WHERE id=?", (rid,))

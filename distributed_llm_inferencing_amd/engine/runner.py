@@ -50,12 +50,13 @@ class StageRunner:
     def _init_static(self):
         B, W = self.max_batch, self.W
         # layout (int32 words):
-        #   ids | pos | slots | ctx | temp | topk | topp | seeds(2B) | src | tables(B*W)
-        # src = lookahead feed rows (StepMeta.feed_src, -1 = host id)
+        #   seeds(2B) | ids | pos | slots | ctx | temp | topk | topp | src | tables(B*W)
+        # seeds first: an int64 view needs an even word offset whatever B is (B = 1 put it at
+        # word 7); src = lookahead feed rows (StepMeta.feed_src, -1 = host id)
         self._off = {}
         o = 0
-        for name, n in (("ids", B), ("pos", B), ("slots", B), ("ctx", B), ("temp", B),
-                        ("topk", B), ("topp", B), ("seeds", 2 * B), ("src", B),
+        for name, n in (("seeds", 2 * B), ("ids", B), ("pos", B), ("slots", B), ("ctx", B),
+                        ("temp", B), ("topk", B), ("topp", B), ("src", B),
                         ("tables", B * W)):
             self._off[name] = (o, n)
             o += n

@@ -19,6 +19,7 @@ later from prompt + generated tokens).
 from __future__ import annotations
 
 import itertools
+import os
 import time
 import zlib
 from collections import deque
@@ -141,7 +142,8 @@ class Scheduler:
     def __init__(self, block_manager: BlockManager, max_seqs_per_mb: int = 256,
                  max_prefill_tokens: int = 16384, num_microbatches: int = 1,
                  eos_token_id: Optional[int] = None, max_model_len: int = 4096,
-                 table_width: Optional[int] = None, native_decode: bool = False):
+                 table_width: Optional[int] = None, native_decode: bool = False,
+                 admit_window_s: Optional[float] = None, admit_min_frac: float = 0.125):
         self.bm = block_manager
         self.bs = block_manager.block_size
         self.max_seqs = max_seqs_per_mb
@@ -158,6 +160,14 @@ class Scheduler:
         self.finished: List[Sequence] = []
         # decode fast path in C++ (runtime.DecodeCore) for microbatches without stop tokens
         self.native_decode = native_decode
+        # admission window: while a microbatch is decoding, a prefill step for it waits until
+        # max(1, admit_min_frac * max_seqs) requests are queued (or as many as fit) or the
+        # oldest has waited admit_window_s. A prefill streams every weight like a decode step
+        # does, so admitting requests one by one as they trickle in over HTTP halves decode
+        # throughput; the window bounds the added time-to-first-token instead.
+        self.admit_window_s = (float(os.environ.get("DLI_ADMIT_WINDOW_S", "0.02"))
+                               if admit_window_s is None else admit_window_s)
+        self.admit_min = max(1, int(admit_min_frac * max_seqs_per_mb))
         self._next_id = 0
         self._step = 0
         self._deadlines = 0
@@ -290,6 +300,11 @@ class Scheduler:
     def _try_prefill(self, mb: int) -> Optional[StepMeta]:
         if not self.waiting or (self.M > 1 and not self._least_loaded_ok(mb)):
             return None
+        if self.running[mb] and self.admit_window_s > 0:
+            want = min(self.admit_min, self.max_seqs - len(self.running[mb]))
+            if (len(self.waiting) < want and
+                    time.perf_counter() - self.waiting[0].arrival < self.admit_window_s):
+                return None                  # keep decoding; batch the arrivals
         picked: List[Sequence] = []
         lens_l: List[int] = []
         tokens = 0

@@ -7,7 +7,8 @@ throughput, output tokens/s, and p50/p99 end-to-end latency (submit -> completed
 queueing, dispatch, the worker's continuous batching and the HTTP hops). Two modes:
 
     closed loop   --concurrency C: C clients, each submits its next request when the last
-                  one finished
+                  one finished (completion seen by a long poll of the status API, or by
+                  polling every --poll seconds as the reference UI does every 2 s)
     open loop     --rate R: Poisson arrivals at R requests/s
 
     python -m distributed_llm_inferencing_amd.loadgen --master http://127.0.0.1:8000 \\
@@ -40,6 +41,9 @@ class LoadGen:
         self.master = master.rstrip("/")
         self.model = model
         self.http = session or requests.Session()
+        if session is None:
+            ad = requests.adapters.HTTPAdapter(pool_maxsize=1024)
+            self.http.mount("http://", ad)
         self.poll_s, self.timeout_s = poll_s, timeout_s
         self.lock = threading.Lock()
         self.results: List[Dict] = []
@@ -52,10 +56,16 @@ class LoadGen:
         rid = r.json()["request_id"]
         st = {}
         while time.perf_counter() - t0 < self.timeout_s:
-            st = self.http.get(f"{self.master}/api/inference/status/{rid}/", timeout=30).json()
+            if self.poll_s <= 0:          # long poll: the master answers on completion
+                st = self.http.get(f"{self.master}/api/inference/status/{rid}/",
+                                   params={"wait": 30}, timeout=60).json()
+            else:
+                st = self.http.get(f"{self.master}/api/inference/status/{rid}/",
+                                   timeout=30).json()
             if st.get("status") in ("completed", "failed"):
                 break
-            time.sleep(self.poll_s)
+            if self.poll_s > 0:
+                time.sleep(self.poll_s)
         res = {"id": rid, "status": st.get("status", "timeout"),
                "latency_s": time.perf_counter() - t0,
                "execution_time": st.get("execution_time"),
@@ -108,7 +118,8 @@ def main(argv=None):
     ap.add_argument("--rate", type=float, default=0.0, help="open loop (requests/s) if > 0")
     ap.add_argument("--prompt-words", type=int, default=24)
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--poll", type=float, default=0.05, help="status poll interval (s)")
+    ap.add_argument("--poll", type=float, default=0.0,
+                    help="status poll interval (s); 0 = long poll (?wait=30)")
     ap.add_argument("--tokens-per-request", type=int, default=0,
                     help="report output tokens/s (requests generate a fixed count)")
     a = ap.parse_args(argv)

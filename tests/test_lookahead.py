@@ -70,3 +70,29 @@ def test_scheduler_schedules_one_step_ahead():
     assert [q.request_id for q in s.pop_finished()] == ["a"]
     s.update(nxt, np.array([9], np.int32))
     assert s.seqs[pre.seq_ids[1]].output_ids == [8, 9]
+
+
+def test_admission_window_batches_trickling_arrivals():
+    """While decoding, a lone arrival waits (up to the window) for more arrivals instead of
+    triggering a one-request prefill; after the window it is admitted; with nothing running
+    it is admitted at once."""
+    import time
+    bm = BlockManager(256, 16)
+    s = Scheduler(bm, max_seqs_per_mb=16, max_model_len=128, admit_window_s=0.05,
+                  admit_min_frac=0.25)                       # want 4 arrivals
+    s.add_request("a", [1, 2, 3], SamplingParams(max_new_tokens=50))
+    m = s.schedule(0)
+    assert m.kind == 1                                        # idle engine: admitted at once
+    s.update(m, np.array([5], np.int32))
+    s.add_request("b", [4, 5], SamplingParams(max_new_tokens=50))
+    assert s.schedule(0).kind == 2                            # decode; "b" waits
+    for i in range(3):
+        s.add_request(f"c{i}", [6, 7], SamplingParams(max_new_tokens=50))
+    m = s.schedule(0)
+    assert m.kind == 1 and m.num_seqs == 4                    # batch of 4 arrivals
+    s.update(m, np.arange(4, dtype=np.int32) + 3)
+    s.add_request("d", [8], SamplingParams(max_new_tokens=5))
+    assert s.schedule(0).kind == 2
+    time.sleep(0.06)
+    m = s.schedule(0)
+    assert m.kind == 1 and m.num_seqs == 1                    # window expired
