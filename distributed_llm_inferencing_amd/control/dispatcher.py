@@ -62,6 +62,7 @@ class Dispatcher:
         # auto-loads on /inference, app.py:278-282). Dropped on any error from that node.
         self._loaded: set = set()
         self.load_calls = 0
+        self._cand_cache: Dict[str, tuple] = {}
 
     # ------------------------------------------------------------------ lifecycle
     def start(self):
@@ -105,15 +106,32 @@ class Dispatcher:
                               headers=self._headers())
 
     def _candidates(self, model_name: str):
-        """(nodes, shard_ids_by_node) — shard holders first, as in views.py:318-340."""
+        """(nodes, shard_ids_by_node) — shard holders first, as in views.py:318-340. The
+        node / shard rows are re-read when this process changed them (store topology
+        version) or after 0.5 s (another process, the heartbeat of a shared database): per-
+        request reads contended the store lock at hundreds of requests/s; the load order is
+        recomputed every time."""
+        now = time.monotonic()
+        ver = getattr(self.store, "topology_version", 0)
+        hit = self._cand_cache.get(model_name)
+        if hit is None or now - hit[0] > 0.5 or hit[1] != ver:
+            hit = (now, ver, self._candidates_uncached(model_name))
+            self._cand_cache[model_name] = hit
+        nodes, by_node = hit[2]
+        return self._pick(nodes), by_node
+
+    def invalidate_candidates(self) -> None:
+        self._cand_cache.clear()
+
+    def _candidates_uncached(self, model_name: str):
         shards = self.store.shards(model_name=model_name, loaded_only=True)
         if shards:
             by_node: Dict[int, List[int]] = defaultdict(list)
             for s in shards:
                 by_node[s["node_id"]].append(s["shard_id"])
             nodes = [n for n in self.store.list_nodes(active_only=True) if n["id"] in by_node]
-            return self._pick(nodes), by_node
-        return self._pick(self.store.list_nodes(active_only=True)), None
+            return nodes, by_node
+        return self.store.list_nodes(active_only=True), None
 
     # ------------------------------------------------------------------ the request path
     def process(self, rid: int) -> None:
@@ -195,3 +213,188 @@ class Dispatcher:
     def _forget(self, node_id: int) -> None:
         with self._lock:
             self._loaded = {k for k in self._loaded if k[0] != node_id}
+
+
+class AsyncDispatcher(Dispatcher):
+    """The same request path on ONE asyncio event loop (aiohttp) instead of one blocked
+    thread per in-flight request.
+
+    Each in-flight request holds its dispatcher thread for the whole generation (0.3-3 s)
+    in the threaded design; at 512 requests in flight that is 512 CPython threads plus the
+    HTTP server's, and the master topped out at ~130 requests/s with the GIL handing itself
+    around (~45 % of one core busy, most threads waiting to be scheduled). Here every worker
+    call is a coroutine on one loop; ``num_workers`` bounds the calls in flight (same
+    meaning as the thread count). Node selection, retries, load caching, messages and
+    timeouts are those of ``Dispatcher``."""
+
+    def start(self):
+        import asyncio
+        self._loop = asyncio.new_event_loop()
+        self._done = threading.Event()
+        t = threading.Thread(target=self._loop_main, name="dli-dispatch-aio", daemon=True)
+        t.start()
+        self._threads.append(t)
+
+    def stop(self, timeout: float = 5.0):
+        self._stop.set()
+        for t in self._threads:
+            t.join(timeout)
+
+    def _loop_main(self):
+        import asyncio
+        asyncio.set_event_loop(self._loop)
+        try:
+            self._loop.run_until_complete(self._main())
+        finally:
+            self._loop.close()
+
+    async def _main(self):
+        import asyncio
+        from concurrent.futures import ThreadPoolExecutor
+
+        import aiohttp
+        loop = asyncio.get_running_loop()
+        self._session = aiohttp.ClientSession(connector=aiohttp.TCPConnector(limit=0))
+        sem = asyncio.Semaphore(max(1, self.num_workers))
+        getter = ThreadPoolExecutor(1, thread_name_prefix="dli-dispatch-q")
+        # store calls wait on the store's database thread: run them off the loop, several at
+        # once, so the database thread can batch them into one transaction
+        self._dbpool = ThreadPoolExecutor(32, thread_name_prefix="dli-dispatch-db")
+        tasks = set()
+        try:
+            while not self._stop.is_set():
+                await sem.acquire()
+                free = 1
+                while free < 256 and not sem.locked():     # claim every free slot (burst)
+                    await sem.acquire()
+                    free += 1
+                rids = await loop.run_in_executor(getter, self.queue.get_many, free, 0.2)
+                for _ in range(free - len(rids)):
+                    sem.release()
+                for rid in rids:
+                    t = asyncio.create_task(self._process_async(rid, sem))
+                    tasks.add(t)
+                    t.add_done_callback(tasks.discard)
+        finally:
+            for t in list(tasks):
+                t.cancel()
+            await asyncio.gather(*tasks, return_exceptions=True)
+            await self._session.close()
+            getter.shutdown(wait=False)
+            self._dbpool.shutdown(wait=False)
+
+    async def _s(self, fn, *args):
+        """A store call, awaited without blocking the event loop: run on the store's database
+        thread itself when the store offers it (no thread hop), else on a small pool."""
+        import asyncio
+        submit = getattr(self.store, "submit", None)
+        if submit is not None:
+            return await asyncio.wrap_future(submit(lambda _c: fn(*args)))
+        return await asyncio.get_running_loop().run_in_executor(self._dbpool, fn, *args)
+
+    async def _process_async(self, rid: int, sem) -> None:
+        try:
+            await self.process_async(rid)
+        finally:
+            sem.release()
+            rel = getattr(self.queue, "release", None)
+            if rel:
+                rel(rid)
+
+    async def process_async(self, rid: int) -> None:
+        try:
+            req = await self._s(self.store.get_request, rid)
+        except KeyError:
+            return
+        model, prompt = req["model_name"], req["prompt"]
+        try:
+            nodes, shard_map = await self._s(self._candidates, model)
+            if not nodes:
+                await self._s(self.store.mark_processing, rid)
+                await self._s(self.store.mark_failed, rid, "No active nodes with loaded shards found"
+                                       if shard_map is not None else
+                                       "No active worker nodes available")
+                return
+            last_err = None
+            for node in nodes[: self.max_attempts]:
+                await self._s(self.store.mark_processing, rid, node["id"])
+                with self._lock:
+                    self.inflight[node["id"]] += 1
+                try:
+                    ok, err = await self._run_on_async(
+                        node, rid, model, prompt, shard_map[node["id"]] if shard_map else None)
+                finally:
+                    with self._lock:
+                        self.inflight[node["id"]] -= 1
+                if ok or err is None:
+                    return
+                last_err = err
+                if self.on_node_error:
+                    self.on_node_error(node["id"], err)
+            await self._s(self.store.mark_failed, rid, last_err or "all candidate nodes failed")
+        except Exception as e:  # noqa: BLE001 — views.py:445-455 fatal fallback
+            log.critical("Fatal error processing inference request %s: %s", rid, e)
+            try:
+                await self._s(self.store.mark_failed, rid, f"Fatal error: {e}")
+            except Exception:  # noqa: BLE001
+                pass
+        finally:
+            self.processed += 1
+
+    async def _post_async(self, node, path, payload, timeout):
+        import aiohttp
+        async with self._session.post(f"{node['url']}{path}", json=payload,
+                                      headers=self._headers(),
+                                      timeout=aiohttp.ClientTimeout(total=timeout)) as r:
+            return r.status, await r.text()
+
+    async def _run_on_async(self, node, rid, model, prompt, shard_ids):
+        import asyncio
+        import json as _json
+
+        import aiohttp
+        t0 = time.perf_counter()
+        try:
+            faults.check("dispatch.post")
+            if shard_ids is None and (node["id"], model) not in self._loaded:
+                self.load_calls += 1
+                st, text = await self._post_async(node, "/load_model", {"model_name": model},
+                                                  HTTP_LOAD_TIMEOUT)
+                if st != 200:
+                    await self._s(self.store.mark_failed, rid, f"Failed to load model: {text}")
+                    return False, None
+                with self._lock:
+                    self._loaded.add((node["id"], model))
+            payload = {"model_name": model, "prompt": prompt, "max_length": self.max_length,
+                       "timeout": WORKER_TIMEOUT}
+            if shard_ids is not None:
+                payload["shard_ids"] = sorted(shard_ids)
+            st, text = await self._post_async(node, "/inference", payload, HTTP_INFER_TIMEOUT)
+        except (aiohttp.ClientError, asyncio.TimeoutError, OSError,
+                faults.InjectedFault) as e:
+            self._forget(node["id"])
+            return False, f"Connection error: {e}"
+        if st == 200:
+            data = _json.loads(text)
+            if data.get("status") == "success":
+                await self._s(self.store.mark_completed, rid, data.get("result", ""),
+                              data.get("execution_time", time.perf_counter() - t0))
+                return True, None
+            await self._s(self.store.mark_failed, rid, data.get("message", "Unknown error"))
+            return False, None
+        self._forget(node["id"])
+        await self._s(self.store.mark_failed, rid, f"Node returned status code {st}: {text}")
+        return False, None
+
+
+def make_dispatcher(store, queue, settings, **kw) -> Dispatcher:
+    """The asyncio dispatcher when aiohttp is importable (``DLI_DISPATCH=threads`` forces
+    the thread pool)."""
+    import os
+    if os.environ.get("DLI_DISPATCH", "async") != "threads":
+        try:
+            import aiohttp  # noqa: F401
+            return AsyncDispatcher(store, queue, settings, **kw)
+        except ImportError:
+            pass
+    return Dispatcher(store, queue, settings, **kw)

@@ -17,8 +17,9 @@ Routes, form fields, JSON shapes, status codes and messages follow
 Additions: POST /api/shards/register/ (the only way the reference could create ModelShard
 rows was the Django admin), POST /api/shards/delete/<id>/, GET /api/shards/,
 GET /metrics (queue depth, request counts, dispatcher stats), GET /healthz.
-Submissions go to a request queue drained by a fixed dispatcher pool (no thread per
-request); a background heartbeat monitor keeps node state fresh.
+Submissions go to a request queue drained by the dispatcher (one asyncio loop for every
+in-flight worker call; no thread per request); a background heartbeat monitor keeps node
+state fresh. GET /api/inference/status/<id>/?wait=<s> long-polls until completion.
 """
 from __future__ import annotations
 
@@ -31,7 +32,7 @@ import requests
 from flask import Flask, jsonify, render_template, request, session
 
 from ..config import Settings, get_settings
-from .dispatcher import Dispatcher
+from .dispatcher import make_dispatcher
 from .health import HealthMonitor, probe
 from .queue import make_queue
 from .store import NotFound, Store, now_iso
@@ -47,9 +48,10 @@ class MasterState:
         self.store = store
         self.queue = make_queue(settings.queue_backend, store, settings)
         self.health = HealthMonitor(store, settings, interval=health_interval)
-        self.dispatcher = Dispatcher(store, self.queue, settings,
-                                     num_workers=dispatch_workers or settings.dispatch_workers,
-                                     on_node_error=self.health.report_failure)
+        self.dispatcher = make_dispatcher(store, self.queue, settings,
+                                          num_workers=dispatch_workers or
+                                          settings.dispatch_workers,
+                                          on_node_error=self.health.report_failure)
         recovered = store.recover("requeue")
         for rid in store.pending_ids():
             self.queue.put(rid)
@@ -334,12 +336,18 @@ def main(argv=None):
     ap.add_argument("--port", type=int, default=8000)
     ap.add_argument("--server", default="werkzeug", choices=["werkzeug", "uvicorn"],
                     help="werkzeug: threaded WSGI server (a thread per connection); uvicorn: "
-                         "its WSGI interface over the module-level app (control/wsgi.py)")
+                         "ASGI front (control/asgi.py: async status long polls) over the "
+                         "same Flask app")
     a = ap.parse_args(argv)
     if a.server == "uvicorn":
+        # ASGI front: status long polls as coroutines, the Flask app behind a WSGI adapter
         import uvicorn
-        uvicorn.run("distributed_llm_inferencing_amd.control.wsgi:application",
-                    interface="wsgi", host=a.host, port=a.port, log_level="warning")
+
+        from .asgi import create_asgi_app
+        from ..utils.log import setup_logging
+        setup_logging("master")
+        uvicorn.run(create_asgi_app(create_master_app()), host=a.host, port=a.port,
+                    log_level="warning", timeout_keep_alive=75, backlog=4096)
         return
     from ..utils.log import setup_logging
     setup_logging("master")

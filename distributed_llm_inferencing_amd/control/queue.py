@@ -27,6 +27,20 @@ class RequestQueue:
     def get(self, timeout: float = 1.0) -> Optional[int]:
         raise NotImplementedError
 
+    def get_many(self, max_n: int, timeout: float = 1.0) -> list:
+        """Up to ``max_n`` ids: waits for the first, then takes what is already queued (the
+        asyncio dispatcher drains a burst per hop to its loop)."""
+        first = self.get(timeout)
+        if first is None:
+            return []
+        out = [first]
+        while len(out) < max_n:
+            nxt = self.get(0.0)
+            if nxt is None:
+                break
+            out.append(nxt)
+        return out
+
     def qsize(self) -> int:
         return 0
 
@@ -45,6 +59,8 @@ class InProcQueue(RequestQueue):
 
     def get(self, timeout: float = 1.0) -> Optional[int]:
         try:
+            if timeout <= 0:
+                return self._q.get_nowait()
             return self._q.get(timeout=timeout)
         except _q.Empty:
             return None

@@ -11,14 +11,16 @@ Mirrors the Django models of the reference (``master/dashboard/models.py:4-62``)
                   with mark_completed / mark_failed.
 
 The reference has no migrations directory, so its tables would not exist
-after ``migrate``; here the schema is created on startup. One connection per thread with a
-process-wide write lock (the reference mutated sqlite from unbounded threads, §5.2).
+after ``migrate``; here the schema is created on startup. One database thread owns the
+connection and serialises every access (the reference mutated sqlite from unbounded
+threads, §5.2).
 Extensions: node ``resources``/``gpu_id``/``role`` columns, request timing + node columns,
 and ``recover()`` which re-queues requests orphaned in ``processing`` by a restart (§5.4).
 """
 from __future__ import annotations
 
 import json
+import queue
 import sqlite3
 import threading
 from datetime import datetime, timezone
@@ -77,44 +79,114 @@ class NotFound(KeyError):
     pass
 
 
+class _Call:
+    __slots__ = ("fn", "ev", "result", "error", "fut")
+
+    def __init__(self, fn, fut=None):
+        self.fn, self.ev, self.result, self.error = fn, threading.Event(), None, None
+        self.fut = fut                      # concurrent.futures.Future for async callers
+
+
+class _Exec:
+    __slots__ = ("lastrowid", "rowcount")
+
+    def __init__(self, cur):
+        self.lastrowid, self.rowcount = cur.lastrowid, cur.rowcount
+
+
 class Store:
+    """The connection is owned by ONE database thread; every other thread hands it a call
+    and sleeps until it is done. The thread runs the calls queued meanwhile in one
+    transaction (one commit per batch). With hundreds of dispatcher and HTTP threads a
+    shared lock around the connection convoyed on the GIL (the holder re-acquires it after
+    each sqlite call): the master topped out at ~140 requests/s; the single owner has no
+    lock to contend for and batches the commits."""
+
     def __init__(self, path: str = ":memory:"):
         self.path = path
-        self._lock = threading.RLock()
-        self._final = threading.Condition()      # signalled when a request completes / fails
-        self._local = threading.local()
-        self._shared = None
-        if path == ":memory:":
-            # one shared connection (an in-memory db is per-connection)
-            self._shared = sqlite3.connect(":memory:", check_same_thread=False)
-            self._shared.row_factory = sqlite3.Row
-            self._shared.execute("PRAGMA foreign_keys = ON")
-        with self._lock:
-            self._conn().executescript(_SCHEMA)
-            self._conn().commit()
+        self._waiters: Dict[int, threading.Event] = {}   # long polls, by request id
+        self._awaiters: Dict[int, list] = {}             # asyncio long polls: [(loop, fut)]
+        self._wlock = threading.Lock()
+        # rows of requests in a TERMINAL state (completed / failed never change again, so
+        # the copy cannot go stale even when other processes share the database): status
+        # reads of finished requests skip the database
+        self._final_rows: Dict[int, Dict[str, Any]] = {}
+        self.topology_version = 0
+        self._q: "queue.SimpleQueue[_Call]" = queue.SimpleQueue()
+        self._conn_obj: Optional[sqlite3.Connection] = None
+        ready = threading.Event()
+        self._t = threading.Thread(target=self._run, args=(ready,), name="dli-store", daemon=True)
+        self._t.start()
+        ready.wait()
+        self._call(lambda c: c.executescript(_SCHEMA))
 
-    def _conn(self) -> sqlite3.Connection:
-        if self._shared is not None:
-            return self._shared
-        c = getattr(self._local, "conn", None)
-        if c is None:
-            c = sqlite3.connect(self.path, timeout=30, check_same_thread=False)
-            c.row_factory = sqlite3.Row
-            c.execute("PRAGMA foreign_keys = ON")
+    # ------------------------------------------------------------------ the db thread
+    def _run(self, ready: threading.Event):
+        # File databases run in WAL mode with synchronous=NORMAL (a commit appends to the
+        # WAL without an fsync); other processes (a second master worker, the sqlite queue)
+        # share the file safely.
+        c = sqlite3.connect(self.path, timeout=30, check_same_thread=False)
+        c.row_factory = sqlite3.Row
+        c.execute("PRAGMA foreign_keys = ON")
+        if self.path != ":memory:":
             c.execute("PRAGMA journal_mode = WAL")
-            self._local.conn = c
-        return c
+            c.execute("PRAGMA synchronous = NORMAL")
+        self._conn_obj = c
+        self._tid = threading.get_ident()
+        ready.set()
+        while True:
+            batch = [self._q.get()]
+            while len(batch) < 256:
+                try:
+                    batch.append(self._q.get_nowait())
+                except queue.Empty:
+                    break
+            for call in batch:
+                try:
+                    call.result = call.fn(c)
+                except BaseException as e:  # noqa: BLE001 — returned to the caller
+                    call.error = e
+            try:
+                c.commit()
+            except sqlite3.Error as e:
+                for call in batch:
+                    call.error = call.error or e
+            for call in batch:
+                if call.fut is not None:
+                    if call.error is not None:
+                        call.fut.set_exception(call.error)
+                    else:
+                        call.fut.set_result(call.result)
+                call.ev.set()
+
+    def _call(self, fn):
+        if threading.get_ident() == getattr(self, "_tid", None):
+            return fn(self._conn_obj)                     # nested call on the db thread
+        call = _Call(fn)
+        self._q.put(call)
+        call.ev.wait()
+        if call.error is not None:
+            raise call.error
+        return call.result
+
+    def submit(self, fn) -> "concurrent.futures.Future":
+        """Run fn(connection) on the database thread; returns a Future (asyncio callers
+        await it with ``asyncio.wrap_future`` instead of blocking a thread)."""
+        import concurrent.futures
+        fut: concurrent.futures.Future = concurrent.futures.Future()
+        self._q.put(_Call(fn, fut))
+        return fut
 
     def _exec(self, sql: str, args=()):
-        with self._lock:
-            c = self._conn()
-            cur = c.execute(sql, args)
-            c.commit()
-            return cur
+        def run(c):
+            r = _Exec(c.execute(sql, args))
+            if "worker_node" in sql or "model_shard" in sql:
+                self.topology_version += 1           # node / shard rows changed
+            return r
+        return self._call(run)
 
     def _query(self, sql: str, args=()) -> List[Dict[str, Any]]:
-        with self._lock:
-            return [dict(r) for r in self._conn().execute(sql, args).fetchall()]
+        return self._call(lambda c: [dict(r) for r in c.execute(sql, args).fetchall()])
 
     # ------------------------------------------------------------------ nodes
     def add_node(self, hostname: str, ip_address: str, port: int = 5000, is_active=False,
@@ -166,7 +238,8 @@ class Store:
     def add_shard(self, node_id: int, model_name: str, shard_id: int, is_loaded=False,
                   path: Optional[str] = None) -> int:
         t = now_iso()
-        with self._lock:
+
+        def tx(_c):
             existing = self._query("SELECT id FROM model_shard WHERE model_name=? AND shard_id=?",
                                    (model_name, shard_id))
             if existing:
@@ -178,6 +251,7 @@ class Store:
                              "path, created_at, updated_at) VALUES (?,?,?,?,?,?,?)",
                              (node_id, model_name, int(shard_id), int(bool(is_loaded)), path, t, t))
             return int(cur.lastrowid)
+        return self._call(tx)
 
     def shards(self, model_name: Optional[str] = None, node_id: Optional[int] = None,
                loaded_only: bool = False) -> List[Dict[str, Any]]:
@@ -205,44 +279,114 @@ class Store:
         return int(cur.lastrowid)
 
     def get_request(self, rid: int) -> Dict[str, Any]:
+        r = self._final_rows.get(rid)
+        if r is not None:
+            return dict(r)
         rows = self._query("SELECT * FROM inference_request WHERE id=?", (rid,))
         if not rows:
             raise NotFound(f"No InferenceRequest matches the given query (id={rid}).")
+        if rows[0]["status"] in ("completed", "failed"):
+            self._remember_final(rows[0])
         return rows[0]
+
+    def _remember_final(self, row: Dict[str, Any]) -> None:
+        if len(self._final_rows) > 200_000:           # bounded: drop the oldest half
+            for k in sorted(self._final_rows)[:100_000]:
+                self._final_rows.pop(k, None)
+        self._final_rows[int(row["id"])] = dict(row)
 
     def mark_processing(self, rid: int, node_id: Optional[int] = None):
         self._exec("UPDATE inference_request SET status='processing', started_at=?, node_id=?, "
                    "attempts=attempts+1 WHERE id=?", (now_iso(), node_id, rid))
 
     def mark_completed(self, rid: int, result: str, execution_time: Optional[float] = None):
-        self._exec("UPDATE inference_request SET status='completed', result=?, completed_at=?, "
-                   "execution_time=? WHERE id=?", (result, now_iso(), execution_time, rid))
-        self._notify_final()
+        def tx(_c):
+            self._exec("UPDATE inference_request SET status='completed', result=?, "
+                       "completed_at=?, execution_time=? WHERE id=?",
+                       (result, now_iso(), execution_time, rid))
+            return self._query("SELECT * FROM inference_request WHERE id=?", (rid,))
+        rows = self._call(tx)
+        if rows:
+            self._remember_final(rows[0])
+        self._notify_final(rid)
 
     def mark_failed(self, rid: int, error: str):
-        self._exec("UPDATE inference_request SET status='failed', error=?, completed_at=? "
-                   "WHERE id=?", (error, now_iso(), rid))
-        self._notify_final()
+        def tx(_c):
+            self._exec("UPDATE inference_request SET status='failed', error=?, completed_at=? "
+                       "WHERE id=?", (error, now_iso(), rid))
+            return self._query("SELECT * FROM inference_request WHERE id=?", (rid,))
+        rows = self._call(tx)
+        if rows:
+            self._remember_final(rows[0])
+        self._notify_final(rid)
 
-    def _notify_final(self):
-        with self._final:
-            self._final.notify_all()
+    def _notify_final(self, rid: int):
+        with self._wlock:
+            ev = self._waiters.get(rid)
+            aws = self._awaiters.pop(rid, None)
+        if ev is not None:
+            ev.set()
+        for loop, fut in aws or ():
+            loop.call_soon_threadsafe(lambda f=fut: f.done() or f.set_result(True))
+
+    async def wait_final_async(self, rid: int, timeout_s: float) -> Dict[str, Any]:
+        """``wait_final`` for asyncio servers: no thread is held while waiting."""
+        import asyncio
+        loop = asyncio.get_running_loop()
+        fut = loop.create_future()
+        with self._wlock:
+            self._awaiters.setdefault(rid, []).append((loop, fut))
+        deadline = loop.time() + max(0.0, timeout_s)
+        try:
+            while True:
+                r = self._final_rows.get(rid)
+                if r is None:
+                    r = await asyncio.wrap_future(self.submit(
+                        lambda c: [dict(x) for x in c.execute(
+                            "SELECT * FROM inference_request WHERE id=?", (rid,)).fetchall()]))
+                    if not r:
+                        raise NotFound(f"No InferenceRequest matches the given query (id={rid}).")
+                    r = r[0]
+                else:
+                    r = dict(r)
+                left = deadline - loop.time()
+                if r["status"] in ("completed", "failed") or left <= 0:
+                    return r
+                try:
+                    await asyncio.wait_for(asyncio.shield(fut), min(left, 2.0))
+                except asyncio.TimeoutError:
+                    pass
+        finally:
+            with self._wlock:
+                lst = self._awaiters.get(rid)
+                if lst is not None:
+                    lst[:] = [x for x in lst if x[1] is not fut]
+                    if not lst:
+                        self._awaiters.pop(rid, None)
 
     def wait_final(self, rid: int, timeout_s: float) -> Dict[str, Any]:
         """The request's row once it is completed / failed, or as it stands after
-        ``timeout_s`` (long-poll support for the status API). Woken by this process's
-        dispatcher; rows finished by another process are seen within 0.1 s."""
+        ``timeout_s`` (long-poll support for the status API). Each waiter sleeps on its own
+        request's event, set by this process's dispatcher (no thundering herd); a row
+        finished by another process is seen within 2 s."""
         import time as _t
         deadline = _t.monotonic() + max(0.0, timeout_s)
-        while True:
-            r = self.get_request(rid)
-            left = deadline - _t.monotonic()
-            if r["status"] in ("completed", "failed") or left <= 0:
-                return r
-            with self._final:
-                self._final.wait(min(left, 0.1))
+        with self._wlock:
+            ev = self._waiters.setdefault(rid, threading.Event())
+        try:
+            while True:
+                r = self.get_request(rid)       # served from the terminal-row cache once set
+                left = deadline - _t.monotonic()
+                if r["status"] in ("completed", "failed") or left <= 0:
+                    return r
+                ev.wait(min(left, 2.0))
+        finally:
+            with self._wlock:
+                if self._waiters.get(rid) is ev:
+                    del self._waiters[rid]
 
     def requeue(self, rid: int):
+        self._final_rows.pop(rid, None)
         self._exec("UPDATE inference_request SET status='pending', node_id=NULL WHERE id=?", (rid,))
 
     def recent_requests(self, n: int = 10) -> List[Dict[str, Any]]:

@@ -207,6 +207,25 @@ class WorkerState:
                 "device": self.device_str, **extra}
 
 
+def request_params(data: dict):
+    """(SamplingParams, timeout) of an /inference body: the reference's generate() call
+    (worker/app.py:297-305: do_sample, T 0.8, top-k 50, top-p 0.95, max_length incl. the
+    prompt) with the optional overrides this API adds."""
+    max_length = int(data.get("max_length", 100))
+    timeout = float(data.get("timeout", 60))
+    params = SamplingParams(max_length=max_length, temperature=0.8, top_k=50, top_p=0.95,
+                            timeout_s=timeout)
+    for k in ("temperature", "top_k", "top_p", "seed", "max_new_tokens"):
+        if k in data:
+            setattr(params, k, data[k])
+    return params, timeout
+
+
+def success_body(out, t0: float) -> dict:
+    return {"status": "success", "result": out.resolve_text(), "execution_time": time.time() - t0,
+            "output_tokens": len(out.output_ids), "finish_reason": out.finish_reason}
+
+
 def create_worker_app(settings: Optional[Settings] = None, device: Optional[str] = None,
                       engine_kwargs: Optional[dict] = None, state: Optional[WorkerState] = None):
     settings = settings or get_settings()
@@ -298,15 +317,9 @@ def create_worker_app(settings: Optional[Settings] = None, device: Optional[str]
         if not name or not prompt:
             return jsonify({"status": "error",
                             "message": "Model name and prompt are required"}), 400
-        max_length = int(data.get("max_length", 100))
-        timeout = float(data.get("timeout", 60))
         shard_ids = data.get("shard_ids")
         t0 = time.time()
-        params = SamplingParams(max_length=max_length, temperature=0.8, top_k=50, top_p=0.95,
-                                timeout_s=timeout)
-        for k in ("temperature", "top_k", "top_p", "seed", "max_new_tokens"):
-            if k in data:
-                setattr(params, k, data[k])
+        params, timeout = request_params(data)
         try:
             faults.check("worker.inference")
             svc = getattr(st, "pipeline_service", None)
@@ -327,10 +340,7 @@ def create_worker_app(settings: Optional[Settings] = None, device: Optional[str]
                 out = st.services[name].generate(prompt, params, timeout=timeout + 30)
             if out.finish_reason == "timeout":
                 raise TimeoutError("Inference generation timed out")
-            return jsonify({"status": "success", "result": out.resolve_text(),
-                            "execution_time": time.time() - t0,
-                            "output_tokens": len(out.output_ids),
-                            "finish_reason": out.finish_reason})
+            return jsonify(success_body(out, t0))
         except TimeoutError as e:
             return jsonify({"status": "error", "message": str(e)}), 408
         except Exception as e:  # noqa: BLE001
@@ -389,6 +399,9 @@ def main(argv=None):
     ap.add_argument("--gpu", type=int, default=None, help="GPU index (implies USE_GPU=1)")
     ap.add_argument("--preload", default="", help="comma-separated models to load at start")
     ap.add_argument("--max-batch", type=int, default=None)
+    ap.add_argument("--server", default="werkzeug", choices=["werkzeug", "uvicorn"],
+                    help="uvicorn: ASGI front (worker/asgi.py: /inference as a coroutine per "
+                         "request) over the same Flask app")
     a = ap.parse_args(argv)
     setup_logging(f"worker{a.port}")
     s = get_settings()
@@ -400,6 +413,13 @@ def main(argv=None):
     app = create_worker_app(s, dev, kw)
     for m in [m for m in a.preload.split(",") if m]:
         app.extensions["dli_worker"].load_model(m)
+    if a.server == "uvicorn":
+        import uvicorn
+
+        from .asgi import create_asgi_app
+        uvicorn.run(create_asgi_app(app), host=a.host, port=a.port, log_level="warning",
+                    timeout_keep_alive=75, backlog=4096)
+        return
     app.run(host=a.host, port=a.port, threaded=True)
 
 

@@ -10,14 +10,14 @@
 # (N requests), then concurrency 1 (latency of a lone request through every hop).
 # Usage: bash scripts/serve_e2e.sh [requests] [concurrency] [max_batch] [server]
 set -u
-N=${1:-1024}; C=${2:-512}; B=${3:-512}; SRV=${4:-werkzeug}
+N=${1:-1024}; C=${2:-512}; B=${3:-512}; SRV=${4:-uvicorn}
 mkdir -p gpurun_out/logs
 export MASTER_DB=/tmp/dli_e2e_$$.sqlite3 DLI_LOG_DIR=gpurun_out/logs DISPATCH_WORKERS=$C
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 python -m distributed_llm_inferencing_amd.cli serve-master --port 8000 --server $SRV \
     > gpurun_out/e2e_master.log 2>&1 &
 MPID=$!
-python -m distributed_llm_inferencing_amd.cli serve-worker --port 5000 --gpu 0 --max-batch $B \
+python -m distributed_llm_inferencing_amd.cli serve-worker --port 5000 --gpu 0 --max-batch $B --server $SRV \
     --preload llama3-8b > gpurun_out/e2e_worker.log 2>&1 &
 WPID=$!
 ok=0

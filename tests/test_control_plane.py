@@ -374,3 +374,80 @@ def test_worker_health_reports_failed_pipeline(worker):
     worker.application.extensions["dli_worker"].pipeline_service = _Broken()
     r = worker.get("/health")
     assert r.status_code == 503 and "stage 3 died" in r.get_json()["message"]
+
+
+def test_worker_asgi_front_matches_flask_route(tmp_path):
+    """serve-worker --server uvicorn: /inference as a coroutine gives the Flask route's
+    JSON / status codes (success, 400, 401, 408), other routes fall through to Flask."""
+    import asyncio
+    import httpx
+    from distributed_llm_inferencing_amd.worker.asgi import create_asgi_app
+    flask_app = create_worker_app(settings(tmp_path), device="cpu", engine_kwargs=SMALL)
+    flask_app.extensions["dli_worker"].load_model("llama-tiny")
+    app = create_asgi_app(flask_app)
+    body = {"model_name": "llama-tiny", "prompt": "Hello", "max_length": 20, "temperature": 0}
+
+    async def run():
+        tr = httpx.ASGITransport(app=app)
+        async with httpx.AsyncClient(transport=tr, base_url="http://w") as c:
+            outs = await asyncio.gather(*(c.post("/inference", json=body) for _ in range(4)))
+            h = await c.get("/health")
+            bad = await c.post("/inference", json={"model_name": "llama-tiny"})
+            late = await c.post("/inference", json={**body, "max_length": 120, "timeout": 0})
+            return outs, h, bad, late
+    outs, h, bad, late = asyncio.run(run())
+    want = flask_app.test_client().post("/inference", json=body).get_json()
+    for r in outs:
+        d = r.json()
+        assert r.status_code == 200 and d["result"] == want["result"]
+        assert d["output_tokens"] == want["output_tokens"] == 15
+    assert h.status_code == 200 and h.json()["loaded_models"] == ["llama-tiny"]
+    assert bad.status_code == 400 and bad.json()["message"] == "Model name and prompt are required"
+    assert late.status_code == 408
+    auth_app = create_worker_app(settings(tmp_path, auth_enabled=True, auth_key="k"),
+                                 device="cpu", engine_kwargs=SMALL)
+    auth_app.extensions["dli_worker"].load_model("llama-tiny")
+    aapp = create_asgi_app(auth_app)
+
+    async def run_auth():
+        async with httpx.AsyncClient(transport=httpx.ASGITransport(app=aapp),
+                                     base_url="http://w") as c:
+            return (await c.post("/inference", json=body),
+                    await c.post("/inference", json=body, headers={"Authorization": "Bearer k"}))
+    no, yes = asyncio.run(run_auth())
+    assert no.status_code == 401 and yes.status_code == 200
+
+
+def test_master_asgi_long_poll(tmp_path):
+    """serve-master --server uvicorn: ?wait= long polls answer on completion (no thread held);
+    plain status / pages go through the Flask app."""
+    import asyncio
+    import httpx
+    from distributed_llm_inferencing_amd.control.asgi import create_asgi_app
+    w = Server(create_worker_app(settings(tmp_path), device="cpu", engine_kwargs=SMALL))
+    flask_app = create_master_app(settings(tmp_path), start_background=True, dispatch_workers=4,
+                                  health_interval=0.5)
+    app = create_asgi_app(flask_app)
+
+    async def run():
+        async with httpx.AsyncClient(transport=httpx.ASGITransport(app=app),
+                                     base_url="http://m", timeout=120) as c:
+            r = await c.post("/api/nodes/add/", data={"hostname": "cpu0",
+                                                      "ip_address": "127.0.0.1", "port": w.port})
+            assert r.json()["status"] == "success"
+            rid = (await c.post("/api/inference/submit/", data={
+                "model_name": "gpt2-tiny", "prompt": "Hello"})).json()["request_id"]
+            now = (await c.get(f"/api/inference/status/{rid}/")).json()
+            done = (await c.get(f"/api/inference/status/{rid}/", params={"wait": 60})).json()
+            missing = await c.get("/api/inference/status/99999/", params={"wait": 1})
+            page = await c.get("/")
+            return now, done, missing, page
+    try:
+        now, done, missing, page = asyncio.run(run())
+    finally:
+        flask_app.extensions["dli"].shutdown()
+        w.close()
+    assert now["status"] in ("pending", "processing", "completed")
+    assert done["status"] == "completed" and done["result"].startswith("Hello")
+    assert missing.status_code == 500 and "No InferenceRequest" in missing.json()["message"]
+    assert page.status_code == 200
