@@ -8,7 +8,8 @@ kernel reads whole 32-token tiles and multiplies the masked ones by 0).
 """
 from __future__ import annotations
 
-from typing import List, Tuple
+import os
+from typing import List, Optional, Tuple
 
 import torch
 
@@ -24,15 +25,28 @@ def blocks_for_budget(cfg: ModelConfig, num_layers: int, block_size: int, budget
 
 
 def auto_num_blocks(cfg: ModelConfig, num_layers: int, block_size: int, device,
-                    fraction: float = 0.85, reserve_bytes: int = 4 << 30,
+                    fraction: float = 0.85, reserve_bytes: Optional[int] = None,
                     cap_tokens: int = 0) -> int:
-    """Blocks that fit in `fraction` of currently free HBM minus a reserve for activations."""
+    """Blocks that fit in ``fraction`` of the HBM still free (weights already resident)
+    minus a reserve for activations, GEMM workspaces and graph pools: the KV pool is sized
+    for the 288 GB of an MI355X (Llama-3-8B: ~1.7M tokens of context on one GPU), not for
+    max_batch x max_model_len. ``cap_tokens`` / ``DLI_KV_MAX_TOKENS`` cap it (0 = no cap).
+    Ranks sharing one device (``DLI_SAME_DEVICE=1`` rehearsals) split it by
+    ``LOCAL_WORLD_SIZE``."""
     dev = torch.device(device)
+    env_cap = int(os.environ.get("DLI_KV_MAX_TOKENS", "0") or 0)
+    cap_tokens = env_cap or cap_tokens
     if dev.type == "cuda":
-        free, _total = torch.cuda.mem_get_info(dev)
+        free, total = torch.cuda.mem_get_info(dev)
+        if reserve_bytes is None:
+            reserve_bytes = max(8 << 30, int(0.03 * total))
+        if os.environ.get("DLI_SAME_DEVICE", "0") == "1":
+            fraction /= max(1, int(os.environ.get("LOCAL_WORLD_SIZE",
+                                                  os.environ.get("WORLD_SIZE", "1"))))
         budget = max(0, int(free * fraction) - reserve_bytes)
     else:
-        budget = 256 << 20
+        budget = 256 << 20                  # CPU (tests / the gpt2 plumbing config)
+        cap_tokens = cap_tokens or (1 << 16)
     n = blocks_for_budget(cfg, max(1, num_layers), block_size, budget)
     if cap_tokens:
         n = min(n, -(-cap_tokens // block_size))

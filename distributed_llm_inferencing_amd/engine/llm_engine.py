@@ -91,7 +91,8 @@ class LLMEngine:
                  kv_fraction: float = 0.85, seed: int = 0, use_graphs: Optional[bool] = None,
                  params: Optional[Dict[str, torch.Tensor]] = None, tokenizer_path=None,
                  max_prefill_tokens: int = 16384, num_layers: Optional[int] = None,
-                 lm: Optional[TransformerLM] = None, lookahead: Optional[bool] = None):
+                 lm: Optional[TransformerLM] = None, lookahead: Optional[bool] = None,
+                 max_kv_tokens: Optional[int] = None):
         self.cfg = get_config(model, num_layers) if isinstance(model, str) else model
         self.device = torch.device(device)
         if self.device.type == "cuda" and self.device.index is None:
@@ -106,9 +107,9 @@ class LLMEngine:
                                        device=self.device)
         max_model_len = min(max_model_len, cfg.max_position)
         if num_blocks is None:
+            # KV pool sized from free HBM, optionally capped
             num_blocks = auto_num_blocks(cfg, cfg.num_layers, block_size, self.device,
-                                         kv_fraction,
-                                         cap_tokens=max(max_batch * max_model_len, 1 << 16))
+                                         kv_fraction, cap_tokens=max_kv_tokens or 0)
         self.kv = KVCache(cfg, cfg.num_layers, num_blocks, block_size, self.device, dtype)
         self.bm = BlockManager(num_blocks, block_size)
         self.scheduler = Scheduler(self.bm, max_seqs_per_mb=max_batch,

@@ -551,10 +551,9 @@ def build_stage(cfg: ModelConfig, rank: int, world: int, device, max_batch: int,
     params = (load_stage_params(shard_dir, rank, world, device, vs)
               if shard_dir is not None else None)
     if num_blocks is None:
-        # every sequence of the M microbatches in flight may reach max_model_len: size the
-        # pool for that (not a fraction of HBM: 288 GB would otherwise all go to KV)
-        cap = _stage_capacity_blocks(cfg, plan, block_size, device, kv_fraction,
-                                     cap_tokens=max(M * max_batch * max_model_len, 1 << 16))
+        # this stage's layers' KV from its free HBM (288 GB per MI355X); every stage holds
+        # the same block ids (the head's allocator), so all take the smallest pool
+        cap = _stage_capacity_blocks(cfg, plan, block_size, device, kv_fraction, cap_tokens=0)
         t = torch.tensor([cap], dtype=torch.int64,
                          device=device if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MIN)     # block ids are global: same pool size

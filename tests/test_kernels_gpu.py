@@ -495,3 +495,48 @@ def test_ep_pack_and_combine(gpu):
     out = ops.moe_combine(y, w, pos)
     ref = (y[p].float() * w.unsqueeze(-1)).sum(1)
     close(out, ref, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("lens,hq,hkv", [([2048, 300], 32, 8), ([8192], 8, 2)])
+def test_prefill_attention_long(gpu, lens, hq, hkv):
+    """Long prompts: 2k and 8k-token causal GQA prefill vs the fp32
+    reference (the 8k case with fewer heads so the fp32 reference's score matrix fits)."""
+    torch.manual_seed(21)
+    hd = 128
+    T = sum(lens)
+    qkv = rnd(T, (hq + 2 * hkv) * hd, dev=gpu)
+    cu = torch.tensor([0] + list(np.cumsum(lens)), device=gpu, dtype=torch.int32)
+    scale = 1 / math.sqrt(hd)
+    out = ops.prefill_attention(qkv, cu, max(lens), hq, hkv, hd, scale)
+    q, k, v = R.split_qkv(qkv, hq, hkv, hd)
+    ref = R.prefill_attention(q, k, v, cu, scale).reshape(T, -1)
+    close(out, ref, rtol=2e-2, atol=2e-2)
+
+
+def test_decode_attention_32k_context(gpu):
+    """Decode against a 32k-token paged context (and a short one in the same batch), with
+    the default split heuristic and forced splits."""
+    torch.manual_seed(22)
+    hq, hkv, hd, bs = 32, 8, 128, 16
+    lens = [32768, 77]
+    nblk = sum(-(-n // bs) for n in lens) + 4
+    kc = rnd(nblk, hkv, bs, hd, dev=gpu)
+    vc = rnd(nblk, hkv, bs, hd, dev=gpu)
+    perm = torch.randperm(nblk - 4, device=gpu).to(torch.int32)      # scattered blocks
+    maxb = -(-max(lens) // bs)
+    tables, o = [], 0
+    for n in lens:
+        nb = -(-n // bs)
+        tables.append(torch.cat([perm[o:o + nb], torch.zeros(maxb - nb, dtype=torch.int32,
+                                                               device=gpu)]))
+        o += nb
+    tables = torch.stack(tables)
+    qkv = rnd(len(lens), (hq + 2 * hkv) * hd, dev=gpu)
+    ctx = torch.tensor(lens, device=gpu, dtype=torch.int32)
+    scale = 1 / math.sqrt(hd)
+    q = qkv[:, : hq * hd].reshape(len(lens), hq, hd)
+    ref = R.decode_attention(q, kc, vc, tables, ctx, scale).reshape(len(lens), -1)
+    for splits in (None, 8, 32):
+        out = ops.decode_attention(qkv, kc, vc, tables, ctx, max(lens), hq, hkv, hd, scale,
+                                   num_splits=splits)
+        close(out, ref, rtol=2e-2, atol=2e-2)
