@@ -1,35 +1,48 @@
 // Causal variable-length (packed) GQA prefill attention on MFMA — SURVEY.md §2.4 K7.
 //
 // Reads q/k/v straight out of the fused QKV activation (row stride = (Hq+2Hkv)*hd) after
-// the in-place RoPE, so no separate K/V copies exist. Each wave owns 16 query rows of one
-// query head and streams 32-key tiles (flash-attention online softmax):
-//   S^T[key, q] = K . Q^T        mfma_f32_16x16x32_bf16, K rows as A operand (16-B loads)
-//   softmax along keys           exp2 domain; per-q max over 2 lane groups (2 shuffles)
+// the in-place RoPE, so no separate K/V copies exist. A workgroup = 4 waves = 64 query rows
+// of one query head (16 per wave); the workgroup streams 64-key tiles of K and V through
+// LDS ONCE for all 4 waves (each wave used to fetch its own K rows from global memory: 4x
+// the K/V traffic, O(L^2) bytes per head for long prompts):
+//   stage      tile t+1 is loaded into registers while tile t is computed, then written
+//              to LDS between two barriers (K rows padded to 272 B: conflict-free
+//              ds_read_b128 of the A operand; V rows to hd*2+32 B for the transposing read)
+//   S^T[key, q] = K . Q^T        mfma_f32_16x16x32_bf16, K rows as the A operand
+//   softmax along keys           exp2 domain, online (flash) rescaling per tile
 //   O[q, d] += P[q, key] . V     P re-used from the accumulator registers (permuted key
-//                                order); V staged row-major in a per-wave LDS tile (rows
-//                                padded to hd*2+32 B) and read as the B operand with the
-//                                CDNA4 transposing ds_read_b64_tr_b16 (cdna_hip_programming.md T10)
-// Grid: (ceil(max_len / 64), num_seqs, Hq); 4 independent waves per workgroup.
+//                                order); V read as the B operand with the CDNA4 transposing
+//                                ds_read_b64_tr_b16 (cdna_hip_programming.md T10)
+// Causality: a wave skips the math of tiles entirely above its rows (it still helps stage
+// them); the workgroup stops at its last row's bound.
+// Grid: (ceil(max_len / 64), num_seqs, Hq).
 #include "common.h"
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
 #define PF_WAVES 4
 #define PF_QROWS 16
-#define PF_KT 32
+#define PF_KT 64
 
 template <int HD>
-__global__ void __launch_bounds__(256) prefill_attn_kernel(
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) prefill_attn_kernel(
     u16* __restrict__ out, int out_stride, const u16* __restrict__ qkv, int row_stride,
     const int* __restrict__ cu_seqlens, int hq, int hkv, float scale_log2) {
   constexpr int KK = HD / 32, DB = HD / 16;
-  constexpr int VROW = HD + 16;                    // padded LDS row, in u16 (HD*2 + 32 bytes)
-  __shared__ __attribute__((aligned(16))) u16 vtile[PF_WAVES][PF_KT * VROW];
+  constexpr int KROW = HD + 8;                     // K row in LDS (u16): 272 B for hd 128
+  constexpr int VROW = HD + 16;                    // V row in LDS (u16): hd*2 + 32 B
+  constexpr int CH = HD / 8;                       // 16-B chunks per row
+  constexpr int PER = PF_KT * CH / 256;            // chunks per thread per tile (K or V)
+  __shared__ __attribute__((aligned(16))) u16 ktile[PF_KT * KROW];
+  __shared__ __attribute__((aligned(16))) u16 vtile[PF_KT * VROW];
   const int seq = blockIdx.y, h = blockIdx.z;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int col = lane & 15, grp = lane >> 4;
   const int s0 = cu_seqlens[seq], len = cu_seqlens[seq + 1] - s0;
-  const int q0 = (blockIdx.x * PF_WAVES + wid) * PF_QROWS;      // position within the sequence
-  if (q0 >= len) return;                                         // wave-uniform exit
+  const int wg_q0 = blockIdx.x * PF_WAVES * PF_QROWS;
+  if (wg_q0 >= len) return;                                      // workgroup-uniform exit
+  const int q0 = wg_q0 + wid * PF_QROWS;                         // this wave's first row
+  const bool active = q0 < len;
   const int G = hq / hkv, kvh = h / G;
   const u16* qbase = qkv + (long)h * HD;
   const u16* kbase = qkv + (long)(hq + kvh) * HD;
@@ -50,36 +63,46 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(
   f32x4 o_acc[DB];
 #pragma unroll
   for (int i = 0; i < DB; ++i) o_acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  u16* vt = vtile[wid];
-  const int kend = min(len, q0 + PF_QROWS);                      // causal bound for this wave
+  const int kend_wg = min(len, wg_q0 + PF_WAVES * PF_QROWS);     // last row's causal bound
+  const int kend_w = min(len, q0 + PF_QROWS);                    // this wave's bound
 
-  for (int k0 = 0; k0 < kend; k0 += PF_KT) {
-    // ---- stage V[k0 .. k0+32) row-major into LDS (each lane: 16-B pieces)
-    constexpr int PIECES = PF_KT * HD / 8;                      // 16-B pieces per tile
+  uint4 kreg[PER], vreg[PER];
+#define PF_LOAD_TILE(K0)                                                              \
+  _Pragma("unroll") for (int j = 0; j < PER; ++j) {                                   \
+    const int i = tid + 256 * j;                                                      \
+    const int r = i / CH, c = i % CH;                                                 \
+    const long row = s0 + min((K0) + r, len - 1);                                     \
+    kreg[j] = *reinterpret_cast<const uint4*>(kbase + row * row_stride + c * 8);      \
+    vreg[j] = *reinterpret_cast<const uint4*>(vbase + row * row_stride + c * 8);      \
+  }
+  PF_LOAD_TILE(0)
+  const int qrow = (lane >> 2) & 3, pcol = lane & 3;
+  for (int k0 = 0; k0 < kend_wg; k0 += PF_KT) {
+    __syncthreads();                                             // previous tile fully read
 #pragma unroll
-    for (int i = lane; i < PIECES; i += 64) {
-      const int r = i / (HD / 8), c = i % (HD / 8);
-      const int key = min(k0 + r, len - 1);
-      uint4 v = *reinterpret_cast<const uint4*>(vbase + (long)(s0 + key) * row_stride + c * 8);
-      *reinterpret_cast<uint4*>(vt + r * VROW + c * 8) = v;
+    for (int j = 0; j < PER; ++j) {
+      const int i = tid + 256 * j;
+      const int r = i / CH, c = i % CH;
+      *reinterpret_cast<uint4*>(ktile + r * KROW + c * 8) = kreg[j];
+      *reinterpret_cast<uint4*>(vtile + r * VROW + c * 8) = vreg[j];
     }
-    // ---- S^T = K . Q^T for two 16-key subtiles
-    f32x4 s_acc[2];
+    __syncthreads();                                             // tile visible to all waves
+    if (k0 + PF_KT < kend_wg) { PF_LOAD_TILE(k0 + PF_KT) }       // in flight during compute
+    if (!active || k0 >= kend_w) continue;                       // tile above this wave's rows
+    // ---- S^T = K . Q^T over four 16-key subtiles
+    f32x4 s_acc[4];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int key = min(k0 + 16 * s + col, len - 1);
-      const u16* kp = kbase + (long)(s0 + key) * row_stride;
+    for (int s = 0; s < 4; ++s) {
+      const u16* kp = ktile + (16 * s + col) * KROW;
       s_acc[s] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int kk = 0; kk < KK; ++kk) {
-        uint4 kv = *reinterpret_cast<const uint4*>(kp + kk * 32 + grp * 8);
-        s_acc[s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<bf16x8*>(&kv),
-                                                          qf[kk], s_acc[s], 0, 0, 0);
-      }
+      for (int kk = 0; kk < KK; ++kk)
+        s_acc[s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            *reinterpret_cast<const bf16x8*>(kp + kk * 32 + grp * 8), qf[kk], s_acc[s], 0, 0, 0);
     }
-    float p[8], tmax = -INFINITY;
+    float p[16], tmax = -INFINITY;
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+    for (int s = 0; s < 4; ++s)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int key = k0 + 16 * s + 4 * grp + r;
@@ -96,7 +119,7 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(
     m_run = m_new;
     float psum = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { p[j] = exp2f(p[j] - m_use); psum += p[j]; }
+    for (int j = 0; j < 16; ++j) { p[j] = exp2f(p[j] - m_use); psum += p[j]; }
     l_part = l_part * alpha + psum;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -104,28 +127,29 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(
 #pragma unroll
       for (int i = 0; i < DB; ++i) o_acc[i][r] *= a;
     }
-    bf16x8 pa;
+    // ---- O += P . V, two 32-key halves; B operand rows: keys 32h + 4grp + q and
+    // 32h + 16 + 4grp + q (the p[] key order), cols 16i + 4p via tr16 reads
 #pragma unroll
-    for (int j = 0; j < 8; ++j) pa[j] = (__bf16)p[j];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // V tile writes landed (same wave)
-    // B operand rows: keys 4grp+q (first read) and 16+4grp+q (second), cols 16db + 4p
-    // tr16 addressing: lane 4q+p of each 16-lane group names row q, columns 4p..4p+3
-    const int qrow = (lane >> 2) & 3, pcol = lane & 3;
+    for (int hh = 0; hh < 2; ++hh) {
+      bf16x8 pa;
 #pragma unroll
-    for (int i = 0; i < DB; ++i) {
-      const u16* a0 = vt + (4 * grp + qrow) * VROW + 16 * i + 4 * pcol;
-      const u16* a1 = vt + (16 + 4 * grp + qrow) * VROW + 16 * i + 4 * pcol;
-      s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          (__attribute__((address_space(3))) s16x4*)(a0));
-      s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          (__attribute__((address_space(3))) s16x4*)(a1));
-      typedef short s16x8 __attribute__((ext_vector_type(8)));
-      s16x8 w = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      o_acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, *reinterpret_cast<bf16x8*>(&w),
-                                                        o_acc[i], 0, 0, 0);
+      for (int j = 0; j < 8; ++j) pa[j] = (__bf16)p[8 * hh + j];
+#pragma unroll
+      for (int i = 0; i < DB; ++i) {
+        const u16* a0 = vtile + (32 * hh + 4 * grp + qrow) * VROW + 16 * i + 4 * pcol;
+        const u16* a1 = vtile + (32 * hh + 16 + 4 * grp + qrow) * VROW + 16 * i + 4 * pcol;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(a0));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(a1));
+        s16x8 w = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        o_acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, *reinterpret_cast<bf16x8*>(&w),
+                                                          o_acc[i], 0, 0, 0);
+      }
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before next overwrite
   }
+#undef PF_LOAD_TILE
+  if (!active) return;
   float l_tot = l_part + __shfl_xor(l_part, 16, 64);
   l_tot += __shfl_xor(l_tot, 32, 64);
   const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
