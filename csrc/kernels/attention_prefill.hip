@@ -15,6 +15,10 @@
 //                                ds_read_b64_tr_b16 (cdna_hip_programming.md T10)
 // Causality: a wave skips the math of tiles entirely above its rows (it still helps stage
 // them); the workgroup stops at its last row's bound.
+// Chunked prefill (PAGED): the chunk's K/V have already been written to the paged cache
+// (rope_cache), so keys come from the cache through the block table: a chunk of len queries
+// at positions [ctx - len, ctx) attends over all ctx cached keys of its sequence (earlier
+// chunks, a recomputed prefix) with the causal bound shifted by ctx - len.
 // Grid: (ceil(max_len / 64), num_seqs, Hq).
 #include "common.h"
 
@@ -24,10 +28,13 @@ typedef short s16x8 __attribute__((ext_vector_type(8)));
 #define PF_QROWS 16
 #define PF_KT 64
 
-template <int HD>
+template <int HD, bool PAGED>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) prefill_attn_kernel(
     u16* __restrict__ out, int out_stride, const u16* __restrict__ qkv, int row_stride,
-    const int* __restrict__ cu_seqlens, int hq, int hkv, float scale_log2) {
+    const int* __restrict__ cu_seqlens, int hq, int hkv, float scale_log2,
+    const int* __restrict__ ctx_lens, const u16* __restrict__ k_cache,
+    const u16* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
+    int block_size) {
   constexpr int KK = HD / 32, DB = HD / 16;
   constexpr int KROW = HD + 8;                     // K row in LDS (u16): 272 B for hd 128
   constexpr int VROW = HD + 16;                    // V row in LDS (u16): hd*2 + 32 B
@@ -39,6 +46,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int col = lane & 15, grp = lane >> 4;
   const int s0 = cu_seqlens[seq], len = cu_seqlens[seq + 1] - s0;
+  const int nkeys = PAGED ? ctx_lens[seq] : len;                 // keys visible to the chunk
+  const int qoff = nkeys - len;                                  // position of query row 0
   const int wg_q0 = blockIdx.x * PF_WAVES * PF_QROWS;
   if (wg_q0 >= len) return;                                      // workgroup-uniform exit
   const int q0 = wg_q0 + wid * PF_QROWS;                         // this wave's first row
@@ -47,6 +56,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))
   const u16* qbase = qkv + (long)h * HD;
   const u16* kbase = qkv + (long)(hq + kvh) * HD;
   const u16* vbase = qkv + (long)(hq + hkv + kvh) * HD;
+  const int* btab = PAGED ? block_tables + (long)seq * bt_stride : nullptr;
+  const long head_off = (long)kvh * block_size * HD;             // (blk, head) panel offset
 
   bf16x8 qf[KK];
   {
@@ -58,22 +69,30 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))
       qf[kk] = *reinterpret_cast<bf16x8*>(&v);
     }
   }
-  const int my_q = q0 + col;               // the query row this lane's S^T column belongs to
+  const int my_q = qoff + q0 + col;        // position of the query row of this lane's column
   float m_run = -INFINITY, l_part = 0.f;
   f32x4 o_acc[DB];
 #pragma unroll
   for (int i = 0; i < DB; ++i) o_acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int kend_wg = min(len, wg_q0 + PF_WAVES * PF_QROWS);     // last row's causal bound
-  const int kend_w = min(len, q0 + PF_QROWS);                    // this wave's bound
+  const int kend_wg = min(nkeys, qoff + wg_q0 + PF_WAVES * PF_QROWS);  // last row's bound
+  const int kend_w = min(nkeys, qoff + q0 + PF_QROWS);                 // this wave's bound
 
   uint4 kreg[PER], vreg[PER];
 #define PF_LOAD_TILE(K0)                                                              \
   _Pragma("unroll") for (int j = 0; j < PER; ++j) {                                   \
     const int i = tid + 256 * j;                                                      \
     const int r = i / CH, c = i % CH;                                                 \
-    const long row = s0 + min((K0) + r, len - 1);                                     \
-    kreg[j] = *reinterpret_cast<const uint4*>(kbase + row * row_stride + c * 8);      \
-    vreg[j] = *reinterpret_cast<const uint4*>(vbase + row * row_stride + c * 8);      \
+    const int tok = min((K0) + r, nkeys - 1);                                         \
+    if (PAGED) {                                                                      \
+      const long e = (long)btab[tok / block_size] * hkv * block_size * HD + head_off +  \
+                     (long)(tok % block_size) * HD + c * 8;                           \
+      kreg[j] = *reinterpret_cast<const uint4*>(k_cache + e);                         \
+      vreg[j] = *reinterpret_cast<const uint4*>(v_cache + e);                         \
+    } else {                                                                          \
+      const long row = s0 + tok;                                                      \
+      kreg[j] = *reinterpret_cast<const uint4*>(kbase + row * row_stride + c * 8);    \
+      vreg[j] = *reinterpret_cast<const uint4*>(vbase + row * row_stride + c * 8);    \
+    }                                                                                 \
   }
   PF_LOAD_TILE(0)
   const int qrow = (lane >> 2) & 3, pcol = lane & 3;
@@ -106,7 +125,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int key = k0 + 16 * s + 4 * grp + r;
-        const float v = (key <= my_q && key < len) ? s_acc[s][r] * scale_log2 : -INFINITY;
+        const float v = (key <= my_q && key < nkeys) ? s_acc[s][r] * scale_log2 : -INFINITY;
         p[s * 4 + r] = v;
         tmax = fmaxf(tmax, v);
       }
@@ -165,19 +184,47 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))
   }
 }
 
-extern "C" int dli_prefill_attention(void* out, int out_stride, const void* qkv, int row_stride,
-                                     const int* cu_seqlens, int num_seqs, int max_seqlen, int hq,
-                                     int hkv, int hd, float scale, hipStream_t st) {
+template <bool PAGED>
+static int launch_prefill(void* out, int out_stride, const void* qkv, int row_stride,
+                          const int* cu_seqlens, int num_seqs, int max_seqlen, int hq, int hkv,
+                          int hd, float scale, const int* ctx_lens, const void* k_cache,
+                          const void* v_cache, const int* block_tables, int bt_stride,
+                          int block_size, hipStream_t st) {
   if (num_seqs <= 0 || max_seqlen <= 0) return 0;
   if (hq % hkv || (hd != 64 && hd != 128)) return (int)hipErrorInvalidValue;
   const int rows_per_wg = PF_WAVES * PF_QROWS;
   dim3 grid((max_seqlen + rows_per_wg - 1) / rows_per_wg, num_seqs, hq);
   const float sl2 = scale * 1.4426950408889634f;
   if (hd == 128)
-    prefill_attn_kernel<128><<<grid, 256, 0, st>>>((u16*)out, out_stride, (const u16*)qkv,
-                                                   row_stride, cu_seqlens, hq, hkv, sl2);
+    prefill_attn_kernel<128, PAGED><<<grid, 256, 0, st>>>(
+        (u16*)out, out_stride, (const u16*)qkv, row_stride, cu_seqlens, hq, hkv, sl2, ctx_lens,
+        (const u16*)k_cache, (const u16*)v_cache, block_tables, bt_stride, block_size);
   else
-    prefill_attn_kernel<64><<<grid, 256, 0, st>>>((u16*)out, out_stride, (const u16*)qkv,
-                                                  row_stride, cu_seqlens, hq, hkv, sl2);
+    prefill_attn_kernel<64, PAGED><<<grid, 256, 0, st>>>(
+        (u16*)out, out_stride, (const u16*)qkv, row_stride, cu_seqlens, hq, hkv, sl2, ctx_lens,
+        (const u16*)k_cache, (const u16*)v_cache, block_tables, bt_stride, block_size);
   DLI_RETURN_LAUNCH();
+}
+
+extern "C" int dli_prefill_attention(void* out, int out_stride, const void* qkv, int row_stride,
+                                     const int* cu_seqlens, int num_seqs, int max_seqlen, int hq,
+                                     int hkv, int hd, float scale, hipStream_t st) {
+  return launch_prefill<false>(out, out_stride, qkv, row_stride, cu_seqlens, num_seqs,
+                               max_seqlen, hq, hkv, hd, scale, nullptr, nullptr, nullptr,
+                               nullptr, 0, 16, st);
+}
+
+// Chunked prefill: q from qkv rows [cu[s], cu[s+1]); keys 0..ctx_lens[s]-1 of sequence s
+// from the paged caches [num_blocks, hkv, block_size, hd] through block_tables[s, :].
+extern "C" int dli_prefill_attention_paged(void* out, int out_stride, const void* qkv,
+                                           int row_stride, const int* cu_seqlens,
+                                           const int* ctx_lens, const void* k_cache,
+                                           const void* v_cache, const int* block_tables,
+                                           int bt_stride, int num_seqs, int max_seqlen, int hq,
+                                           int hkv, int hd, int block_size, float scale,
+                                           hipStream_t st) {
+  if (block_size <= 0) return (int)hipErrorInvalidValue;
+  return launch_prefill<true>(out, out_stride, qkv, row_stride, cu_seqlens, num_seqs,
+                              max_seqlen, hq, hkv, hd, scale, ctx_lens, k_cache, v_cache,
+                              block_tables, bt_stride, block_size, st);
 }

@@ -38,6 +38,9 @@ class StepMeta:
     # lookahead (single stage, not on the wire): row of the in-flight step's device output
     # that holds this sequence's input id, -1 = input_ids holds it
     feed_src: Optional[np.ndarray] = None
+    # chunked prefill (not on the wire): True for rows whose chunk completes the prompt; the
+    # token sampled for any other row is discarded. None = every row samples.
+    sample_mask: Optional[np.ndarray] = None
     # columns of block_tables that hold blocks (the scheduler knows it; pack trims to it)
     table_used: Optional[int] = None
     # seq_ids as int64 numpy (set by the decode scheduler; saves list -> array conversions)
@@ -51,6 +54,10 @@ class StepMeta:
     @property
     def num_seqs(self) -> int:
         return len(self.seq_ids)
+
+    @property
+    def num_sampled(self) -> int:
+        return self.num_seqs if self.sample_mask is None else int(self.sample_mask.sum())
 
     @property
     def num_tokens(self) -> int:
@@ -210,6 +217,11 @@ def to_device(meta: StepMeta, device, pin: bool = True) -> DeviceBatch:
         db.cu_seqlens = t(cu, torch.int32)
         db.max_seqlen = int(lens.max()) if S else 0
         db.last_token_idx = t(cu[1:] - 1, torch.int64)
+        if meta.block_tables is not None and np.shape(meta.block_tables)[1] > 0:
+            # chunked prefill: queries attend over the paged cache (earlier chunks + this one)
+            db.block_tables = t(meta.block_tables, torch.int32)
+            db.context_lens = t(meta.context_lens, torch.int32)
+            db.max_context = int(np.max(meta.context_lens)) if S else 0
     else:
         db.block_tables = t(meta.block_tables, torch.int32)
         db.context_lens = t(meta.context_lens, torch.int32)

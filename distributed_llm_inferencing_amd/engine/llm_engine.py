@@ -192,7 +192,7 @@ class LLMEngine:
                 tok = done[2].get()
             with self.timer.phase("update"):
                 self.scheduler.update(done[0], tok)
-            self.stats.tokens_out += done[0].num_seqs
+            self.stats.tokens_out += done[0].num_sampled
         if meta is not None or done is not None:
             self.stats.busy_s += time.perf_counter() - t0
         outs = []

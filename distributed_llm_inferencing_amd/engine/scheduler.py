@@ -155,6 +155,12 @@ class Scheduler:
         self.table_width = table_width or -(-max_model_len // self.bs)
         self.waiting: deque = deque()
         self.running: List[List[Sequence]] = [[] for _ in range(self.M)]
+        # chunked prefill: prompts longer than max_prefill_tokens are prefilled over several
+        # steps (their KV blocks are held from the first chunk on); between two chunk steps of
+        # a microbatch that is also decoding, one decode step runs, so a long prompt delays
+        # the running sequences' next token by at most one chunk
+        self.prefilling: List[List[Sequence]] = [[] for _ in range(self.M)]
+        self._chunk_turn = [True] * self.M
         self._state: List[Optional[_MBState]] = [None] * self.M
         self.seqs: Dict[int, Sequence] = {}
         self.finished: List[Sequence] = []
@@ -204,7 +210,7 @@ class Scheduler:
         return False
 
     def has_work(self) -> bool:
-        return bool(self.waiting) or any(self.running)
+        return bool(self.waiting) or any(self.running) or any(self.prefilling)
 
     def num_running(self) -> int:
         return sum(len(r) for r in self.running)
@@ -231,6 +237,11 @@ class Scheduler:
                 r.remove(seq)
             except ValueError:
                 pass
+        elif seq.state == SeqState.PREFILLING:
+            try:
+                self.prefilling[seq.microbatch].remove(seq)
+            except ValueError:
+                pass
         self._mark_finished(seq, reason)
 
     def _mark_finished(self, seq: Sequence, reason: str, free: bool = True):
@@ -247,7 +258,8 @@ class Scheduler:
         if self._deadlines <= 0:
             return
         now = time.perf_counter()
-        for seq in list(self.waiting) + [s for r in self.running for s in r]:
+        for seq in (list(self.waiting) + [s for r in self.running for s in r] +
+                    [s for r in self.prefilling for s in r]):
             dl = seq.deadline
             if dl is not None and now > dl:
                 self._finish(seq, "timeout")
@@ -261,6 +273,7 @@ class Scheduler:
         r.remove(victim)
         self.bm.free(victim.seq_id)
         victim.state = SeqState.WAITING
+        victim.num_prefilled = 0
         victim.num_preemptions += 1
         self.waiting.appendleft(victim)
         return True
@@ -298,57 +311,114 @@ class Scheduler:
         return len(self.running[mb]) <= min(loads)
 
     def _try_prefill(self, mb: int) -> Optional[StepMeta]:
-        if not self.waiting or (self.M > 1 and not self._least_loaded_ok(mb)):
-            return None
-        if self.running[mb] and self.admit_window_s > 0:
-            want = min(self.admit_min, self.max_seqs - len(self.running[mb]))
-            if (len(self.waiting) < want and
-                    time.perf_counter() - self.waiting[0].arrival < self.admit_window_s):
-                return None                  # keep decoding; batch the arrivals
+        partial = self.prefilling[mb]
+        if partial:
+            # a chunk step every other step while the microbatch also decodes
+            if self.running[mb] and not self._chunk_turn[mb]:
+                self._chunk_turn[mb] = True
+                return None
+            self._chunk_turn[mb] = False
+        if not partial:
+            if not self.waiting or (self.M > 1 and not self._least_loaded_ok(mb)):
+                return None
+            if self.running[mb] and self.admit_window_s > 0:
+                want = min(self.admit_min, self.max_seqs - len(self.running[mb]))
+                if (len(self.waiting) < want and
+                        time.perf_counter() - self.waiting[0].arrival < self.admit_window_s):
+                    return None              # keep decoding; batch the arrivals
+        budget = self.max_prefill_tokens
         picked: List[Sequence] = []
+        starts_l: List[int] = []
         lens_l: List[int] = []
-        tokens = 0
-        room = self.max_seqs - len(self.running[mb])
-        for seq in self.waiting:
-            if len(picked) >= room:
+        for seq in partial:                  # continue chunked prompts first, in order
+            if budget <= 0:
                 break
-            n = seq.total_len
-            if picked and tokens + n > self.max_prefill_tokens:
-                break
+            n = min(seq.total_len - seq.num_prefilled, budget)
             picked.append(seq)
+            starts_l.append(seq.num_prefilled)
             lens_l.append(n)
-            tokens += n
+            budget -= n
+        n_cont = len(picked)
+        new: List[Sequence] = []
+        new_lens: List[int] = []
+        room = self.max_seqs - len(self.running[mb]) - len(partial)
+        if budget > 0 and room > 0 and not (self.M > 1 and n_cont == 0
+                                            and not self._least_loaded_ok(mb)):
+            for seq in self.waiting:
+                if len(new) >= room or budget <= 0:
+                    break
+                n = seq.total_len
+                if n > budget and (new or n_cont or n <= self.max_prefill_tokens):
+                    break                    # whole prompts only, except a chunked first
+                new.append(seq)
+                new_lens.append(n)
+                budget -= min(n, budget)
+        if new:
+            # blocks for every new prompt (whole length, also when chunked) in one C++ call;
+            # stops at the first that does not fit
+            sid_new = np.fromiter((s.seq_id for s in new), np.int64, len(new))
+            got = self.bm.ensure_batch(sid_new, np.asarray(new_lens, dtype=np.int32))
+            new = new[:got]
+            for _ in range(got):
+                self.waiting.popleft()
+            budget = self.max_prefill_tokens - sum(lens_l)
+            for s in new:
+                n = min(s.total_len, budget)
+                picked.append(s)
+                starts_l.append(0)
+                lens_l.append(n)
+                budget -= n
         if not picked:
             return None
-        # blocks for every picked prompt in one C++ call; stops at the first that does not fit
-        sid = np.fromiter((s.seq_id for s in picked), np.int64, len(picked))
+        S = len(picked)
+        sid = np.fromiter((s.seq_id for s in picked), np.int64, S)
+        starts = np.asarray(starts_l, dtype=np.int32)
         lens = np.asarray(lens_l, dtype=np.int32)
-        got = self.bm.ensure_batch(sid, lens)
-        if got == 0:
-            return None
-        if got < len(picked):
-            picked, sid, lens = picked[:got], sid[:got], lens[:got]
-        for _ in range(got):
-            self.waiting.popleft()
-        self._drop_state(mb)
-        for s in picked:
-            s.state = SeqState.RUNNING
+        chunked = n_cont > 0 or any(n < s.total_len for s, n in zip(new, lens_l[n_cont:]))
+        final = np.fromiter((st + n == s.total_len for s, st, n in zip(picked, starts_l, lens_l)),
+                            np.bool_, S)
+        joined = False
+        for s, st, n, f in zip(picked, starts_l, lens_l, final.tolist()):
+            s.num_prefilled = st + n
             s.microbatch = mb
-            self.running[mb].append(s)
+            if f:
+                if s.state == SeqState.PREFILLING:
+                    partial.remove(s)
+                s.state = SeqState.RUNNING
+                self.running[mb].append(s)
+                joined = True
+            elif s.state != SeqState.PREFILLING:
+                s.state = SeqState.PREFILLING
+                partial.append(s)
+        if joined:
+            self._drop_state(mb)
         T = int(lens.sum())
-        ids = np.fromiter(itertools.chain.from_iterable(
-            (s.prompt_ids + s.output_ids) if s.output_ids else s.prompt_ids for s in picked),
-            np.int32, T)
-        starts = np.zeros(len(picked), np.int32)
-        starts[1:] = np.cumsum(lens)[:-1]
-        pos = (np.arange(T, dtype=np.int32) - np.repeat(starts, lens)).astype(np.int32)
-        slots = self.bm.slot_mapping(sid, np.zeros(len(picked), np.int32), lens)
+        if chunked:
+            ids = np.fromiter(itertools.chain.from_iterable(
+                (s.prompt_ids + s.output_ids)[st:st + n]
+                for s, st, n in zip(picked, starts_l, lens_l)), np.int32, T)
+        else:
+            ids = np.fromiter(itertools.chain.from_iterable(
+                (s.prompt_ids + s.output_ids) if s.output_ids else s.prompt_ids for s in picked),
+                np.int32, T)
+        cu = np.zeros(S, np.int32)
+        cu[1:] = np.cumsum(lens)[:-1]
+        pos = (np.arange(T, dtype=np.int32) - np.repeat(cu - starts, lens)).astype(np.int32)
+        slots = self.bm.slot_mapping(sid, starts, lens)
+        ctx = starts + lens
+        if chunked:
+            width = -(-max(s.total_len for s in picked) // self.bs)   # blocks held per seq
+            tables = self.bm.fill_tables(sid.tolist(), width)
+        else:
+            tables = np.zeros((S, 0), np.int32)
         temp, topk, topp, seeds = self._sampling_arrays(picked)
-        return StepMeta(kind=PREFILL, seq_ids=sid.tolist(), input_ids=ids, positions=pos,
-                        slot_mapping=slots, seq_lens=lens, context_lens=lens.copy(),
-                        block_tables=np.zeros((len(picked), 0), np.int32), temperature=temp,
-                        top_k=topk, top_p=topp, seeds=seeds, microbatch=mb, step_id=self._step,
-                        seq_ids_arr=sid)
+        meta = StepMeta(kind=PREFILL, seq_ids=sid.tolist(), input_ids=ids, positions=pos,
+                        slot_mapping=slots, seq_lens=lens, context_lens=ctx,
+                        block_tables=tables, temperature=temp, top_k=topk, top_p=topp,
+                        seeds=seeds, microbatch=mb, step_id=self._step, seq_ids_arr=sid)
+        if not final.all():
+            meta.sample_mask = final
+        return meta
 
     def _mb_state(self, mb: int, native: bool = False):
         st = self._state[mb]
@@ -548,9 +618,10 @@ class Scheduler:
         done = []
         now = time.perf_counter()
         touched = set()
+        mask = meta.sample_mask
         for i, sid in enumerate(meta.seq_ids):
             seq = self.seqs.get(sid)
-            if seq is None or seq.state != SeqState.RUNNING:
+            if seq is None or seq.state != SeqState.RUNNING or (mask is not None and not mask[i]):
                 continue
             touched.add(seq.microbatch)
             t = int(tokens[i])

@@ -42,6 +42,7 @@ class SeqState(enum.Enum):
     WAITING = 0
     RUNNING = 1
     FINISHED = 2
+    PREFILLING = 3          # chunked prefill in progress (KV blocks held, not decoding yet)
 
 
 @dataclass(eq=False)          # identity semantics: list.remove / `in` must not compare fields
@@ -59,6 +60,7 @@ class Sequence:
     finish_reason: Optional[str] = None
     seed: int = 0
     num_preemptions: int = 0
+    num_prefilled: int = 0  # tokens of all_ids() whose KV a scheduled prefill chunk writes
 
     @property
     def prompt_len(self) -> int:

@@ -171,6 +171,11 @@ class TransformerLM:
     def _attend(self, qkv, b: DeviceBatch, kc, vc) -> torch.Tensor:
         cfg = self.cfg
         if b.is_prefill:
+            if b.block_tables is not None:       # chunked prefill over the paged cache
+                return ops.prefill_attention_paged(qkv, b.cu_seqlens, b.max_seqlen,
+                                                   b.context_lens, b.block_tables, kc, vc,
+                                                   cfg.num_heads, cfg.num_kv_heads,
+                                                   cfg.head_dim, self.scale)
             return ops.prefill_attention(qkv, b.cu_seqlens, b.max_seqlen, cfg.num_heads,
                                          cfg.num_kv_heads, cfg.head_dim, self.scale)
         return ops.decode_attention(qkv, kc, vc, b.block_tables, b.context_lens, b.max_context,
@@ -181,6 +186,11 @@ class TransformerLM:
         ops.rope_and_cache(qkv, b.positions, b.slot_mapping, self.cos_sin, kc, vc, cfg.num_heads,
                            cfg.num_kv_heads, cfg.head_dim, use_rope=cfg.arch != "gpt2")
         if b.is_prefill:
+            if b.block_tables is not None:       # chunked prefill over the paged cache
+                return ops.prefill_attention_paged(qkv, b.cu_seqlens, b.max_seqlen,
+                                                   b.context_lens, b.block_tables, kc, vc,
+                                                   cfg.num_heads, cfg.num_kv_heads,
+                                                   cfg.head_dim, self.scale)
             return ops.prefill_attention(qkv, b.cu_seqlens, b.max_seqlen, cfg.num_heads,
                                          cfg.num_kv_heads, cfg.head_dim, self.scale)
         return ops.decode_attention(qkv, kc, vc, b.block_tables, b.context_lens, b.max_context,

@@ -282,6 +282,30 @@ def prefill_attention(qkv, cu_seqlens, max_seqlen: int, hq, hkv, hd, scale, out=
     return out
 
 
+def prefill_attention_paged(qkv, cu_seqlens, max_seqlen: int, context_lens, block_tables,
+                            k_cache, v_cache, hq, hkv, hd, scale, out=None):
+    """Chunked prefill attention: each sequence's chunk of queries (packed rows of ``qkv``)
+    attends over all ``context_lens[i]`` keys of the sequence in the paged cache — earlier
+    chunks plus this one (already written by ``rope_and_cache``); [T, Hq*hd]."""
+    T = qkv.shape[0]
+    if not _use_native(qkv):
+        q = qkv[:, : hq * hd].reshape(T, hq, hd)
+        o = R.prefill_attention_paged(q, k_cache, v_cache, cu_seqlens, context_lens,
+                                      block_tables, scale).reshape(T, hq * hd)
+        if out is not None:
+            out.copy_(o)
+            return out
+        return o
+    if out is None:
+        out = torch.empty(T, hq * hd, dtype=qkv.dtype, device=qkv.device)
+    nseq = cu_seqlens.shape[0] - 1
+    _native_call("dli_prefill_attention_paged", _p(out), out.stride(0), _p(qkv), qkv.stride(0),
+                 _p(cu_seqlens), _p(context_lens), _p(k_cache), _p(v_cache), _p(block_tables),
+                 block_tables.stride(0), nseq, max_seqlen, hq, hkv, hd, k_cache.shape[2], scale,
+                 _st())
+    return out
+
+
 def decode_num_splits(B: int, hkv: int, max_context: int) -> int:
     """KV splits so that the B*Hkv*splits work items (one wave each) fill the chip's ~2048
     resident waves for long contexts, keeping >= 128 tokens per split."""

@@ -192,6 +192,31 @@ def gather_kv(k_cache, v_cache, block_table: torch.Tensor, ctx_len: int):
     return kk, vv
 
 
+def prefill_attention_paged(q, k_cache, v_cache, cu_seqlens, context_lens, block_tables,
+                            scale: float) -> torch.Tensor:
+    """Chunked prefill: the queries q[cu[i]:cu[i+1]] sit at positions [ctx-L, ctx) of
+    sequence i and attend causally over its ctx = context_lens[i] cached keys."""
+    out = torch.empty(q.shape, dtype=q.dtype, device=q.device)
+    hq, hkv = q.shape[1], k_cache.shape[1]
+    rep = hq // hkv
+    cu, lens = cu_seqlens.tolist(), context_lens.tolist()
+    for i in range(len(cu) - 1):
+        s, e = cu[i], cu[i + 1]
+        if e <= s:
+            continue
+        L, ctx = e - s, lens[i]
+        kk, vv = gather_kv(k_cache, v_cache, block_tables[i], ctx)
+        kk = kk.float().transpose(0, 1).repeat_interleave(rep, 0)   # [Hq, ctx, hd]
+        vv = vv.float().transpose(0, 1).repeat_interleave(rep, 0)
+        qs = q[s:e].float().transpose(0, 1)                          # [Hq, L, hd]
+        sc = (qs @ kk.transpose(1, 2)) * scale                       # [Hq, L, ctx]
+        qpos = torch.arange(ctx - L, ctx, device=q.device).unsqueeze(1)
+        mask = torch.arange(ctx, device=q.device).unsqueeze(0) > qpos
+        sc = sc.masked_fill(mask, float("-inf"))
+        out[s:e] = (sc.softmax(-1) @ vv).transpose(0, 1).to(q.dtype)
+    return out
+
+
 def decode_attention(q, k_cache, v_cache, block_tables, context_lens, scale) -> torch.Tensor:
     """q [B,Hq,hd] single query per sequence against its paged cache."""
     out = torch.empty(q.shape, dtype=q.dtype, device=q.device)

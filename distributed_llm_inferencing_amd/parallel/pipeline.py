@@ -302,7 +302,7 @@ class PipelineHead:
                 tw = pc()
                 wait_s += tw - t0
                 self.sched.update(m, arr)
-                self.stats.tokens_out += m.num_seqs
+                self.stats.tokens_out += m.num_sampled
                 ph["update"] += pc() - tw
             t1 = pc()
             if admit is not None:
@@ -687,7 +687,7 @@ class LocalPipeline:
         if j in self._inflight:
             m, toks = self._inflight.pop(j)
             self.sched.update(m, toks)
-            self.stats.tokens_out += m.num_seqs
+            self.stats.tokens_out += m.num_sampled
         meta = self.sched.schedule(k % N) if self.sched.has_work() else None
         if meta is not None:
             data = None

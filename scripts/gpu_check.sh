@@ -50,6 +50,11 @@ for s in "$@"; do
     ep2) step ep2 900 env DLI_DIST_BACKEND=gloo DLI_SAME_DEVICE=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29535 bench.py --model mixtral-8x7b --gpus 2 --steps 1 --warmup 1 --batch 32 ;;
     llama70) step llama70 1100 python bench.py --model llama3-70b --steps 1 --warmup 1 --batch 64 ;;
     bench_small) step bench_small 600 python bench.py --steps 2 --warmup 1 --batch 64 ;;
+    b1) step bench_b1 600 python bench.py --steps 16 --warmup 2 --batch 1 ;;
+    prof8k) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+          step prof8k 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof8k -o bench -- python bench.py --steps 1 --warmup 1 --batch 1 --prompt-len 8064 --max-length 8180 --max-model-len 8192
+          python scripts/prof_summary.py gpurun_out/prof8k 40 --tail-ms 250 > gpurun_out/prof8k_summary.txt
+          rm -f gpurun_out/prof8k/*trace.csv ;;
     lookahead) step la_on 600 python bench.py --steps 3 --warmup 1
                step la_off 600 env DLI_LOOKAHEAD=0 python bench.py --steps 3 --warmup 1
                step la_on2 600 python bench.py --steps 3 --warmup 1 ;;

@@ -540,3 +540,37 @@ def test_decode_attention_32k_context(gpu):
         out = ops.decode_attention(qkv, kc, vc, tables, ctx, max(lens), hq, hkv, hd, scale,
                                    num_splits=splits)
         close(out, ref, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("hq,hkv,hd,bs,chunks", [
+    (32, 8, 128, 16, [(100, 37), (2053, 512), (16, 16), (1, 1)]),
+    (12, 12, 64, 32, [(70, 70), (300, 64), (129, 1)]),
+    (8, 1, 128, 16, [(4096, 700)])])
+def test_prefill_attention_paged_chunks(gpu, hq, hkv, hd, bs, chunks):
+    """Chunked prefill: each chunk of queries (positions [ctx-L, ctx)) attends over all ctx
+    keys of its sequence in a scattered paged cache, vs the fp32 reference."""
+    torch.manual_seed(23)
+    ctxs = [c for c, _ in chunks]
+    lens = [n for _, n in chunks]
+    nblk = sum(-(-c // bs) for c in ctxs) + 4
+    kc = rnd(nblk, hkv, bs, hd, dev=gpu)
+    vc = rnd(nblk, hkv, bs, hd, dev=gpu)
+    perm = torch.randperm(nblk - 4, device=gpu).to(torch.int32)
+    maxb = -(-max(ctxs) // bs)
+    tables, o = [], 0
+    for c in ctxs:
+        nb = -(-c // bs)
+        tables.append(torch.cat([perm[o:o + nb], torch.zeros(maxb - nb, dtype=torch.int32,
+                                                               device=gpu)]))
+        o += nb
+    tables = torch.stack(tables)
+    T = sum(lens)
+    qkv = rnd(T, (hq + 2 * hkv) * hd, dev=gpu)
+    cu = torch.tensor([0] + list(np.cumsum(lens)), device=gpu, dtype=torch.int32)
+    ctx = torch.tensor(ctxs, device=gpu, dtype=torch.int32)
+    scale = 1 / math.sqrt(hd)
+    out = ops.prefill_attention_paged(qkv, cu, max(lens), ctx, tables, kc, vc, hq, hkv, hd,
+                                      scale)
+    q = qkv[:, : hq * hd].reshape(T, hq, hd)
+    ref = R.prefill_attention_paged(q, kc, vc, cu, ctx, tables, scale).reshape(T, -1)
+    close(out, ref, rtol=2e-2, atol=2e-2)
