@@ -76,10 +76,11 @@ __global__ void __launch_bounds__(256) splitk_add_rmsnorm_kernel(
 template <int VPT>
 static int launch_add_rmsnorm(u16* o, u16* r, const float* ws, int splits, int M, int N,
                               const u16* wp, float eps, int threads, hipStream_t st) {
-  // the register-resident partials of SPL x VPT cap the unrolled variants at 8 slabs
+  // the register-resident partials of SPL x VPT cap the unrolled variants at 8 slabs, so
+  // they exist for rows up to 4096 wide (VPT <= 2) and the split counts the planner offers
+  // (2/4/8); wider rows and other counts take the runtime-split loop (SPL = 0)
   switch (VPT <= 2 ? splits : 0) {
     case 2: splitk_add_rmsnorm_kernel<VPT, 2><<<M, threads, 0, st>>>(o, r, ws, 2, M, N, wp, eps); break;
-    case 3: splitk_add_rmsnorm_kernel<VPT, 3><<<M, threads, 0, st>>>(o, r, ws, 3, M, N, wp, eps); break;
     case 4: splitk_add_rmsnorm_kernel<VPT, 4><<<M, threads, 0, st>>>(o, r, ws, 4, M, N, wp, eps); break;
     case 8: splitk_add_rmsnorm_kernel<VPT, 8><<<M, threads, 0, st>>>(o, r, ws, 8, M, N, wp, eps); break;
     default: splitk_add_rmsnorm_kernel<VPT, 0><<<M, threads, 0, st>>>(o, r, ws, splits, M, N, wp, eps);
