@@ -282,6 +282,12 @@ def prefill_attention(qkv, cu_seqlens, max_seqlen: int, hq, hkv, hd, scale, out=
     return out
 
 
+def prefill_long_min_len(n: int = 0) -> int:
+    """Shortest max_seqlen routed to the 256-row (32x32x16) prefill attention kernel; n > 0
+    sets it. Returns the previous value (A/B runs and tests force either kernel with it)."""
+    return int(N.require_native().dli_prefill_set_min_len(int(n)))
+
+
 def prefill_attention_paged(qkv, cu_seqlens, max_seqlen: int, context_lens, block_tables,
                             k_cache, v_cache, hq, hkv, hd, scale, out=None):
     """Chunked prefill attention: each sequence's chunk of queries (packed rows of ``qkv``)

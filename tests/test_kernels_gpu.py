@@ -500,7 +500,8 @@ def test_ep_pack_and_combine(gpu):
     close(out, ref, rtol=1e-2, atol=1e-2)
 
 
-@pytest.mark.parametrize("lens,hq,hkv", [([2048, 300], 32, 8), ([8192], 8, 2)])
+@pytest.mark.parametrize("lens,hq,hkv", [([2048, 300], 32, 8), ([8192], 8, 2),
+                                          ([1000, 400, 5, 700], 32, 8)])
 def test_prefill_attention_long(gpu, lens, hq, hkv):
     """Long prompts: 2k and 8k-token causal GQA prefill vs the fp32
     reference (the 8k case with fewer heads so the fp32 reference's score matrix fits)."""
@@ -510,10 +511,15 @@ def test_prefill_attention_long(gpu, lens, hq, hkv):
     qkv = rnd(T, (hq + 2 * hkv) * hd, dev=gpu)
     cu = torch.tensor([0] + list(np.cumsum(lens)), device=gpu, dtype=torch.int32)
     scale = 1 / math.sqrt(hd)
-    out = ops.prefill_attention(qkv, cu, max(lens), hq, hkv, hd, scale)
     q, k, v = R.split_qkv(qkv, hq, hkv, hd)
     ref = R.prefill_attention(q, k, v, cu, scale).reshape(T, -1)
-    close(out, ref, rtol=2e-2, atol=2e-2)
+    for thr in (1, 1 << 30):            # the 256-row 32x32x16 kernel and the 64-row kernel
+        old = ops.prefill_long_min_len(thr)
+        try:
+            out = ops.prefill_attention(qkv, cu, max(lens), hq, hkv, hd, scale)
+        finally:
+            ops.prefill_long_min_len(old)
+        close(out, ref, rtol=2e-2, atol=2e-2)
 
 
 def test_decode_attention_32k_context(gpu):

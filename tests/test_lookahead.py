@@ -96,3 +96,29 @@ def test_admission_window_batches_trickling_arrivals():
     time.sleep(0.06)
     m = s.schedule(0)
     assert m.kind == 1 and m.num_seqs == 1                    # window expired
+
+
+def test_refill_pacing_when_nearly_full():
+    """More requests in flight than slots: a nearly full microbatch (fewer free slots than
+    admit_min) refills at most once per refill interval instead of running a prefill step
+    after every decode step that frees a slot or two; with admit_min free slots it refills
+    at once."""
+    import time
+    bm = BlockManager(512, 16)
+    s = Scheduler(bm, max_seqs_per_mb=16, max_model_len=128, admit_window_s=0.01,
+                  admit_min_frac=0.25, refill_interval_s=0.05)     # admit_min = 4
+    for i in range(14):
+        s.add_request(f"r{i}", [1, 2], SamplingParams(max_new_tokens=2 if i < 1 else 60))
+    m = s.schedule(0)
+    assert m.kind == 1 and m.num_seqs == 14
+    s.update(m, np.full(14, 3, np.int32))
+    for i in range(6):
+        s.add_request(f"q{i}", [4, 5], SamplingParams(max_new_tokens=60))
+    time.sleep(0.02)                                   # queued longer than the window
+    m = s.schedule(0)
+    assert m.kind == 2                                 # 2 free slots < 4: paced
+    s.update(m, np.full(m.num_seqs, 3, np.int32))      # r0 finishes: 3 free
+    assert s.schedule(0).kind == 2
+    time.sleep(0.05)
+    m = s.schedule(0)
+    assert m.kind == 1 and m.num_seqs == 3             # interval passed: refill the 3 slots
