@@ -23,6 +23,8 @@
 #include "common.h"
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+typedef const __attribute__((address_space(1))) void gbl_void;
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 #define PF_WAVES 4
 #define PF_QROWS 16
@@ -184,6 +186,261 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Long sequences: 8 waves x 32 query rows = 256 rows per workgroup, v_mfma_f32_32x32x16_bf16,
+// "swapped" products so that no value moves between lanes except one max exchange per tile:
+//   S^T[key, q] = K . Q^T        A = K rows from LDS (ds_read_b128), B = Q^T from registers;
+//                                each lane owns ONE query (its column) and 32 of the tile's
+//                                64 keys (its rows), so the row max / sum are lane-local
+//   O^T[d, q] += V^T . P^T       the S^T accumulator converted to bf16 IS the B operand
+//                                (cdna_hip_programming.md §3 'accumulator as operand': k-step s
+//                                = registers 8s..8s+7, keys 16s + 8(j>>2) + 4h + (j&3)); V^T
+//                                comes from ds_read_b64_tr_b16 reads of those key rows
+// so the online-softmax rescale of O^T is lane-local too. K/V tiles of 64 keys are staged
+// ONCE per workgroup (8 waves share them: half the LDS reads per FLOP of the 16-row kernel)
+// through registers into a double-buffered LDS image with the 256-B-row XOR swizzle that
+// keeps both the row reads and the transposed reads conflict-free (§5.5 T10 image (b)); the
+// next tile's global loads are in flight during the current tile (one barrier per tile).
+// Causal: key tiles stop at the workgroup's last row; a wave skips tiles entirely above its
+// rows and masks only tiles that cross its diagonal. Row blocks run longest-first.
+#define PL_WAVES 8
+#define PL_QROWS 32
+#define PL_ROWS (PL_WAVES * PL_QROWS)
+#define PL_KT 64
+// shortest max_seqlen that takes the 256-row kernel; below, the 64-row kernel wastes fewer
+// idle waves (settable for A/B runs and tests: dli_prefill_set_min_len)
+static int g_pl_min_len = 256;
+
+// Tile image: 8-row x 32-column subtiles of 512 B (cdna_hip_programming.md §5.5 T10, image
+// (a)): conflict-free for the 32x32x16 row reads (ds_read_b128) AND the transposed reads
+// (ds_read_b64_tr_b16), and every read's address is one of 2 lane bases + an immediate.
+__device__ __forceinline__ int pl_off(int row, int ch) {      // byte offset of 16-B chunk
+  return 2048 * (row >> 3) + 512 * (ch >> 2) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3));
+}
+__device__ __forceinline__ float pl_max3(float a, float b, float c) {  // no canonicalise
+  float r;
+  asm volatile("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+#define PL_RESCALE_THR 8.f      // log2 units: a running max is raised only by more than this
+
+template <int HD, bool PAGED>
+__global__ void __launch_bounds__(512) prefill_attn32_kernel(
+    u16* __restrict__ out, int out_stride, const u16* __restrict__ qkv, int row_stride,
+    const int* __restrict__ cu_seqlens, int hq, int hkv, float scale_log2,
+    const int* __restrict__ ctx_lens, const u16* __restrict__ k_cache,
+    const u16* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
+    int block_size) {
+  static_assert(HD == 128, "long-sequence kernel: head_dim 128");
+  constexpr int KC = HD / 16;                      // K-steps of the QK^T product
+  constexpr int DBK = HD / 32;                     // 32-wide d blocks of O^T
+  constexpr int TILE_B = PL_KT * HD * 2;           // bytes per K (or V) tile image
+  constexpr int NBUF = 3;
+  __shared__ __attribute__((aligned(16))) char lds[NBUF][2][TILE_B];   // [buf][K/V]
+  const int seq = blockIdx.y, h = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int qc = lane & 31, hi = lane >> 5;
+  const int s0 = cu_seqlens[seq], len = cu_seqlens[seq + 1] - s0;
+  const int nblk = (len + PL_ROWS - 1) / PL_ROWS;
+  const int blk = (int)(gridDim.x - 1 - blockIdx.x);            // longest blocks first
+  if (blk >= nblk) return;                                       // workgroup-uniform
+  const int nkeys = PAGED ? ctx_lens[seq] : len;
+  const int qoff = nkeys - len;
+  const int wg_q0 = blk * PL_ROWS;
+  const int q0 = wg_q0 + wid * PL_QROWS;                         // this wave's first row
+  const bool active = q0 < len;
+  const int G = hq / hkv, kvh = h / G;
+  const u16* kbase = qkv + (long)(hq + kvh) * HD;
+  const u16* vbase = qkv + (long)(hq + hkv + kvh) * HD;
+  const int* btab = PAGED ? block_tables + (long)seq * bt_stride : nullptr;
+  const long head_off = (long)kvh * block_size * HD;
+
+  // Q^T operand: lane (query qc, half hi) holds Q[q][16c + 8hi .. +7]
+  bf16x8 qf[KC];
+  {
+    const int qr = min(q0 + qc, len - 1);
+    const u16* qp = qkv + (long)(s0 + qr) * row_stride + (long)h * HD + 8 * hi;
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+      uint4 v = *reinterpret_cast<const uint4*>(qp + 16 * c);
+      qf[c] = *reinterpret_cast<bf16x8*>(&v);
+    }
+  }
+  const int qpos = qoff + q0 + qc;                 // position of this lane's query
+  const int wq_lo = qoff + q0, wq_hi = qoff + min(q0 + PL_QROWS, len) - 1;
+  const int kend_wg = min(nkeys, qoff + min(wg_q0 + PL_ROWS, len));
+  const int ntiles = (kend_wg + PL_KT - 1) / PL_KT;
+
+  f32x16 o[DBK];
+#pragma unroll
+  for (int i = 0; i < DBK; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
+  float m_run = -INFINITY, l_part = 0.f;
+
+  // global -> LDS by LDS-DMA (global_load_lds_dwordx4, no staging registers): an operand's
+  // tile image is 16 pieces of 1 KiB (= subtiles 2hp, 2hp+1 of 8-row group rg); wave w
+  // stages pieces w and w + 8 of K and of V. The DMA writes lane-linearly (lane L at byte
+  // 16L of the piece), so each lane loads the logical chunk that lands there.
+  auto stage = [&](int buf, int k0) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int piece = wid + 8 * j;
+      const int rg = piece >> 1, hp = piece & 1;
+      const int r = 8 * rg + ((lane & 31) >> 2);
+      const int c = 4 * (2 * hp + (lane >> 5)) + ((lane & 3) ^ ((r >> 2) & 3));
+      const int tok = min(k0 + r, nkeys - 1);
+      const u16 *ks, *vs;
+      if (PAGED) {
+        const long e = (long)btab[tok / block_size] * hkv * block_size * HD + head_off +
+                       (long)(tok % block_size) * HD + c * 8;
+        ks = k_cache + e;
+        vs = v_cache + e;
+      } else {
+        const long row = (long)(s0 + tok) * row_stride + c * 8;
+        ks = kbase + row;
+        vs = vbase + row;
+      }
+      __builtin_amdgcn_global_load_lds((gbl_void*)ks, (lds_void*)&lds[buf][0][piece * 1024],
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_void*)vs, (lds_void*)&lds[buf][1][piece * 1024],
+                                       16, 0, 0);
+    }
+  };
+
+  stage(0, 0);
+  if (ntiles > 1) {
+    stage(1, PL_KT);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");             // tile 0 landed
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  // LDS read bases (image (a)): K row reads of row 32 sub + qc, chunk 2c + hi; transposed V
+  // reads by 16-lane group g16, lane (q4, p4) of the group: rows 16 ks + 4 hi + q4 (+8)
+  const int g16 = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+  int kbase_off[2], vbase_off[2];
+#pragma unroll
+  for (int par = 0; par < 2; ++par)
+    kbase_off[par] = 2048 * (qc >> 3) + 64 * (qc & 7) + 16 * ((2 * par + hi) ^ ((qc >> 2) & 3));
+  {
+    const int cl = 2 * (g16 & 1) + (p4 >> 1);
+    vbase_off[0] = 64 * (4 * hi + q4) + 16 * (cl ^ hi) + 8 * (p4 & 1);
+    vbase_off[1] = 2048 + 64 * (4 * hi + q4) + 16 * (cl ^ (hi ^ 2)) + 8 * (p4 & 1);
+  }
+  // One barrier per tile: tile t+2 is DMA'd into the buffer tile t-1 used while tile t is
+  // computed; the counted vmcnt + barrier closing iteration t retire tile t+1. (A variant
+  // running the two 4-wave groups one half-tile apart measured 2x slower: the per-segment
+  // branches split the loop body and the compiler no longer interleaves the softmax VALU
+  // work with the MFMAs.)
+  f32x16 sacc[2];
+  int cur = 0;
+  for (int t = 0; t < ntiles; ++t) {
+    const int k0 = t * PL_KT;
+    if (t + 2 < ntiles) stage(cur == 0 ? 2 : cur - 1, k0 + 2 * PL_KT);
+    if (active && k0 <= wq_hi) {
+      const char* kt = lds[cur][0];
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sacc[sub][r] = 0.f;
+#pragma unroll
+        for (int c = 0; c < KC; ++c) {
+          // = pl_off(32 sub + qc, 2c + hi): lane base by c parity + immediate
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(
+              kt + kbase_off[c & 1] + 8192 * sub + 512 * (c >> 1));
+          sacc[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[c], sacc[sub], 0, 0, 0);
+        }
+      }
+      // mask (only tiles crossing this wave's diagonal or the key end)
+      if (k0 + PL_KT - 1 > wq_lo || k0 + PL_KT > nkeys) {
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = k0 + 32 * sub + (r & 3) + 8 * (r >> 2) + 4 * hi;
+            if (key > qpos || key >= nkeys) sacc[sub][r] = -INFINITY;
+          }
+      }
+      float mloc = pl_max3(sacc[0][0], sacc[0][1], sacc[0][2]);
+#pragma unroll
+      for (int r = 3; r < 15; r += 2) mloc = pl_max3(mloc, sacc[0][r], sacc[0][r + 1]);
+      mloc = pl_max3(mloc, sacc[0][15], sacc[1][0]);
+#pragma unroll
+      for (int r = 1; r < 15; r += 2) mloc = pl_max3(mloc, sacc[1][r], sacc[1][r + 1]);
+      mloc = pl_max3(mloc, sacc[1][15], sacc[1][15]);
+      mloc = pl_max3(mloc, __shfl_xor(mloc, 32, 64), mloc);
+      // deferred rescale (§5.5 T13): the running max moves only when the tile's max exceeds
+      // it by more than 2^PL_RESCALE_THR, so P <= 2^8 and O^T is rescaled on few tiles
+      float alpha = 1.f;
+      if ((mloc - m_run) * scale_log2 > PL_RESCALE_THR) {
+        alpha = m_run == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((m_run - mloc) * scale_log2);
+        m_run = mloc;
+      }
+      const float mc = (m_run == -INFINITY ? 0.f : m_run) * scale_log2;
+      float psum = 0.f;
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float e = __builtin_amdgcn_exp2f(fmaf(sacc[sub][r], scale_log2, -mc));
+          sacc[sub][r] = e;
+          psum += e;
+        }
+      l_part = l_part * alpha + psum;
+      if (__ballot(alpha != 1.f)) {
+#pragma unroll
+        for (int i = 0; i < DBK; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+      }
+      // O^T += V^T . P^T over 4 k-steps of 16 keys
+      const char* vt = lds[cur][1];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int sub = ks >> 1, s = ks & 1;
+        bf16x8 pb;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pb[j] = (__bf16)sacc[sub][8 * s + j];
+#pragma unroll
+        for (int db = 0; db < DBK; ++db) {
+          // rows 16 ks + 4hi + q4 (and +8), chunk 4db + 2(g16&1) + (p4>>1), half p4&1:
+          // pl_off + 8(p4&1) = vbase_off[0 or 1] + 4096 ks + 512 db
+          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s16x4*)(vt + vbase_off[0] + 4096 * ks + 512 * db));
+          const s16x4 up = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s16x4*)(vt + vbase_off[1] + 4096 * ks + 512 * db));
+          const s16x8 w = {lo[0], lo[1], lo[2], lo[3], up[0], up[1], up[2], up[3]};
+          o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(&w),
+                                                         pb, o[db], 0, 0, 0);
+        }
+      }
+    }
+    if (t + 2 < ntiles) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0xC07F);                          // lgkmcnt(0): own reads done
+    __builtin_amdgcn_s_barrier();
+    cur = (cur == 2) ? 0 : cur + 1;
+  }
+  if (!active) return;
+  const float l_tot = l_part + __shfl_xor(l_part, 32, 64);
+  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  const int qr = q0 + qc;
+  if (qr < len) {
+    u16* op = out + (long)(s0 + qr) * out_stride + (long)h * HD;
+#pragma unroll
+    for (int db = 0; db < DBK; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        U16x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v.v[r] = f2bf(o[db][4 * g + r] * inv);
+        *reinterpret_cast<U16x4*>(op + 32 * db + 8 * g + 4 * hi) = v;
+      }
+  }
+}
+
 template <bool PAGED>
 static int launch_prefill(void* out, int out_stride, const void* qkv, int row_stride,
                           const int* cu_seqlens, int num_seqs, int max_seqlen, int hq, int hkv,
@@ -192,9 +449,16 @@ static int launch_prefill(void* out, int out_stride, const void* qkv, int row_st
                           int block_size, hipStream_t st) {
   if (num_seqs <= 0 || max_seqlen <= 0) return 0;
   if (hq % hkv || (hd != 64 && hd != 128)) return (int)hipErrorInvalidValue;
+  const float sl2 = scale * 1.4426950408889634f;
+  if (hd == 128 && max_seqlen >= g_pl_min_len) {     // long sequences: 256-row workgroups
+    dim3 grid32((max_seqlen + PL_ROWS - 1) / PL_ROWS, num_seqs, hq);
+    prefill_attn32_kernel<128, PAGED><<<grid32, 512, 0, st>>>(
+        (u16*)out, out_stride, (const u16*)qkv, row_stride, cu_seqlens, hq, hkv, sl2, ctx_lens,
+        (const u16*)k_cache, (const u16*)v_cache, block_tables, bt_stride, block_size);
+    DLI_RETURN_LAUNCH();
+  }
   const int rows_per_wg = PF_WAVES * PF_QROWS;
   dim3 grid((max_seqlen + rows_per_wg - 1) / rows_per_wg, num_seqs, hq);
-  const float sl2 = scale * 1.4426950408889634f;
   if (hd == 128)
     prefill_attn_kernel<128, PAGED><<<grid, 256, 0, st>>>(
         (u16*)out, out_stride, (const u16*)qkv, row_stride, cu_seqlens, hq, hkv, sl2, ctx_lens,
@@ -227,4 +491,10 @@ extern "C" int dli_prefill_attention_paged(void* out, int out_stride, const void
   return launch_prefill<true>(out, out_stride, qkv, row_stride, cu_seqlens, num_seqs,
                               max_seqlen, hq, hkv, hd, scale, ctx_lens, k_cache, v_cache,
                               block_tables, bt_stride, block_size, st);
+}
+
+extern "C" int dli_prefill_set_min_len(int n) {
+  const int old = g_pl_min_len;
+  if (n > 0) g_pl_min_len = n;
+  return old;
 }
