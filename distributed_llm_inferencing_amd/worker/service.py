@@ -8,6 +8,7 @@ continuous-batching scheduler and steps it, so concurrent requests share every d
 """
 from __future__ import annotations
 
+import contextlib
 import queue
 import threading
 import time
@@ -56,9 +57,14 @@ class EngineService:
             except Exception as e:  # noqa: BLE001
                 fut.set_exception(e)
 
+    def _phase(self, name):
+        t = getattr(self.engine, "timer", None)
+        return t.phase(name) if t is not None else contextlib.nullcontext()
+
     def _run(self):
         while not self._stop.is_set():
-            self._admit()
+            with self._phase("svc_admit"):
+                self._admit()
             if not self.engine.has_work():
                 self._wake.wait(0.05)
                 self._wake.clear()
@@ -73,13 +79,16 @@ class EngineService:
                 self._futures.clear()
                 time.sleep(0.1)
                 continue
-            for o in outs:
-                f = self._futures.pop(o.request_id, None)
-                if f is not None and not f.done():
-                    f.set_result(o)
+            with self._phase("svc_resolve"):
+                for o in outs:
+                    f = self._futures.pop(o.request_id, None)
+                    if f is not None and not f.done():
+                        f.set_result(o)
 
     def stats(self) -> dict:
         s = self.engine.stats.snapshot() if hasattr(self.engine, "stats") else {}
+        if getattr(self.engine, "timer", None) is not None:
+            s["phases"] = self.engine.timer.snapshot()     # host time per engine-loop phase
         s["queued"] = self._inbox.qsize()
         s["in_flight"] = len(self._futures)
         return s
