@@ -282,6 +282,13 @@ def prefill_attention(qkv, cu_seqlens, max_seqlen: int, hq, hkv, hd, scale, out=
     return out
 
 
+def decode_pipelined(v: int) -> int:
+    """Select the pipelined (1), one-tile-per-round (0) or automatic (2: pipelined for KV
+    splits of >= 768 tokens) decode attention kernel for head_dim 128 (-1: from
+    DLI_DECODE_PIPE, default 2). Returns the previous setting."""
+    return int(N.require_native().dli_decode_set_pipe(int(v)))
+
+
 def prefill_long_min_len(n: int = 0) -> int:
     """Shortest max_seqlen routed to the 256-row (32x32x16) prefill attention kernel; n > 0
     sets it. Returns the previous value (A/B runs and tests force either kernel with it)."""

@@ -38,14 +38,25 @@ def main():
         lens = torch.full((B,), ctx, dtype=torch.int32, device=dev)
         qkv = torch.randn(B, (hq + 2 * hkv) * hd, device=dev).to(torch.bfloat16)
         sc = 1 / math.sqrt(hd)
-        out = ops.decode_attention(qkv, kc, vc, tables, lens, ctx, hq, hkv, hd, sc)
         ref = R.decode_attention(qkv[:, : hq * hd].reshape(B, hq, hd).float(), kc.float(),
                                  vc.float(), tables, lens, sc).reshape(B, hq * hd)
-        err = (out.float() - ref.float()).abs().max().item()
-        ms = ops.benchmark(lambda: ops.decode_attention(qkv, kc, vc, tables, lens, ctx, hq, hkv,
-                                                        hd, sc), iters=50)
         kv_bytes = B * ctx * hkv * hd * 2 * 2
-        rec = {"B": B, "ctx": ctx, "us": ms * 1e3, "TBps": kv_bytes / ms / 1e9, "max_err": err}
+        rec = {"B": B, "ctx": ctx}
+        times = {0: [], 1: []}
+        for v in (0, 1):                   # one-tile-per-round vs pipelined kernel
+            ops.decode_pipelined(v)
+            out = ops.decode_attention(qkv, kc, vc, tables, lens, ctx, hq, hkv, hd, sc)
+            rec[f"max_err_{v}"] = (out.float() - ref.float()).abs().max().item()
+        for _ in range(5):                 # interleaved rounds
+            for v in (0, 1):
+                ops.decode_pipelined(v)
+                times[v].append(ops.benchmark(lambda: ops.decode_attention(
+                    qkv, kc, vc, tables, lens, ctx, hq, hkv, hd, sc), iters=20))
+        ops.decode_pipelined(-1)
+        for v, name in ((0, "round"), (1, "pipe")):
+            ms = sorted(times[v])[len(times[v]) // 2]
+            rec[f"us_{name}"] = ms * 1e3
+            rec[f"TBps_{name}"] = kv_bytes / ms / 1e9
         res.append(rec)
         print(json.dumps(rec), flush=True)
     Path(a.out).parent.mkdir(parents=True, exist_ok=True)

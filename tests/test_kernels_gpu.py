@@ -225,10 +225,15 @@ def test_decode_attention_paged(gpu, hq, hkv, hd, bs, lens):
     scale = 1 / math.sqrt(hd)
     q = qkv[:, : hq * hd].reshape(len(lens), hq, hd)
     ref = R.decode_attention(q, kc, vc, tables, ctx, scale).reshape(len(lens), -1)
-    for splits in (1, 2, 4):
-        out = ops.decode_attention(qkv, kc, vc, tables, ctx, max(lens), hq, hkv, hd, scale,
-                                   num_splits=splits)
-        close(out, ref, rtol=2e-2, atol=2e-2)
+    for pipe in (1, 0):                      # pipelined and one-tile-per-round kernels
+        old = ops.decode_pipelined(pipe)
+        try:
+            for splits in (1, 2, 4):
+                out = ops.decode_attention(qkv, kc, vc, tables, ctx, max(lens), hq, hkv, hd,
+                                           scale, num_splits=splits)
+                close(out, ref, rtol=2e-2, atol=2e-2)
+        finally:
+            ops.decode_pipelined(old)
 
 
 def test_sampling_greedy_and_support(gpu):
@@ -545,10 +550,15 @@ def test_decode_attention_32k_context(gpu):
     scale = 1 / math.sqrt(hd)
     q = qkv[:, : hq * hd].reshape(len(lens), hq, hd)
     ref = R.decode_attention(q, kc, vc, tables, ctx, scale).reshape(len(lens), -1)
-    for splits in (None, 8, 32):
-        out = ops.decode_attention(qkv, kc, vc, tables, ctx, max(lens), hq, hkv, hd, scale,
-                                   num_splits=splits)
-        close(out, ref, rtol=2e-2, atol=2e-2)
+    for pipe in (1, 0):                      # pipelined and one-tile-per-round kernels
+        old = ops.decode_pipelined(pipe)
+        try:
+            for splits in (None, 8, 32):
+                out = ops.decode_attention(qkv, kc, vc, tables, ctx, max(lens), hq, hkv, hd,
+                                           scale, num_splits=splits)
+                close(out, ref, rtol=2e-2, atol=2e-2)
+        finally:
+            ops.decode_pipelined(old)
 
 
 @pytest.mark.parametrize("hq,hkv,hd,bs,chunks", [
