@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <deque>
 #include <mutex>
 #include <unordered_map>
 #include <vector>
@@ -22,15 +23,61 @@ struct BlockManager {
   int block_size;
   std::vector<int> free_list;                              // stack of free block ids
   std::unordered_map<long long, std::vector<int>> tables;  // seq id -> blocks
+  // automatic prefix caching: a FULL block whose tokens (and all tokens before them) are
+  // known carries a chain hash; a later sequence with the same prefix maps the same block
+  // (refcount) instead of recomputing its KV. A block released by its last user keeps its
+  // hash and content and waits in `evictable` (oldest first) until the pool runs dry.
+  std::vector<int> refcnt;
+  std::vector<unsigned long long> hash_of;                 // 0 = no hash
+  std::unordered_map<unsigned long long, int> cached;      // hash -> block
+  std::deque<int> evictable;                               // lazily pruned (refcnt > 0)
+  int n_evictable = 0;
+  long long hits = 0;                                      // blocks served from the cache
   std::mutex mu;
 
-  BlockManager(int nb, int bs) : num_blocks(nb), block_size(bs) {
+  BlockManager(int nb, int bs)
+      : num_blocks(nb), block_size(bs), refcnt(nb, 0), hash_of(nb, 0ull) {
     free_list.reserve(nb);
     // hand out low block ids first (LIFO stack, reversed fill)
     for (int b = nb - 1; b >= 0; --b) free_list.push_back(b);
   }
   int blocks_for(long long tokens) const {
     return (int)((tokens + block_size - 1) / block_size);
+  }
+  int available() const { return (int)free_list.size() + n_evictable; }
+  // a block for exclusive use: a never-hashed free one first, else evict the oldest cached
+  int alloc() {
+    if (!free_list.empty()) {
+      const int b = free_list.back();
+      free_list.pop_back();
+      refcnt[b] = 1;
+      return b;
+    }
+    while (!evictable.empty()) {
+      const int b = evictable.front();
+      evictable.pop_front();
+      if (refcnt[b] != 0 || hash_of[b] == 0) continue;       // revived / stale entry
+      cached.erase(hash_of[b]);
+      hash_of[b] = 0;
+      --n_evictable;
+      refcnt[b] = 1;
+      return b;
+    }
+    return -1;
+  }
+  void release(int b) {
+    if (--refcnt[b] > 0) return;
+    if (hash_of[b] != 0) {
+      evictable.push_back(b);
+      ++n_evictable;
+    } else {
+      free_list.push_back(b);
+    }
+  }
+  bool grow(std::vector<int>& tab, int need) {               // all-or-nothing
+    if (available() < need) return false;
+    for (int i = 0; i < need; ++i) tab.push_back(alloc());
+    return true;
   }
 };
 
@@ -49,7 +96,7 @@ void dli_bm_destroy(void* h) { delete H(h); }
 
 int dli_bm_num_free(void* h) {
   std::lock_guard<std::mutex> g(H(h)->mu);
-  return (int)H(h)->free_list.size();
+  return H(h)->available();
 }
 
 int dli_bm_num_blocks(void* h) { return H(h)->num_blocks; }
@@ -71,13 +118,9 @@ int dli_bm_ensure(void* h, long long seq, long long total_tokens) {
   auto& tab = m->tables[seq];
   const int need = m->blocks_for(total_tokens) - (int)tab.size();
   if (need <= 0) return 0;
-  if ((int)m->free_list.size() < need) {
+  if (!m->grow(tab, need)) {
     if (tab.empty()) m->tables.erase(seq);
     return -1;
-  }
-  for (int i = 0; i < need; ++i) {
-    tab.push_back(m->free_list.back());
-    m->free_list.pop_back();
   }
   return need;
 }
@@ -91,13 +134,9 @@ int dli_bm_ensure_batch(void* h, const long long* seqs, const int* totals, int n
     auto& tab = m->tables[seqs[i]];
     const int need = m->blocks_for(totals[i]) - (int)tab.size();
     if (need <= 0) continue;
-    if ((int)m->free_list.size() < need) {
+    if (!m->grow(tab, need)) {
       if (tab.empty()) m->tables.erase(seqs[i]);
       return i;
-    }
-    for (int k = 0; k < need; ++k) {
-      tab.push_back(m->free_list.back());
-      m->free_list.pop_back();
     }
   }
   return n;
@@ -110,8 +149,7 @@ int dli_bm_free(void* h, long long seq) {
   auto it = m->tables.find(seq);
   if (it == m->tables.end()) return 0;
   const int n = (int)it->second.size();
-  for (auto it2 = it->second.rbegin(); it2 != it->second.rend(); ++it2)
-    m->free_list.push_back(*it2);
+  for (auto it2 = it->second.rbegin(); it2 != it->second.rend(); ++it2) m->release(*it2);
   m->tables.erase(it);
   return n;
 }
@@ -125,8 +163,7 @@ int dli_bm_free_batch(void* h, const long long* seqs, int n) {
     auto it = m->tables.find(seqs[i]);
     if (it == m->tables.end()) continue;
     total += (int)it->second.size();
-    for (auto it2 = it->second.rbegin(); it2 != it->second.rend(); ++it2)
-      m->free_list.push_back(*it2);
+    for (auto it2 = it->second.rbegin(); it2 != it->second.rend(); ++it2) m->release(*it2);
     m->tables.erase(it);
   }
   return total;
@@ -178,15 +215,9 @@ int dli_bm_decode_prepare(void* h, const long long* seqs, const int* ctx, int n,
   for (int i = 0; i < n; ++i) {
     auto& tab = m->tables[seqs[i]];
     const int need = m->blocks_for(ctx[i]) - (int)tab.size();
-    if (need > 0) {
-      if ((int)m->free_list.size() < need) {
-        if (tab.empty()) m->tables.erase(seqs[i]);
-        return -(i + 1);
-      }
-      for (int k = 0; k < need; ++k) {
-        tab.push_back(m->free_list.back());
-        m->free_list.pop_back();
-      }
+    if (need > 0 && !m->grow(tab, need)) {
+      if (tab.empty()) m->tables.erase(seqs[i]);
+      return -(i + 1);
     }
     const int cnt = (int)tab.size();
     if (cnt > max_blocks) return -(n + 1);
@@ -218,6 +249,60 @@ int dli_bm_slot_mapping(void* h, const long long* seqs, const int* starts, const
     }
   }
   return (int)o;
+}
+
+// Prefix caching. A new sequence `seq` (no blocks yet) maps the longest run of cached blocks
+// whose chain hashes are hashes[0..n): returns the number of blocks mapped (their tokens need
+// no prefill). Each mapped block gains a reference.
+int dli_bm_match_prefix(void* h, long long seq, const unsigned long long* hashes, int n) {
+  auto* m = H(h);
+  std::lock_guard<std::mutex> g(m->mu);
+  auto& tab = m->tables[seq];
+  if (!tab.empty()) return 0;
+  int k = 0;
+  for (; k < n; ++k) {
+    auto it = m->cached.find(hashes[k]);
+    if (it == m->cached.end()) break;
+    const int b = it->second;
+    if (m->refcnt[b] == 0) --m->n_evictable;                // revived (queue entry goes stale)
+    ++m->refcnt[b];
+    tab.push_back(b);
+  }
+  if (tab.empty()) m->tables.erase(seq);
+  m->hits += k;
+  return k;
+}
+
+// Publish blocks [first, first + n) of `seq` (their KV is written by a step already queued
+// on the device) under hashes[0..n) so later sequences can map them. A hash that is already
+// cached (another sequence computed the same prefix) is left alone. Returns blocks added.
+int dli_bm_register_prefix(void* h, long long seq, const unsigned long long* hashes,
+                           int first, int n) {
+  auto* m = H(h);
+  std::lock_guard<std::mutex> g(m->mu);
+  auto it = m->tables.find(seq);
+  if (it == m->tables.end()) return 0;
+  const auto& tab = it->second;
+  int added = 0;
+  for (int k = 0; k < n && first + k < (int)tab.size(); ++k) {
+    const int b = tab[first + k];
+    const unsigned long long hv = hashes[k];
+    if (hv == 0 || m->hash_of[b] != 0 || m->cached.count(hv)) continue;
+    m->hash_of[b] = hv;
+    m->cached[hv] = b;
+    ++added;
+  }
+  return added;
+}
+
+long long dli_bm_prefix_hits(void* h) {
+  std::lock_guard<std::mutex> g(H(h)->mu);
+  return H(h)->hits;
+}
+
+int dli_bm_num_cached(void* h) {
+  std::lock_guard<std::mutex> g(H(h)->mu);
+  return (int)H(h)->cached.size();
 }
 
 }  // extern "C"

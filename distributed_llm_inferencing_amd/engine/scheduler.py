@@ -138,13 +138,26 @@ class _MBCore:
                 s.output_ids.extend(row)
 
 
+try:                                   # 64-bit block hashes (collisions ~2^-64 per pair)
+    import xxhash as _xxhash
+
+    def _hash64(b: bytes) -> int:
+        return _xxhash.xxh3_64_intdigest(b)
+except ImportError:                    # pragma: no cover - xxhash ships in the image
+    import hashlib as _hashlib
+
+    def _hash64(b: bytes) -> int:
+        return int.from_bytes(_hashlib.blake2b(b, digest_size=8).digest(), "little")
+
+
 class Scheduler:
     def __init__(self, block_manager: BlockManager, max_seqs_per_mb: int = 256,
                  max_prefill_tokens: int = 16384, num_microbatches: int = 1,
                  eos_token_id: Optional[int] = None, max_model_len: int = 4096,
                  table_width: Optional[int] = None, native_decode: bool = False,
                  admit_window_s: Optional[float] = None, admit_min_frac: float = 0.125,
-                 refill_interval_s: Optional[float] = None):
+                 refill_interval_s: Optional[float] = None,
+                 prefix_caching: Optional[bool] = None):
         self.bm = block_manager
         self.bs = block_manager.block_size
         self.max_seqs = max_seqs_per_mb
@@ -184,6 +197,13 @@ class Scheduler:
         self.refill_interval_s = (float(os.environ.get("DLI_REFILL_INTERVAL_S", "0.06"))
                                   if refill_interval_s is None else refill_interval_s)
         self._last_admit = [0.0] * num_microbatches
+        # automatic prefix caching: a new sequence maps the cached KV blocks of its longest
+        # known full-block prefix (chain hashes of the token blocks) and prefills only the
+        # rest, as a chunk over the paged cache; full prompt blocks are published when their
+        # prefill is scheduled (the device runs steps in order)
+        self.prefix_caching = (os.environ.get("DLI_PREFIX_CACHE", "1") == "1"
+                               if prefix_caching is None else bool(prefix_caching))
+        self.prefix_hit_tokens = 0
         self._next_id = 0
         self._step = 0
         self._deadlines = 0
@@ -320,6 +340,34 @@ class Scheduler:
         loads = [len(r) for r in self.running]
         return len(self.running[mb]) <= min(loads)
 
+    def _block_hashes(self, seq: Sequence, nblocks: int) -> np.ndarray:
+        """Chain hashes of the first ``nblocks`` full token blocks of ``seq`` (a block's hash
+        covers every token before it too)."""
+        ids = np.asarray(seq.prompt_ids + seq.output_ids if seq.output_ids else seq.prompt_ids,
+                         dtype=np.int32)
+        bs = self.bs
+        out = np.empty(nblocks, np.uint64)
+        h = 0
+        for i in range(nblocks):
+            h = _hash64(h.to_bytes(8, "little") + ids[i * bs:(i + 1) * bs].tobytes()) or 1
+            out[i] = h
+        return out
+
+    def _match_prefix(self, seq: Sequence) -> None:
+        if not self.prefix_caching or seq.num_prefilled or seq.total_len <= self.bs:
+            return
+        nb = (seq.total_len - 1) // self.bs          # keep >= 1 token to compute
+        m = self.bm.match_prefix(seq.seq_id, self._block_hashes(seq, nb))
+        if m:
+            seq.num_prefilled = m * self.bs
+            self.prefix_hit_tokens += m * self.bs
+
+    def _unmatch(self, seq: Sequence) -> None:
+        if seq.num_prefilled:
+            self.bm.free(seq.seq_id)
+            self.prefix_hit_tokens -= seq.num_prefilled
+            seq.num_prefilled = 0
+
     def _try_prefill(self, mb: int) -> Optional[StepMeta]:
         partial = self.prefilling[mb]
         if partial:
@@ -362,11 +410,13 @@ class Scheduler:
             for seq in self.waiting:
                 if len(new) >= room or budget <= 0:
                     break
-                n = seq.total_len
+                self._match_prefix(seq)              # cached prefix blocks need no prefill
+                n = seq.total_len - seq.num_prefilled
                 if n > budget and (new or n_cont or n <= self.max_prefill_tokens):
+                    self._unmatch(seq)
                     break                    # whole prompts only, except a chunked first
                 new.append(seq)
-                new_lens.append(n)
+                new_lens.append(seq.total_len)
                 budget -= min(n, budget)
         if new:
             self._last_admit[mb] = time.perf_counter()
@@ -374,14 +424,16 @@ class Scheduler:
             # stops at the first that does not fit
             sid_new = np.fromiter((s.seq_id for s in new), np.int64, len(new))
             got = self.bm.ensure_batch(sid_new, np.asarray(new_lens, dtype=np.int32))
+            for s in new[got:]:
+                self._unmatch(s)
             new = new[:got]
             for _ in range(got):
                 self.waiting.popleft()
             budget = self.max_prefill_tokens - sum(lens_l)
             for s in new:
-                n = min(s.total_len, budget)
+                n = min(s.total_len - s.num_prefilled, budget)
                 picked.append(s)
-                starts_l.append(0)
+                starts_l.append(s.num_prefilled)
                 lens_l.append(n)
                 budget -= n
         if not picked:
@@ -390,7 +442,8 @@ class Scheduler:
         sid = np.fromiter((s.seq_id for s in picked), np.int64, S)
         starts = np.asarray(starts_l, dtype=np.int32)
         lens = np.asarray(lens_l, dtype=np.int32)
-        chunked = n_cont > 0 or any(n < s.total_len for s, n in zip(new, lens_l[n_cont:]))
+        chunked = any(st > 0 or st + n < s.total_len
+                      for s, st, n in zip(picked, starts_l, lens_l))
         final = np.fromiter((st + n == s.total_len for s, st, n in zip(picked, starts_l, lens_l)),
                             np.bool_, S)
         joined = False
@@ -403,6 +456,9 @@ class Scheduler:
                 s.state = SeqState.RUNNING
                 self.running[mb].append(s)
                 joined = True
+                if self.prefix_caching and s.total_len >= self.bs:
+                    self.bm.register_prefix(s.seq_id,
+                                            self._block_hashes(s, s.total_len // self.bs))
             elif s.state != SeqState.PREFILLING:
                 s.state = SeqState.PREFILLING
                 partial.append(s)

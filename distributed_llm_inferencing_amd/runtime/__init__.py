@@ -38,6 +38,10 @@ _SIGS = {
     "dli_bm_slot_mapping": ([_P, _P, _P, _P, _I, _P], _I),
     "dli_bm_decode_prepare": ([_P, _P, _P, _I, _P, _P, _I], _I),
     "dli_bm_ensure_batch": ([_P, _P, _P, _I], _I),
+    "dli_bm_match_prefix": ([_P, _LL, _P, _I], _I),
+    "dli_bm_register_prefix": ([_P, _LL, _P, _I, _I], _I),
+    "dli_bm_prefix_hits": ([_P], _LL),
+    "dli_bm_num_cached": ([_P], _I),
     "dli_mb_create": ([_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I], _P),
     "dli_mb_destroy": ([_P], None),
     "dli_mb_rows": ([_P], _I),
@@ -160,6 +164,31 @@ class BlockManager:
         if r < 0:
             return -1, -r - 1, None
         return slots, tables, r
+
+    # ---- automatic prefix caching (csrc/runtime/block_manager.cpp)
+    def match_prefix(self, seq_id: int, hashes: np.ndarray) -> int:
+        """Map the longest run of cached blocks with chain hashes ``hashes`` (uint64) as the
+        first blocks of new sequence ``seq_id``; returns the number of blocks mapped."""
+        h = np.ascontiguousarray(hashes, dtype=np.uint64)
+        if h.shape[0] == 0:
+            return 0
+        return lib().dli_bm_match_prefix(self._h, int(seq_id), _np_ptr(h), h.shape[0])
+
+    def register_prefix(self, seq_id: int, hashes: np.ndarray, first_block: int = 0) -> int:
+        """Publish blocks [first_block, first_block + len(hashes)) of ``seq_id``."""
+        h = np.ascontiguousarray(hashes, dtype=np.uint64)
+        if h.shape[0] == 0:
+            return 0
+        return lib().dli_bm_register_prefix(self._h, int(seq_id), _np_ptr(h), int(first_block),
+                                            h.shape[0])
+
+    @property
+    def prefix_hits(self) -> int:
+        return int(lib().dli_bm_prefix_hits(self._h))
+
+    @property
+    def num_cached(self) -> int:
+        return int(lib().dli_bm_num_cached(self._h))
 
     def slot_mapping(self, seq_ids, starts, counts) -> np.ndarray:
         ids = np.asarray(seq_ids, dtype=np.int64)

@@ -87,6 +87,9 @@ class EngineService:
 
     def stats(self) -> dict:
         s = self.engine.stats.snapshot() if hasattr(self.engine, "stats") else {}
+        sch = getattr(self.engine, "scheduler", None)
+        if sch is not None:
+            s["prefix_hit_tokens"] = sch.prefix_hit_tokens
         if getattr(self.engine, "timer", None) is not None:
             s["phases"] = self.engine.timer.snapshot()     # host time per engine-loop phase
         s["queued"] = self._inbox.qsize()
