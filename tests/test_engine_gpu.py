@@ -76,3 +76,42 @@ def test_loopback_pipeline_on_gpu_matches_single_stage(gpu, n):
         pp = LocalPipeline("llama-tiny", n, device="cuda", max_batch=8, max_model_len=128,
                            num_blocks=64, seed=2)
         assert [o.all_ids for o in pp.generate(prompts, sp)] == [o.all_ids for o in ref]
+
+
+@pytest.mark.parametrize("name", ["llama3-70b", "mixtral-8x7b"])
+def test_real_shape_layers_close_to_hf_fp32(gpu, name):
+    """Llama-3-70B and Mixtral-8x7B at their real layer shapes (hidden 8192 / 64 heads / GQA 8
+    / FFN 28672; hidden 4096 / 8 experts x FFN 14336, top-2) and real vocabularies, 2 layers
+    each: prefill logits of the HIP path vs HF transformers in fp32 on the same weights."""
+    torch.manual_seed(0)
+    cfg = get_config(name, num_layers=2)
+    with torch.device(gpu):
+        hm = hf_model(cfg)
+    ids = IDS + [1234, 4321, 777]
+    with torch.no_grad():
+        ref = hm(torch.tensor([ids], device=gpu)).logits[0, -1].float().cpu()
+        params = from_hf_state_dict(cfg, hm.state_dict(), dtype=torch.bfloat16)
+    del hm
+    params = {k: v.to(gpu) for k, v in params.items()}
+    ours = our_last_logits(cfg, params, ids, device=gpu).float().cpu()
+    err = (ours - ref).abs().max().item()
+    assert err < 0.05 * ref.abs().max().item() + 0.02, err
+
+
+@pytest.mark.parametrize("name", ["llama3-70b", "mixtral-8x7b"])
+def test_real_shape_engine_decode(gpu, name, monkeypatch):
+    """The serving path at real layer shapes (2 layers): continuous batching, graph-captured
+    decode with autotuned GEMM plans and fused split-K reduces (N = 8192 rows for 70B),
+    grouped expert GEMMs (Mixtral); graph decode equals eager decode token for token."""
+    monkeypatch.setenv("DLI_GEMM_AUTOTUNE", "0")      # same GEMM plans on both sides
+    prompts = [IDS[:5], IDS[:9], IDS[3:14]]
+    sp = SamplingParams(max_length=24, seed=5, ignore_eos=True)
+    outs = []
+    for graphs in (False, True):
+        eng = LLMEngine(name, device="cuda", max_batch=4, max_model_len=64, num_blocks=64,
+                        num_layers=2, use_graphs=graphs, seed=1)
+        outs.append([o.output_ids for o in eng.generate(prompts, sp)])
+        assert all(len(o) == 24 - len(p) for o, p in zip(outs[-1], prompts))
+        del eng
+        torch.cuda.empty_cache()
+    assert outs[0] == outs[1]
