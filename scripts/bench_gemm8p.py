@@ -60,7 +60,7 @@ def main():
     ap.add_argument("--iters", type=int, default=4)
     ap.add_argument("--out", default="gpurun_out/gemm8p.json")
     ap.add_argument("--only", default="")
-    ap.add_argument("--tiles", default="13,22")
+    ap.add_argument("--tiles", default="13,22,26")
     a = ap.parse_args()
     dev = torch.device("cuda")
     torch.manual_seed(0)

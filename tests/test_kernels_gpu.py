@@ -79,6 +79,22 @@ def test_gemm_bf16_all_tiles(gpu, M, N, K):
             close(out, ref, rtol=1e-2, atol=1e-2)
 
 
+@pytest.mark.parametrize("M,N,K,epi", [(512, 28672, 4096, "silu_mul"), (500, 2240, 14336, "none"),
+                                       (1000, 7168, 1024, "f32")])
+def test_gemm_256x224_pingpong(gpu, M, N, K, epi):
+    """Tile 26 (256x224 ping-pong) at the Llama-3 gate/up decode shape and with long K /
+    partial M tiles, against the fp32 reference."""
+    torch.manual_seed(5)
+    x, w = rnd(M, K, dev=gpu), rnd(N, K, dev=gpu, scale=0.05)
+    if epi == "silu_mul":
+        ref = R.silu_mul(R.linear(x, w).float().to(BF))
+    else:
+        ref = R.linear(x, w, out_dtype=torch.float32)
+    for splits in (1, 2):
+        out = ops._gemm_native(x, w, epi, plan=G.GemmPlan("dli", 26, splits))
+        close(out, ref, rtol=2e-2, atol=2e-2)
+
+
 def test_gemm_asymmetric_identity(gpu):
     """A = I with asymmetric B catches a transposed C write (cdna_hip_programming.md §3)."""
     n = 128
@@ -102,7 +118,7 @@ def test_gemm_epilogues(gpu, epi, M, N, K):
         ref = R.gelu_tanh(R.linear(x, w, b))
     else:
         ref = R.linear(x, w, b)
-    for tile in (0, 2, 13, 14, 20, 22):
+    for tile in (0, 2, 13, 14, 20, 22, 26):
         for splits in (1, 2):
             out = ops._gemm_native(x, w, epi, bias=b if "bias" in epi else None,
                                    plan=G.GemmPlan("dli", tile, splits))
