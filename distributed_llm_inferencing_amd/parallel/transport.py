@@ -99,8 +99,25 @@ class PipeChannel:
                 w.wait()
             if int(r.item()) != self.prev:
                 raise RuntimeError(f"pipeline ring check failed on rank {self.rank}")
+        # DLI_PP_COMM=rccl: the data plane on this module's own RCCL communicator
+        # (csrc/runtime/comm.cpp), enqueued on the compute stream; default: torch.distributed
+        self.rccl = None
+        if self.world > 1 and self.nccl and os.environ.get("DLI_PP_COMM", "torch") == "rccl":
+            self._init_rccl()
 
     # ------------------------------------------------------------------ setup
+    def _init_rccl(self) -> None:
+        from ..runtime import RcclComm
+        box = [RcclComm.unique_id() if self.rank == 0 else None]
+        dist.broadcast_object_list(box, src=0, group=self.ctrl_group)
+        self.rccl = RcclComm(box[0], self.world, self.rank)
+        t = torch.full((1,), float(self.rank), device=self.device)
+        r = torch.empty(1, device=self.device)
+        self.rccl.exchange([(t, self.next)], [(r, self.prev)],
+                           torch.cuda.current_stream(self.device).cuda_stream)
+        if int(r.item()) != self.prev:
+            raise RuntimeError(f"RCCL ring check failed on rank {self.rank}")
+
     def _init_ctrl(self, mode: str) -> None:
         hosts = [None] * self.world
         dist.all_gather_object(hosts, socket.gethostname(), group=self.ctrl_group)
@@ -210,6 +227,15 @@ class PipeChannel:
         RCCL: every Work is waited on the CURRENT stream — a stream dependency, not a host
         wait — so the next kernels on this stream (the consumer replay, or the replay that
         rewrites a sent static output) run after the transfer. gloo: a host wait."""
+        if self.rccl is not None:            # stream-ordered, no waits (comm.cpp)
+            with trace_range("pp.exchange"):
+                self.rccl.exchange(
+                    [(t.contiguous(), peer) for t, peer, _ in sends
+                     if t is not None and t.numel()],
+                    [(b, peer) for b, peer, _ in recvs if b.numel()],
+                    torch.cuda.current_stream(self.device).cuda_stream)
+            self.exchanges += 1
+            return
         ops = []
         with trace_range("pp.exchange"):
             for t, peer, tag in sends:
@@ -240,6 +266,9 @@ class PipeChannel:
             w.wait()
 
     def close(self) -> None:
+        if getattr(self, "rccl", None) is not None:
+            self.rccl.close()
+            self.rccl = None
         if self.ring is not None:
             if self.rank == 0:
                 self.ring.close()

@@ -71,6 +71,13 @@ _SIGS = {
     "dli_ring_min_consumed": ([_P], _LL),
     "dli_ring_close": ([_P], None),
     "dli_ring_destroy": ([_P], None),
+    "dli_comm_available": ([], _I),
+    "dli_comm_error_string": ([_I], ctypes.c_char_p),
+    "dli_comm_unique_id": ([_P], _I),
+    "dli_comm_id_bytes": ([], _I),
+    "dli_comm_init": ([_P, _P, _I, _I], _I),
+    "dli_comm_destroy": ([_P], _I),
+    "dli_comm_exchange": ([_P, _P, _I, _P, _P, _P, _I, _P, _P, _P], _I),
 }
 
 
@@ -429,5 +436,67 @@ class ShmRing:
     def __del__(self):
         try:
             self.destroy()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+class RcclComm:
+    """A pipeline's RCCL communicator driven directly (``csrc/runtime/comm.cpp``): a tick's
+    sends and receives go out in one ncclGroupStart/End on the caller's stream (the stage's
+    compute stream), ordered with the kernels around them without events or host waits.
+    ``uid`` is the 128-byte id from ``RcclComm.unique_id()`` on rank 0, shared by every rank
+    (the pipeline ships it over its gloo control group)."""
+
+    def __init__(self, uid: bytes, world: int, rank: int):
+        L = lib()
+        if not L.dli_comm_available():
+            raise RuntimeError("RCCL (librccl.so.1) could not be loaded")
+        h = ctypes.c_void_p()
+        buf = ctypes.create_string_buffer(bytes(uid), len(uid))
+        r = L.dli_comm_init(ctypes.byref(h), buf, int(world), int(rank))
+        if r != 0:
+            raise RuntimeError(f"ncclCommInitRank failed: {L.dli_comm_error_string(r).decode()}")
+        self._h = h.value
+        self.world, self.rank = world, rank
+
+    @staticmethod
+    def available() -> bool:
+        return bool(lib().dli_comm_available())
+
+    @staticmethod
+    def unique_id() -> bytes:
+        L = lib()
+        n = L.dli_comm_id_bytes()
+        buf = ctypes.create_string_buffer(n)
+        r = L.dli_comm_unique_id(buf)
+        if r != 0:
+            raise RuntimeError(f"ncclGetUniqueId failed: {L.dli_comm_error_string(r).decode()}")
+        return buf.raw
+
+    def exchange(self, sends, recvs, stream: int) -> None:
+        """``sends`` / ``recvs`` = [(device tensor, peer)]; enqueued on ``stream`` (an int
+        hipStream_t, e.g. ``torch.cuda.current_stream().cuda_stream``)."""
+        def pack(items):
+            n = len(items)
+            ptrs = (ctypes.c_void_p * max(n, 1))(*[t.data_ptr() for t, _ in items])
+            nbytes = (ctypes.c_longlong * max(n, 1))(*[t.numel() * t.element_size()
+                                                      for t, _ in items])
+            peers = (ctypes.c_int * max(n, 1))(*[int(p) for _, p in items])
+            return n, ptrs, nbytes, peers
+        ns, sp, sb, spe = pack(sends)
+        nr, rp, rb, rpe = pack(recvs)
+        r = lib().dli_comm_exchange(self._h, ctypes.c_void_p(stream), ns, sp, sb, spe, nr, rp,
+                                    rb, rpe)
+        if r != 0:
+            raise RuntimeError(f"RCCL exchange failed: {lib().dli_comm_error_string(r).decode()}")
+
+    def close(self) -> None:
+        if self._h is not None:
+            lib().dli_comm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
         except Exception:  # noqa: BLE001
             pass

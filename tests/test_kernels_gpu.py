@@ -609,3 +609,22 @@ def test_prefill_attention_paged_chunks(gpu, hq, hkv, hd, bs, chunks):
     q = qkv[:, : hq * hd].reshape(T, hq, hd)
     ref = R.prefill_attention_paged(q, kc, vc, cu, ctx, tables, scale).reshape(T, -1)
     close(out, ref, rtol=2e-2, atol=2e-2)
+
+
+def test_rccl_comm_module_self_exchange(gpu):
+    """csrc/runtime/comm.cpp on one GPU: a world-1 communicator, send-to-self + receive in one
+    group on the current stream (the pipeline data plane's DLI_PP_COMM=rccl path), several
+    buffers of different sizes in one group, then an invalid peer fails loudly."""
+    from distributed_llm_inferencing_amd.runtime import RcclComm
+    assert RcclComm.available()
+    comm = RcclComm(RcclComm.unique_id(), 1, 0)
+    st = torch.cuda.current_stream().cuda_stream
+    a = torch.randn(4096, 512, device=gpu).to(BF)
+    b = torch.arange(1000, device=gpu, dtype=torch.int32)
+    ra, rb = torch.empty_like(a), torch.empty_like(b)
+    comm.exchange([(a, 0), (b, 0)], [(ra, 0), (rb, 0)], st)
+    torch.cuda.synchronize()
+    assert torch.equal(ra, a) and torch.equal(rb, b)
+    with pytest.raises(RuntimeError):
+        comm.exchange([(a, 3)], [], st)
+    comm.close()
