@@ -444,6 +444,16 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(
   };
   auto wait_issued = [&](int u) {
     if (VAR & 4) { wait_deep(u); return; }
+    if (VAR & 512) {
+      // one counted wait per K-tile (the 8-phase template's schedule): at phase 3 of K-tile
+      // T every DMA of T+1 is retired; only T+2's slots 0-2 (issued in phases 1-3) stay in
+      // flight. Phases 0-2 do not wait at all.
+      if ((u & 3) == 3) {
+        if ((u >> 2) + 2 < nk) wait_vmcnt<6>();
+        else wait_vmcnt<0>();
+      }
+      return;
+    }
     const int lo = max(1, u - 2), hi = min(u, last_issue_seg);
     const int cnt = hi >= lo ? hi - lo + 1 : 0;    // wave-uniform
     if (cnt >= 3) wait_vmcnt<6>();
@@ -889,10 +899,13 @@ static int launch_cfg(const void* A, int lda, const void* W, int ldw, void* C, i
   DLI_RETURN_LAUNCH();
 }
 
-// measured on MI355X (scripts/bench_gemm8p.py, profiles/r1_gemm8p/): grouped tile order
-// (+6-14 % on prefill shapes) and a static priority for waves 4-7 (+1.5-5 %) over per-cluster
-// flips; the deep-prefetch plan (VAR 4) and glds-before-ds_read order measured slower / equal
-constexpr int GEMM8P_DEFAULT = 8 | 256;
+// measured on MI355X (scripts/bench_gemm8p.py, profiles/r1_gemm8p/, profiles/r2_s2/): grouped
+// tile order (+6-14 % on prefill shapes), a static priority for waves 4-7 (+1.5-5 %) over
+// per-cluster flips, and one counted vmcnt per K-tile instead of one per phase (VAR 512:
+// +6 % on prefill shapes, +6-11 % on the decode gate/up, down and LM head); the
+// deep-prefetch plan (VAR 4) and glds-before-ds_read order measured slower / equal
+constexpr int GEMM8P_DEFAULT = 8 | 256 | 512;
+constexpr int GEMM8P_PER_PHASE_WAITS = 8 | 256;     // round-1 schedule (tile 27, for A/Bs)
 
 template <int EPI, int VAR = 0>
 static int launch_8p(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M,
@@ -972,6 +985,8 @@ static int dispatch_tile(int tile_cfg, const void* A, int lda, const void* W, in
     DLI_CFG(18, 128, 96, 2) DLI_CFG(19, 128, 96, 3) DLI_CFG(20, 128, 64, 2) DLI_CFG(21, 128, 64, 3)
     // 256x256 8-phase ping-pong (gemm8p_kernel)
     case 22: return launch_8p<EPI, GEMM8P_DEFAULT>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
+    // 22 with the round-1 schedule (a counted vmcnt in every phase), for A/B runs
+    case 27: return launch_8p<EPI, GEMM8P_PER_PHASE_WAITS>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
     // 192-wide tiles: N = 6144 (fused QKV) = 32 column tiles, so M = 512 fills 256 CUs with
     // 4 x 32 x split 2 (128-row) or 2 x 32 x split 4 (256-row) workgroups of 8 waves
     DLI_CFG8(23, 128, 192, 3, 2, 4) DLI_CFG8(24, 128, 192, 2, 2, 4) DLI_CFG8(25, 256, 192, 2, 4, 2)

@@ -38,10 +38,12 @@ TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256), 4: (256, 128),
          # with split-K 2 / 4)
          23: (128, 192), 24: (128, 192), 25: (256, 192),
          # 256x224 ping-pong: N = 28672 (Llama-3 gate/up) at M = 512 = 256 tiles on 256 CUs
-         26: (256, 224)}
+         26: (256, 224),
+         # 22 with the round-1 schedule (a vmcnt wait every phase), for A/B runs only
+         27: (256, 256)}
 TILE_WAVES = {13: (2, 4), 14: (4, 2), 15: (2, 4), 16: (4, 2), 17: (2, 4),
               22: (2, 4), 23: (2, 4), 24: (2, 4), 25: (4, 2),
-              26: (4, 2)}                                         # default 2 x 2
+              26: (4, 2), 27: (2, 4)}                             # default 2 x 2
 
 
 def tile_ok(tile: int, epi: str) -> bool:
@@ -286,7 +288,9 @@ def candidate_plans(M: int, N: int, K: int, epi: str):
     # Default: 26 (256x224). It fills all 256 CUs on the gate/up GEMM and wins the isolated
     # autotune (98.8 vs ~106 us), but in the decode step it ran 97.9 vs 99.0 us per call and
     # the bench 0.3-0.7 % lower in three same-box A/B runs (profiles/r2_s2/README.md)
-    excl = {int(t) for t in os.environ.get("DLI_GEMM_EXCLUDE", "26").split(",") if t.strip()}
+    # 27 is tile 22 with the round-1 wait schedule (A/B reference only)
+    excl = {int(t) for t in os.environ.get("DLI_GEMM_EXCLUDE", "26,27").split(",")
+            if t.strip()}
     for tile, (bm, bn) in TILES.items():
         if not tile_ok(tile, epi) or tile in excl:
             continue
