@@ -903,7 +903,9 @@ static int launch_cfg(const void* A, int lda, const void* W, int ldw, void* C, i
 // tile order (+6-14 % on prefill shapes), a static priority for waves 4-7 (+1.5-5 %) over
 // per-cluster flips, and one counted vmcnt per K-tile instead of one per phase (VAR 512:
 // +6 % on prefill shapes, +6-11 % on the decode gate/up, down and LM head); the
-// deep-prefetch plan (VAR 4) and glds-before-ds_read order measured slower / equal
+// deep-prefetch plan (VAR 4) and glds-before-ds_read order measured slower / equal, and so
+// (within 1 %, profiles/r2_s2/gemm8p_wait/variants.log) did the template's B-before-A read
+// order, an lgkmcnt(0) after the barrier and per-cluster priority flips
 constexpr int GEMM8P_DEFAULT = 8 | 256 | 512;
 constexpr int GEMM8P_PER_PHASE_WAITS = 8 | 256;     // round-1 schedule (tile 27, for A/Bs)
 

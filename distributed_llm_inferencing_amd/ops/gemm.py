@@ -43,7 +43,7 @@ TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256), 4: (256, 128),
          27: (256, 256)}
 TILE_WAVES = {13: (2, 4), 14: (4, 2), 15: (2, 4), 16: (4, 2), 17: (2, 4),
               22: (2, 4), 23: (2, 4), 24: (2, 4), 25: (4, 2),
-              26: (4, 2), 27: (2, 4)}                             # default 2 x 2
+              26: (4, 2), 27: (2, 4)}
 
 
 def tile_ok(tile: int, epi: str) -> bool:
