@@ -107,7 +107,10 @@ extern "C" int dli_splitk_add_rmsnorm(void* out, void* residual, const float* ws
   }
 }
 
-// one lane: 8 dims of the first half of a head + the matching 8 of the second half
+// one lane: 8 dims of the first half of a head + the matching 8 of the second half. SPL > 0:
+// compile-time split count, every partial's loads issued before the first add (and the
+// position / cos-sin loads ahead of them); SPL == 0: runtime loop.
+template <int SPL>
 __global__ void __launch_bounds__(256) splitk_rope_cache_kernel(
     u16* __restrict__ qkv, const float* __restrict__ ws, int splits, int T, int N,
     const int* __restrict__ positions, const int* __restrict__ slot_mapping,
@@ -124,22 +127,38 @@ __global__ void __launch_bounds__(256) splitk_rope_cache_kernel(
   const int t = (int)(th / heads);
   const int half = hd >> 1, d0 = c * 8;
   const long col1 = (long)h * hd + d0, col2 = col1 + half;
+  const bool is_q = h < hq, is_k = !is_q && h < hq + hkv;
+  const bool rope = use_rope && (is_q || is_k);
+  const int pos = rope ? positions[t] : 0;
   float x1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, x2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int s = 0; s < splits; ++s) {
-    const float* base = ws + ((long)s * T + t) * N;
-    const float4* p1 = reinterpret_cast<const float4*>(base + col1);
-    const float4* p2 = reinterpret_cast<const float4*>(base + col2);
-    const float4 a = p1[0], b = p1[1], e = p2[0], f = p2[1];
-    x1[0] += a.x; x1[1] += a.y; x1[2] += a.z; x1[3] += a.w;
-    x1[4] += b.x; x1[5] += b.y; x1[6] += b.z; x1[7] += b.w;
-    x2[0] += e.x; x2[1] += e.y; x2[2] += e.z; x2[3] += e.w;
-    x2[4] += f.x; x2[5] += f.y; x2[6] += f.z; x2[7] += f.w;
+  auto add4 = [](float* x, const float4& a, const float4& b) {
+    x[0] += a.x; x[1] += a.y; x[2] += a.z; x[3] += a.w;
+    x[4] += b.x; x[5] += b.y; x[6] += b.z; x[7] += b.w;
+  };
+  if constexpr (SPL > 0) {
+    float4 pa[SPL], pb[SPL], pe[SPL], pf[SPL];
+#pragma unroll
+    for (int s = 0; s < SPL; ++s) {
+      const float* base = ws + ((long)s * T + t) * N;
+      const float4* p1 = reinterpret_cast<const float4*>(base + col1);
+      const float4* p2 = reinterpret_cast<const float4*>(base + col2);
+      pa[s] = p1[0]; pb[s] = p1[1]; pe[s] = p2[0]; pf[s] = p2[1];
+    }
+#pragma unroll
+    for (int s = 0; s < SPL; ++s) { add4(x1, pa[s], pb[s]); add4(x2, pe[s], pf[s]); }
+  } else {
+    for (int s = 0; s < splits; ++s) {
+      const float* base = ws + ((long)s * T + t) * N;
+      const float4* p1 = reinterpret_cast<const float4*>(base + col1);
+      const float4* p2 = reinterpret_cast<const float4*>(base + col2);
+      add4(x1, p1[0], p1[1]);
+      add4(x2, p2[0], p2[1]);
+    }
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) { x1[j] = bf2f(f2bf(x1[j])); x2[j] = bf2f(f2bf(x2[j])); }
-  const bool is_q = h < hq, is_k = !is_q && h < hq + hkv;
-  if (use_rope && (is_q || is_k)) {
-    const float* cs = cos_sin + (long)positions[t] * hd;
+  if (rope) {
+    const float* cs = cos_sin + (long)pos * hd;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float co = cs[d0 + j], si = cs[half + d0 + j];
@@ -170,8 +189,15 @@ extern "C" int dli_splitk_rope_cache(void* qkv, const float* ws, int splits, int
   if (T <= 0) return 0;
   if (hd % 16 || N != (hq + 2 * hkv) * hd) return (int)hipErrorInvalidValue;
   const long total = (long)T * (hq + 2 * hkv) * (hd / 16);
-  splitk_rope_cache_kernel<<<(int)((total + 255) / 256), 256, 0, st>>>(
-      (u16*)qkv, ws, splits, T, N, positions, slot_mapping, cos_sin, (u16*)k_cache,
-      (u16*)v_cache, hq, hkv, hd, block_size, use_rope);
+  const int blocks = (int)((total + 255) / 256);
+#define DLI_SRC(S) splitk_rope_cache_kernel<S><<<blocks, 256, 0, st>>>(                   \
+      (u16*)qkv, ws, splits, T, N, positions, slot_mapping, cos_sin, (u16*)k_cache,        \
+      (u16*)v_cache, hq, hkv, hd, block_size, use_rope)
+  switch (splits) {
+    case 2: DLI_SRC(2); break;
+    case 4: DLI_SRC(4); break;
+    default: DLI_SRC(0);
+  }
+#undef DLI_SRC
   DLI_RETURN_LAUNCH();
 }

@@ -154,19 +154,20 @@ def test_fused_splitk_add_rmsnorm(gpu, M, N, K):
     G.clear_plans()
 
 
-@pytest.mark.parametrize("hq,hkv,hd", [(32, 8, 128), (4, 2, 64)])
-def test_fused_splitk_rope_cache(gpu, hq, hkv, hd):
+@pytest.mark.parametrize("hq,hkv,hd,splits", [(32, 8, 128, 4), (32, 8, 128, 2),
+                                              (4, 2, 64, 2), (4, 2, 64, 3)])
+def test_fused_splitk_rope_cache(gpu, hq, hkv, hd, splits):
     lens = [5, 17, 1, 40]
     T = sum(lens)
     _, pos, slots, kc, vc, _ = _paged_setup(gpu, lens, hq, hkv, hd, 16)
-    K = 1024
+    K = 1536                                              # divisible into 2, 3 and 4 splits
     N = (hq + 2 * hkv) * hd
     x, w = rnd(T, K, dev=gpu), rnd(N, K, dev=gpu, scale=0.05)
     cs = R.rope_cos_sin(256, hd, 500000.0, device=gpu)
     ref = R.linear(x, w)
     kc1, vc1 = kc.clone(), vc.clone()
     R.rope_and_cache(ref, pos, slots, cs, kc1, vc1, hq, hkv, hd)
-    G.set_plan(T, N, K, "splitk", G.GemmPlan("dli", 0, 4))
+    G.set_plan(T, N, K, "splitk", G.GemmPlan("dli", 0, splits))
     out = ops.linear_rope_cache(x, w, pos, slots, cs, kc, vc, hq, hkv, hd)
     G.clear_plans()
     close(out, ref, rtol=2e-2, atol=2e-2)
