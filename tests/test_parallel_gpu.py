@@ -1,0 +1,115 @@
+"""Multi-process pipeline (PP) and expert-parallel (EP) exchanges with GPU tensors: 2 ranks
+share cuda:0 over gloo (RCCL refuses two ranks on one GPU). The data plane, the shared-memory
+control ring, the hipGraph stage runners and the EP buckets all run on device memory here,
+so the only thing the 8-GPU driver run adds is the RCCL transport itself.
+Each rank's output must equal the single-process engine's, token for token."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from distributed_llm_inferencing_amd.engine import SamplingParams
+from distributed_llm_inferencing_amd.engine.llm_engine import LLMEngine
+
+pytestmark = pytest.mark.gpu
+PROMPTS = [[5, 6, 7, 8], [9, 10, 11], [1, 2, 3, 4, 5, 6, 7], [100, 200], [7] * 9, [3, 4], [8] * 3]
+GREEDY = SamplingParams(max_length=24, do_sample=False, ignore_eos=True)
+SAMPLED = SamplingParams(max_length=24, seed=11, ignore_eos=True)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _env(rank, world, port, **extra):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), DLI_DIST_BACKEND="gloo",
+                      DLI_SAME_DEVICE="1", DLI_GEMM_AUTOTUNE="0", **extra)
+
+
+def _pp_worker(rank, world, port, q, vp):
+    _env(rank, world, port, DLI_PP_VOCAB_PARALLEL=vp)
+    import torch.distributed as dist
+    from distributed_llm_inferencing_amd.parallel.pipeline import DistributedPipelineEngine
+    eng = DistributedPipelineEngine("llama-tiny", "cuda", max_batch=8, max_model_len=64,
+                                    num_blocks=256)
+    if rank == 0:
+        res = [[o.all_ids for o in eng.generate(PROMPTS, sp)] for sp in (GREEDY, SAMPLED)]
+        res.append(eng.vocab_parallel)
+        eng.shutdown()
+        q.put(res)
+    else:
+        eng.serve()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run(target, world, *args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        n = world if target is _ep_worker else 1
+        res = [q.get(timeout=240) for _ in range(n)]
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    return res
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("vp", ["0", "1"])
+def test_pipeline_two_ranks_on_gpu_match_single_stage(gpu, vp):
+    """2-stage pipeline over gloo on GPU tensors (tail LM head, and the vocab-parallel head
+    with the HIP per-slice top-k) == the single-stage engine."""
+    (res,) = _run(_pp_worker, 2, vp)
+    os.environ["DLI_GEMM_AUTOTUNE"] = "0"
+    try:
+        eng = LLMEngine("llama-tiny", device="cuda", max_batch=8, max_model_len=64,
+                        num_blocks=64)
+        assert res[0] == [o.all_ids for o in eng.generate(PROMPTS, GREEDY)]
+        assert res[1] == [o.all_ids for o in eng.generate(PROMPTS, SAMPLED)]
+    finally:
+        del os.environ["DLI_GEMM_AUTOTUNE"]
+    assert res[2] == (vp == "1")
+
+
+def _ep_worker(rank, world, port, q):
+    _env(rank, world, port)
+    import torch.distributed as dist
+    from distributed_llm_inferencing_amd.parallel.expert import ExpertParallelEngine
+    eng = ExpertParallelEngine("mixtral-tiny", "cuda", max_batch=8, max_model_len=64,
+                               num_blocks=64)
+    mine = PROMPTS[rank::world]
+    out = [o.all_ids for o in eng.generate(mine, GREEDY)]
+    q.put((rank, mine, out, eng.moe.host_reads, eng.lockstep_syncs, eng.steps,
+           eng.engine.lookahead))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_expert_parallel_two_ranks_on_gpu_match_dense(gpu):
+    """DP attention + experts split over 2 ranks (ep_pack buckets, grouped GEMMs, moe_combine
+    on the GPU, exchanged over gloo) == one process holding all experts; no routing value
+    read on the host on any step, one lockstep sync per step."""
+    res = _run(_ep_worker, 2)
+    os.environ["DLI_GEMM_AUTOTUNE"] = "0"
+    try:
+        eng = LLMEngine("mixtral-tiny", device="cuda", max_batch=8, max_model_len=64,
+                        num_blocks=64)
+        for rank, mine, out, reads, syncs, steps, la in res:
+            assert out == [o.all_ids for o in eng.generate(mine, GREEDY)], rank
+            assert reads == 0 and syncs == steps + 1 and la
+    finally:
+        del os.environ["DLI_GEMM_AUTOTUNE"]
