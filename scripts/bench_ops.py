@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Per-op timings at the bench's decode shapes (Llama-3-8B, B=256, ctx 32..100)."""
+"""Per-op timings at the bench's decode shapes (Llama-3-8B, B=256, ctx 32..100), plus plain
+device-copy rates to calibrate the memory-bound kernels against."""
 import math
 import sys
 from pathlib import Path
@@ -62,6 +63,15 @@ def main():
     ms = ops.benchmark(lambda: ops.rope_and_cache(qkv, pos, slots, cs, kc, vc, hq, hkv, hd),
                        iters=50)
     res["rope_cache"] = (ms * 1e3, qkv.numel() * 2 * 2 / ms / 1e6)
+    # plain device copies for calibration (read + write bytes): a 1 GiB copy streams from HBM;
+    # the 33 / 67 MB ones are the split-4 / split-8 slab sizes and, run back to back, stay
+    # largely in the 256 MB Infinity Cache as the slabs a reduce reads right after its GEMM do
+    for mb in (33, 67, 1024):
+        n = mb * (1 << 20) // 4
+        src, dst = torch.randn(n, device=dev), torch.empty(n, device=dev)
+        ms = ops.benchmark(lambda: dst.copy_(src), iters=30)
+        res[f"copy_{mb}MB"] = (ms * 1e3, 2 * n * 4 / ms / 1e6)
+        del src, dst
     for kname, (us, gbs) in res.items():
         print(f"{kname:20s} {us:8.1f} us  {gbs:8.1f} GB/s")
 
