@@ -133,7 +133,7 @@ def test_gemm_epilogues(gpu, epi, M, N, K):
 
 
 @pytest.mark.parametrize("M,N,K", [(3, 512, 1024), (256, 4096, 4096), (77, 4096, 14336),
-                                   (64, 8192, 3072)])
+                                   (64, 8192, 3072), (5, 2000, 1024)])
 def test_fused_splitk_add_rmsnorm(gpu, M, N, K):
     torch.manual_seed(11)
     x, w = rnd(M, K, dev=gpu), rnd(N, K, dev=gpu, scale=0.02)
@@ -141,7 +141,7 @@ def test_fused_splitk_add_rmsnorm(gpu, M, N, K):
     y = R.linear(x, w)                                    # bf16-rounded GEMM output
     ref_out, ref_res = R.fused_add_rmsnorm(y, r0, nw, 1e-5)
     # 2/4/8: compile-time split variants up to N = 4096; 3 and N = 8192 (Llama-3-70B rows,
-    # 4 vectors per thread): the runtime-split loop
+    # 4 vectors per thread): the runtime-split loop; N = 2000: a partly masked last vector
     for splits in (2, 3, 4, 8) if K % (3 * 64) == 0 else (2, 4, 8):
         G.set_plan(M, N, K, "splitk", G.GemmPlan("dli", 0, splits))
         res = r0.clone()
