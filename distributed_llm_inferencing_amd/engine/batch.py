@@ -1,7 +1,8 @@
 """Per-step batch metadata shared by the scheduler, the model and the pipeline transport.
 
-A step is either all-prefill (packed prompts, causal varlen attention over the prompt) or
-all-decode (one token per running sequence, paged attention over the cache). The host
+A step is all-prefill (packed prompts, causal varlen attention over the prompt), all-decode
+(one token per running sequence, paged attention over the cache) or mixed (a prefill step
+whose first ``num_decode`` sequences are one-token decode rows of running sequences). The host
 builds the metadata once per step as ONE packed int32 buffer (``pack``/``unpack``) so it
 can travel with the activations between pipeline stages in a single message, and be
 copied into static device buffers for hipGraph replay.
@@ -41,6 +42,9 @@ class StepMeta:
     # chunked prefill (not on the wire): True for rows whose chunk completes the prompt; the
     # token sampled for any other row is discarded. None = every row samples.
     sample_mask: Optional[np.ndarray] = None
+    # mixed step (single stage, not on the wire): the first num_decode sequences are decode
+    # rows (one token each, attended by the decode kernel), the rest prefill chunks
+    num_decode: int = 0
     # columns of block_tables that hold blocks (the scheduler knows it; pack trims to it)
     table_used: Optional[int] = None
     # seq_ids as int64 numpy (set by the decode scheduler; saves list -> array conversions)
@@ -183,6 +187,12 @@ class DeviceBatch:
     top_k: Optional[torch.Tensor] = None
     top_p: Optional[torch.Tensor] = None
     seeds: Optional[torch.Tensor] = None
+    # mixed step: decode rows [0, num_decode) (their max context = max_context_decode) and the
+    # prefill part's own cu_seqlens / max_seqlen over rows [num_decode, T)
+    num_decode: int = 0
+    max_context_decode: int = 0
+    cu_seqlens_prefill: Optional[torch.Tensor] = None
+    max_seqlen_prefill: int = 0
 
     @property
     def is_prefill(self) -> bool:
@@ -222,6 +232,13 @@ def to_device(meta: StepMeta, device, pin: bool = True) -> DeviceBatch:
             db.block_tables = t(meta.block_tables, torch.int32)
             db.context_lens = t(meta.context_lens, torch.int32)
             db.max_context = int(np.max(meta.context_lens)) if S else 0
+        nd = int(meta.num_decode)
+        if nd:
+            ctx = np.asarray(meta.context_lens)
+            db.num_decode = nd
+            db.max_context_decode = int(ctx[:nd].max())
+            db.cu_seqlens_prefill = t(cu[nd:] - nd, torch.int32)
+            db.max_seqlen_prefill = int(lens[nd:].max()) if S > nd else 0
     else:
         db.block_tables = t(meta.block_tables, torch.int32)
         db.context_lens = t(meta.context_lens, torch.int32)

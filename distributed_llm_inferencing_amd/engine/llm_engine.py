@@ -34,6 +34,7 @@ class EngineStats:
     decode_steps: int = 0
     tokens_out: int = 0
     prompt_tokens: int = 0
+    mixed_steps: int = 0            # prefill steps that also carried decode rows
     busy_s: float = 0.0
     finished: int = 0
     latencies: List[float] = field(default_factory=list)
@@ -42,7 +43,8 @@ class EngineStats:
         lat = sorted(self.latencies[-4096:])
         pct = lambda q: lat[min(len(lat) - 1, int(q * len(lat)))] if lat else None  # noqa: E731
         return {"steps": self.steps, "prefill_steps": self.prefill_steps,
-                "decode_steps": self.decode_steps, "output_tokens": self.tokens_out,
+                "decode_steps": self.decode_steps, "mixed_steps": self.mixed_steps,
+                "output_tokens": self.tokens_out,
                 "prompt_tokens": self.prompt_tokens, "finished_requests": self.finished,
                 "busy_s": round(self.busy_s, 4),
                 "tokens_per_s": (self.tokens_out / self.busy_s) if self.busy_s > 0 else 0.0,
@@ -92,7 +94,7 @@ class LLMEngine:
                  params: Optional[Dict[str, torch.Tensor]] = None, tokenizer_path=None,
                  max_prefill_tokens: int = 16384, num_layers: Optional[int] = None,
                  lm: Optional[TransformerLM] = None, lookahead: Optional[bool] = None,
-                 max_kv_tokens: Optional[int] = None):
+                 max_kv_tokens: Optional[int] = None, mixed_steps: Optional[bool] = None):
         self.cfg = get_config(model, num_layers) if isinstance(model, str) else model
         self.device = torch.device(device)
         if self.device.type == "cuda" and self.device.index is None:
@@ -112,9 +114,14 @@ class LLMEngine:
                                          kv_fraction, cap_tokens=max_kv_tokens or 0)
         self.kv = KVCache(cfg, cfg.num_layers, num_blocks, block_size, self.device, dtype)
         self.bm = BlockManager(num_blocks, block_size)
+        # mixed prefill+decode steps (DLI_MIXED_STEPS=0 = off); engines in lockstep with peer
+        # ranks (EP / TP) pass False so every rank's step kinds stay aligned
+        self.mixed_steps = (os.environ.get("DLI_MIXED_STEPS", "1") == "1"
+                            if mixed_steps is None else bool(mixed_steps))
         self.scheduler = Scheduler(self.bm, max_seqs_per_mb=max_batch,
                                    max_prefill_tokens=max_prefill_tokens,
-                                   eos_token_id=cfg.eos_token_id, max_model_len=max_model_len)
+                                   eos_token_id=cfg.eos_token_id, max_model_len=max_model_len,
+                                   mixed_steps=self.mixed_steps)
         self.runner = StageRunner(self.model, self.kv, max_batch, self.scheduler.table_width,
                                   use_graphs=use_graphs)
         self.tokenizer = load_tokenizer(cfg, tokenizer_path)
@@ -179,7 +186,9 @@ class LLMEngine:
             self.stats.steps += 1
             if meta.kind == 1:
                 self.stats.prefill_steps += 1
-                self.stats.prompt_tokens += meta.num_tokens
+                self.stats.prompt_tokens += meta.num_tokens - meta.num_decode
+                if meta.num_decode:
+                    self.stats.mixed_steps += 1
             else:
                 self.stats.decode_steps += 1
         if self.lookahead:

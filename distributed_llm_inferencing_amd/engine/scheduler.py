@@ -157,7 +157,7 @@ class Scheduler:
                  table_width: Optional[int] = None, native_decode: bool = False,
                  admit_window_s: Optional[float] = None, admit_min_frac: float = 0.125,
                  refill_interval_s: Optional[float] = None,
-                 prefix_caching: Optional[bool] = None):
+                 prefix_caching: Optional[bool] = None, mixed_steps: bool = False):
         self.bm = block_manager
         self.bs = block_manager.block_size
         self.max_seqs = max_seqs_per_mb
@@ -204,6 +204,14 @@ class Scheduler:
         self.prefix_caching = (os.environ.get("DLI_PREFIX_CACHE", "1") == "1"
                                if prefix_caching is None else bool(prefix_caching))
         self.prefix_hit_tokens = 0
+        # mixed steps: a prefill step of a microbatch that is also decoding carries the running
+        # sequences' decode rows too (one token each, ahead of the prompt rows), so admitting
+        # prompts or prefilling a chunk no longer stalls the running sequences for a step and
+        # their rows ride on the prefill's (compute-bound) GEMMs instead of costing a separate
+        # weight-streaming decode step. Single-stage engines only (the pipeline wire format
+        # has no decode/prefill split).
+        self.mixed_steps = bool(mixed_steps)
+        self.num_mixed = 0
         self._next_id = 0
         self._step = 0
         self._deadlines = 0
@@ -330,10 +338,54 @@ class Scheduler:
         token is dropped by ``update`` (the sequence is no longer running)."""
         self._expire()
         self._step += 1
+        if self.mixed_steps and self.running[mb] and (self.waiting or self.prefilling[mb]):
+            # the decode rows are scheduled first, against the sequences running before this
+            # step's admissions (a prompt finishing its prefill here has no token to feed yet)
+            dec = self._decode(mb, inflight, allow_native=False)
+            pre = self._try_prefill(mb, mixed=True)
+            if pre is None or dec is None:
+                return dec if pre is None else pre
+            return self._merge(dec, pre)
         meta = self._try_prefill(mb)
         if meta is not None:
             return meta
         return self._decode(mb, inflight)
+
+    def _merge(self, dec: StepMeta, pre: StepMeta) -> StepMeta:
+        """One PREFILL-kind step: ``dec``'s decode rows (one token each) then ``pre``'s prompt
+        chunks. Its tokens are applied by the per-sequence update path (the microbatch's
+        decode state is dropped), rows of unfinished chunks masked out."""
+        mb = dec.microbatch
+        self._drop_state(mb)
+        nd, npf = dec.num_seqs, pre.num_seqs
+        width = max(dec.block_tables.shape[1], pre.block_tables.shape[1])
+
+        def pad(t):
+            return t if t.shape[1] == width else np.pad(t, ((0, 0), (0, width - t.shape[1])))
+        sid = np.concatenate([np.asarray(dec.seq_ids_arr if dec.seq_ids_arr is not None
+                                         else dec.seq_ids, np.int64), pre.seq_ids_arr])
+        cat = np.concatenate
+        meta = StepMeta(kind=PREFILL, seq_ids=sid.tolist(),
+                        input_ids=cat([np.asarray(dec.input_ids, np.int32), pre.input_ids]),
+                        positions=cat([np.asarray(dec.positions, np.int32), pre.positions]),
+                        slot_mapping=cat([np.asarray(dec.slot_mapping, np.int32),
+                                          pre.slot_mapping]),
+                        seq_lens=cat([np.ones(nd, np.int32), pre.seq_lens]),
+                        context_lens=cat([np.asarray(dec.context_lens, np.int32),
+                                          pre.context_lens]),
+                        block_tables=cat([pad(np.asarray(dec.block_tables, np.int32)),
+                                          pad(np.asarray(pre.block_tables, np.int32))]),
+                        temperature=cat([dec.temperature, pre.temperature]),
+                        top_k=cat([dec.top_k, pre.top_k]), top_p=cat([dec.top_p, pre.top_p]),
+                        seeds=cat([dec.seeds, pre.seeds]), microbatch=mb, step_id=pre.step_id,
+                        seq_ids_arr=sid)
+        meta.num_decode = nd
+        if dec.feed_src is not None:
+            meta.feed_src = cat([dec.feed_src, np.full(int(pre.num_tokens), -1, np.int32)])
+        if pre.sample_mask is not None:
+            meta.sample_mask = cat([np.ones(nd, np.bool_), pre.sample_mask])
+        self.num_mixed += 1
+        return meta
 
     def _least_loaded_ok(self, mb: int) -> bool:
         # balance admissions across microbatches: only admit into mb if it is among the least loaded
@@ -368,9 +420,11 @@ class Scheduler:
             self.prefix_hit_tokens -= seq.num_prefilled
             seq.num_prefilled = 0
 
-    def _try_prefill(self, mb: int) -> Optional[StepMeta]:
+    def _try_prefill(self, mb: int, mixed: bool = False) -> Optional[StepMeta]:
+        """``mixed``: the step also carries the microbatch's decode rows (chunks then run every
+        step, and the block tables are always built: the mixed step attends over the cache)."""
         partial = self.prefilling[mb]
-        if partial:
+        if partial and not mixed:
             # a chunk step every other step while the microbatch also decodes
             if self.running[mb] and not self._chunk_turn[mb]:
                 self._chunk_turn[mb] = True
@@ -478,7 +532,7 @@ class Scheduler:
         pos = (np.arange(T, dtype=np.int32) - np.repeat(cu - starts, lens)).astype(np.int32)
         slots = self.bm.slot_mapping(sid, starts, lens)
         ctx = starts + lens
-        if chunked:
+        if chunked or mixed:
             width = -(-max(s.total_len for s in picked) // self.bs)   # blocks held per seq
             tables = self.bm.fill_tables(sid.tolist(), width)
         else:
@@ -559,10 +613,11 @@ class Scheduler:
         meta.core = (st, st.core.steps, S)
         return meta
 
-    def _decode(self, mb: int, inflight: Optional[StepMeta] = None) -> Optional[StepMeta]:
+    def _decode(self, mb: int, inflight: Optional[StepMeta] = None,
+                allow_native: bool = True) -> Optional[StepMeta]:
         if not self.running[mb]:
             return None
-        if self._native_ok(mb, inflight):
+        if allow_native and self._native_ok(mb, inflight):
             return self._decode_native(mb)
         while True:
             st = self._mb_state(mb)

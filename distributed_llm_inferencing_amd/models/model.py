@@ -171,6 +171,19 @@ class TransformerLM:
     def _attend(self, qkv, b: DeviceBatch, kc, vc) -> torch.Tensor:
         cfg = self.cfg
         if b.is_prefill:
+            if b.num_decode:                     # mixed step: decode rows, then prefill chunks
+                nd = b.num_decode
+                out = torch.empty(qkv.shape[0], cfg.num_heads * cfg.head_dim,
+                                  dtype=qkv.dtype, device=qkv.device)
+                ops.decode_attention(qkv[:nd], kc, vc, b.block_tables[:nd],
+                                     b.context_lens[:nd], b.max_context_decode, cfg.num_heads,
+                                     cfg.num_kv_heads, cfg.head_dim, self.scale, out=out[:nd])
+                ops.prefill_attention_paged(qkv[nd:], b.cu_seqlens_prefill,
+                                            b.max_seqlen_prefill, b.context_lens[nd:],
+                                            b.block_tables[nd:], kc, vc, cfg.num_heads,
+                                            cfg.num_kv_heads, cfg.head_dim, self.scale,
+                                            out=out[nd:])
+                return out
             if b.block_tables is not None:       # chunked prefill over the paged cache
                 return ops.prefill_attention_paged(qkv, b.cu_seqlens, b.max_seqlen,
                                                    b.context_lens, b.block_tables, kc, vc,
@@ -185,16 +198,7 @@ class TransformerLM:
         cfg = self.cfg
         ops.rope_and_cache(qkv, b.positions, b.slot_mapping, self.cos_sin, kc, vc, cfg.num_heads,
                            cfg.num_kv_heads, cfg.head_dim, use_rope=cfg.arch != "gpt2")
-        if b.is_prefill:
-            if b.block_tables is not None:       # chunked prefill over the paged cache
-                return ops.prefill_attention_paged(qkv, b.cu_seqlens, b.max_seqlen,
-                                                   b.context_lens, b.block_tables, kc, vc,
-                                                   cfg.num_heads, cfg.num_kv_heads,
-                                                   cfg.head_dim, self.scale)
-            return ops.prefill_attention(qkv, b.cu_seqlens, b.max_seqlen, cfg.num_heads,
-                                         cfg.num_kv_heads, cfg.head_dim, self.scale)
-        return ops.decode_attention(qkv, kc, vc, b.block_tables, b.context_lens, b.max_context,
-                                    cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, self.scale)
+        return self._attend(qkv, b, kc, vc)
 
     def _moe_local(self, h: torch.Tensor, lp: dict, layer: int) -> torch.Tensor:
         router_logits = ops.linear(h, lp["router"])

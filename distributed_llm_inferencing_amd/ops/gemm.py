@@ -100,7 +100,16 @@ def _heuristic(M: int, N: int, K: int, epi: str) -> GemmPlan:
         if (os.environ.get("DLI_GEMM_PREFILL_BLAS", "0") == "1" and epi in ("none", "splitk")
                 and os.environ.get("DLI_GEMM_NO_BLAS", "0") != "1"):
             return GemmPlan("hipblaslt", 2, 1)
-        return GemmPlan("dli", 22, 1)
+        # mid-sized steps (serving refills / mixed steps of ~1-2k rows): 256x256 tiles leave
+        # most CUs idle on the N = 4096 / 6144 projections (M = 1200: 80 / 120 tiles), so
+        # split K while the grid stays within one wave of the chip
+        tiles = -(-M // 256) * -(-N // 256)
+        splits = 1
+        if epi in ("none", "splitk"):
+            while (tiles * splits * 2 <= NUM_CUS and K % (64 * splits * 2) == 0
+                   and K // (splits * 2) >= 1024 and splits < 4):
+                splits *= 2
+        return GemmPlan("dli", 22, splits)
     if M <= 128:
         tile = 0 if N <= 8192 else 1
     elif M <= 256:

@@ -171,7 +171,8 @@ class ExpertParallelEngine:
         self.engine = LLMEngine(cfg, device=str(dev), dtype=dtype, max_batch=max_batch,
                                 max_model_len=max_model_len, num_blocks=num_blocks,
                                 use_graphs=False, lm=lm,
-                                max_prefill_tokens=max_prefill_tokens, lookahead=lookahead)
+                                max_prefill_tokens=max_prefill_tokens, lookahead=lookahead,
+                                mixed_steps=False)
         self.device = dev
         self.steps = 0
         self.lockstep_syncs = 0

@@ -96,7 +96,8 @@ class TensorParallelEngine:
         self.engine = LLMEngine(local, device=str(dev), dtype=dtype, max_batch=max_batch,
                                 max_model_len=max_model_len, num_blocks=num_blocks,
                                 use_graphs=False, lm=lm, max_prefill_tokens=max_prefill_tokens,
-                                lookahead=False)   # lockstep all-reduces on every rank
+                                lookahead=False,   # lockstep all-reduces on every rank
+                                mixed_steps=False)
         self.device = dev
 
     def generate(self, prompts, params=None):

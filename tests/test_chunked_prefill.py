@@ -69,16 +69,18 @@ def test_chunked_prefill_token_identical(chunk):
     assert not any(eng.scheduler.prefilling)
 
 
-def test_chunks_interleave_with_decode():
-    """A long prompt submitted while short requests decode: its chunks alternate with decode
-    steps (the running sequences keep producing tokens) and every output is unchanged."""
+@pytest.mark.parametrize("mixed", [False, True])
+def test_chunks_interleave_with_decode(mixed):
+    """A long prompt submitted while short requests decode: the running sequences keep
+    producing tokens and every output is unchanged. Without mixed steps the chunks alternate
+    with decode steps; with them every chunk step also carries the decode rows."""
     sp = SamplingParams(max_length=60, do_sample=False, ignore_eos=True)
     long_p = list(range(10, 10 + 150))
     ref = _engine(4096)
     want_short = [o.all_ids for o in ref.generate(PROMPTS[1:2] + PROMPTS[3:4], sp)]
     want_long = ref.generate([long_p], SamplingParams(max_length=170, do_sample=False,
                                                        ignore_eos=True))[0].all_ids
-    eng = _engine(16)
+    eng = _engine(16, mixed_steps=mixed)
     rids = [eng.add_request(p, sp) for p in (PROMPTS[1], PROMPTS[3])]
     for _ in range(3):
         eng.step()
@@ -89,16 +91,23 @@ def test_chunks_interleave_with_decode():
     while eng.has_work():
         meta = eng.plan_step()
         if meta is not None:
-            kinds.append((meta.kind, bool(meta.sample_mask is not None)))
+            kinds.append((meta.kind, bool(meta.sample_mask is not None), meta.num_decode))
         for o in eng.finish_step(meta):
             outs[o.request_id] = o
     assert [outs[r].all_ids for r in rids] == want_short
     assert outs[rid_long].all_ids == want_long
-    chunk_steps = [i for i, (k, partial) in enumerate(kinds) if k == 1 and partial]
+    chunk_steps = [i for i, (k, partial, _) in enumerate(kinds) if k == 1 and partial]
     assert len(chunk_steps) >= 8                       # 150 tokens in 16-token chunks
-    # while the short requests still decode, no two chunk steps are adjacent
-    gaps = np.diff(chunk_steps[:3])
-    assert (gaps >= 2).all(), kinds[:20]
+    if mixed:
+        # back-to-back chunk steps, each with both short requests' decode rows
+        assert np.diff(chunk_steps[:3]).tolist() == [1, 1], kinds[:20]
+        assert all(kinds[i][2] == 2 for i in chunk_steps[:3]), kinds[:20]
+        assert eng.stats.mixed_steps >= 3
+    else:
+        # while the short requests still decode, no two chunk steps are adjacent
+        gaps = np.diff(chunk_steps[:3])
+        assert (gaps >= 2).all(), kinds[:20]
+        assert eng.stats.mixed_steps == 0
 
 
 def test_chunked_prefill_with_preemption():

@@ -115,3 +115,28 @@ def test_real_shape_engine_decode(gpu, name, monkeypatch):
         del eng
         torch.cuda.empty_cache()
     assert outs[0] == outs[1]
+
+
+def test_mixed_steps_token_identical_on_gpu(gpu, monkeypatch):
+    """Prompts arriving while others decode: the mixed prefill+decode steps (decode rows on
+    the decode kernel, prompt rows on the paged prefill kernel, one GEMM pass) produce the
+    tokens of the engine without mixed steps; graphs and lookahead on."""
+    monkeypatch.setenv("DLI_GEMM_AUTOTUNE", "0")
+    waves = [[IDS[:5], IDS[:9], IDS[3:14]], [IDS[:2], IDS[1:4]], [IDS[2:11]]]
+    sp = SamplingParams(max_length=40, seed=7, ignore_eos=True)
+    res = []
+    for mixed in (False, True):
+        eng = LLMEngine("llama-tiny", device="cuda", max_batch=8, max_model_len=128,
+                        num_blocks=64, seed=2, mixed_steps=mixed)
+        outs, rids = {}, []
+        for w, wave in enumerate(waves):
+            rids += [eng.add_request(p, sp) for p in wave]
+            for _ in range(2):
+                for o in eng.step():
+                    outs[o.request_id] = o
+        while eng.has_work():
+            for o in eng.step():
+                outs[o.request_id] = o
+        res.append([outs[r].all_ids for r in rids])
+        assert (eng.stats.mixed_steps > 0) == mixed
+    assert res[0] == res[1]

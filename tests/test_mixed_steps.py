@@ -1,0 +1,74 @@
+"""Mixed prefill+decode steps: when prompts arrive while a microbatch is decoding, the
+prefill step also carries every running sequence's decode row (decode rows first, attended by
+the decode kernel; prompt rows by the paged prefill kernel). Outputs must be token-identical
+to the engine without mixed steps, with lookahead on and off, with stop tokens that end a
+sequence inside an in-flight step, and with chunked prompts."""
+import pytest
+import torch
+
+from distributed_llm_inferencing_amd.engine import SamplingParams
+from distributed_llm_inferencing_amd.engine.llm_engine import LLMEngine
+
+WAVES = [
+    [[5, 6, 7, 8], [9, 10, 11], list(range(30, 52))],
+    [[100, 200], [7] * 9],
+    [list(range(60, 100)), [3, 4]],
+]
+
+
+def _engine(mixed, lookahead, chunk=4096):
+    return LLMEngine("llama-tiny", device="cpu", dtype=torch.float32, max_batch=8,
+                     max_model_len=128, num_blocks=128, max_prefill_tokens=chunk,
+                     mixed_steps=mixed, lookahead=lookahead)
+
+
+def _run(eng, params):
+    """Submit WAVES[0], step twice, submit WAVES[1], step once, submit WAVES[2], drain."""
+    outs, rids, k = {}, [], 0
+    for w, wave in enumerate(WAVES):
+        for p in wave:
+            rids.append(eng.add_request(p, params[k]))
+            k += 1
+        for _ in range((2, 1, 0)[w]):
+            for o in eng.step():
+                outs[o.request_id] = o
+    while eng.has_work():
+        for o in eng.step():
+            outs[o.request_id] = o
+    return [(outs[r].all_ids, outs[r].finish_reason) for r in rids]
+
+
+@pytest.mark.parametrize("lookahead", [True, False])
+@pytest.mark.parametrize("chunk", [4096, 16])
+def test_mixed_steps_token_identical(lookahead, chunk):
+    n = sum(len(w) for w in WAVES)
+    greedy = [SamplingParams(max_length=40 + 3 * i, do_sample=False, ignore_eos=True)
+              for i in range(n)]
+    sampled = [SamplingParams(max_length=36, seed=100 + i, ignore_eos=True) for i in range(n)]
+    for params in (greedy, sampled):
+        want = _run(_engine(False, lookahead, chunk), params)
+        eng = _engine(True, lookahead, chunk)
+        got = _run(eng, params)
+        assert got == want
+        assert eng.stats.mixed_steps > 0
+        assert eng.stats.tokens_out == sum(len(a) - len(p) for (a, _), p in
+                                           zip(got, [p for w in WAVES for p in w]))
+
+
+def test_mixed_steps_with_stop_tokens():
+    """A sequence that stops on a stop token while its next row is already scheduled (the
+    in-flight step under lookahead) loses that row's token in both engines alike."""
+    n = sum(len(w) for w in WAVES)
+    base = [SamplingParams(max_length=44, do_sample=False, ignore_eos=True) for _ in range(n)]
+    free = _run(_engine(False, True), base)
+    params = []
+    for (ids, _), p in zip(free, [p for w in WAVES for p in w]):
+        gen = ids[len(p):]
+        stop = [gen[len(gen) // 3]] if len(gen) > 3 else []
+        params.append(SamplingParams(max_length=44, do_sample=False, ignore_eos=True,
+                                     stop_token_ids=stop))
+    want = _run(_engine(False, True), params)
+    assert any(r == "stop" for _, r in want)
+    eng = _engine(True, True)
+    assert _run(eng, params) == want
+    assert eng.stats.mixed_steps > 0

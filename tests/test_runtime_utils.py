@@ -251,6 +251,12 @@ def test_prefill_gemm_plan_is_own_kernel(monkeypatch):
     for epi in ("none", "silu_mul", "splitk", "f32"):
         p = G.plan(16384, 6144, 4096, epi)
         assert p.backend == "dli" and p.tile == 22 and p.splits == 1, (epi, p)
+    # mid-sized steps split K until the grid fills the chip (no split for fused epilogues)
+    assert G.plan(1200, 6144, 4096, "splitk") == G.GemmPlan("dli", 22, 2)      # 120 tiles
+    assert G.plan(1200, 4096, 4096, "none") == G.GemmPlan("dli", 22, 2)        # 80 tiles
+    assert G.plan(1100, 4096, 14336, "splitk") == G.GemmPlan("dli", 22, 2)
+    assert G.plan(1024, 4096, 4096, "splitk") == G.GemmPlan("dli", 22, 4)      # 64 tiles
+    assert G.plan(1200, 28672, 4096, "silu_mul").splits == 1
     assert all(p.backend == "dli" for p in G.candidate_plans(512, 4096, 4096, "none"))
     G.clear_plans()
     monkeypatch.setenv("DLI_GEMM_PREFILL_BLAS", "1")
