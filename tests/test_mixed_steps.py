@@ -16,8 +16,8 @@ WAVES = [
 ]
 
 
-def _engine(mixed, lookahead, chunk=4096):
-    return LLMEngine("llama-tiny", device="cpu", dtype=torch.float32, max_batch=8,
+def _engine(mixed, lookahead, chunk=4096, model="llama-tiny"):
+    return LLMEngine(model, device="cpu", dtype=torch.float32, max_batch=8,
                      max_model_len=128, num_blocks=128, max_prefill_tokens=chunk,
                      mixed_steps=mixed, lookahead=lookahead)
 
@@ -70,5 +70,17 @@ def test_mixed_steps_with_stop_tokens():
     want = _run(_engine(False, True), params)
     assert any(r == "stop" for _, r in want)
     eng = _engine(True, True)
+    assert _run(eng, params) == want
+    assert eng.stats.mixed_steps > 0
+
+
+@pytest.mark.parametrize("model", ["gpt2-tiny", "mixtral-tiny"])
+def test_mixed_steps_other_families(model):
+    """GPT-2 (learned positions, LayerNorm, no RoPE) and Mixtral (routed experts over the
+    mixed rows) through mixed steps."""
+    n = sum(len(w) for w in WAVES)
+    params = [SamplingParams(max_length=36, seed=300 + i, ignore_eos=True) for i in range(n)]
+    want = _run(_engine(False, True, model=model), params)
+    eng = _engine(True, True, model=model)
     assert _run(eng, params) == want
     assert eng.stats.mixed_steps > 0
