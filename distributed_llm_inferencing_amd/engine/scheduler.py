@@ -109,11 +109,12 @@ class _MBCore:
     """The same mirror in C++ (``runtime.DecodeCore``): the decode fast path of the pipeline
     head, where one tick's scheduling + token application must cost tens of microseconds.
     Used when no lookahead is involved and no row has stop tokens."""
-    __slots__ = ("seqs", "core", "first_rows")
+    __slots__ = ("seqs", "core", "first_rows", "vp")
 
     def __init__(self, seqs: List[Sequence], eos: Optional[int], max_model_len: int):
         from ..runtime import DecodeCore
         self.seqs = list(seqs)
+        self.vp = None           # (rows, flag): pipeline head's vocab-parallel check, cached
         n = len(seqs)
         out_cnt = np.fromiter((len(s.output_ids) for s in seqs), np.int32, n)
         budget = np.fromiter((s.params.budget(s.prompt_len) for s in seqs), np.int32, n)

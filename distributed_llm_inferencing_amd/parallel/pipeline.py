@@ -175,9 +175,17 @@ def vp_ok(meta: Optional[StepMeta]) -> bool:
     candidates per rank (greedy included); top_k <= 0 (full-vocab sampling) falls back."""
     if meta is None or meta.top_k is None or meta.num_seqs == 0:
         return False
+    core = getattr(meta, "core", None)      # native decode step: rows' params are fixed and
+    if core is not None:                    # rows only ever leave the core (compaction)
+        st, _, S = core
+        if st.vp is not None and st.vp[0] == S:
+            return st.vp[1]
     tk = np.asarray(meta.top_k)
     greedy = np.asarray(meta.temperature) <= 0
-    return bool(np.all(greedy | ((tk >= 1) & (tk <= CAND))))
+    ok = bool(np.all(greedy | ((tk >= 1) & (tk <= CAND))))
+    if core is not None:
+        st.vp = (S, ok)
+    return ok
 
 
 H_VP = 13          # ctrl header word: 1 = vocab-parallel head for this step
@@ -259,6 +267,22 @@ class PipelineHead:
         if self.vp and self.N > 1:
             self.hf_rx = channel.recv_buffer((B, D))
             self.cand_rx = channel.recv_buffer((self.N - 1, B, 2 * CAND), torch.int32)
+        # row-count -> views of the receive buffers (a decode microbatch keeps its row count
+        # for many ticks; slicing 2N tensors per tick is ~4 us each on the head's host)
+        self._hf_views: Dict[int, torch.Tensor] = {}
+        self._cand_views: Dict[int, List[torch.Tensor]] = {}
+
+    def _hf_view(self, S: int) -> torch.Tensor:
+        v = self._hf_views.get(S)
+        if v is None:
+            v = self._hf_views[S] = self.hf_rx[:S]
+        return v
+
+    def _cand_view(self, S: int) -> List[torch.Tensor]:
+        v = self._cand_views.get(S)
+        if v is None:
+            v = self._cand_views[S] = [self.cand_rx[q, :S] for q in range(self.N - 1)]
+        return v
 
     def _account(self, meta: StepMeta):
         self.stats.steps += 1
@@ -292,9 +316,11 @@ class PipelineHead:
         toks = self.tokens
         ph = self.phase_s
         pc = time.perf_counter
+        tt = time.thread_time       # this thread's CPU time: host cost without preemption
         while True:
             t0 = pc()
-            wait_s = 0.0
+            c0 = tt()
+            wait_s = wait_c = 0.0
             s = k - M
             if s in started:
                 m, _ = started.pop(s)
@@ -339,25 +365,27 @@ class PipelineHead:
             recvs = []
             if ret is not None:
                 S = ret[0].num_seqs
-                recvs.append((self.hf_rx[:S], N - 1, 2) if ret[1] else
+                recvs.append((self._hf_view(S), N - 1, 2) if ret[1] else
                              (toks.slot(k - N, S), N - 1, 2))
             if smp is not None and smp[1]:
-                S2 = smp[0].num_seqs
-                recvs += [(self.cand_rx[q - 1, :S2], q, 3) for q in range(1, N)]
-            tw = pc()
+                cv = self._cand_view(smp[0].num_seqs)
+                recvs += [(cv[q - 1], q, 3) for q in range(1, N)]
+            tw, cw = pc(), tt()
             ch.exchange([(prev_out, 1, 1)] if prev_out is not None else [], recvs)
             ch.reap_ctrl()
             t5 = pc()
             wait_s += t5 - tw
+            wait_c += tt() - cw
             cand_now = None
             if ret is not None:
                 if ret[1]:
-                    cand_now = st.candidates(ch.to_compute(self.hf_rx[:ret[0].num_seqs]))
+                    cand_now = st.candidates(ch.to_compute(self._hf_view(ret[0].num_seqs)))
                 else:
                     toks.landed(k - N, ret[0].num_seqs)
             if smp is not None and smp[1]:
                 S2 = smp[0].num_seqs
-                bufs = [ch.to_compute(self.cand_rx[q, :S2]) for q in range(N - 1)]
+                cv = self._cand_view(S2)
+                bufs = cv if ch.data_device == ch.device else [ch.to_compute(b) for b in cv]
                 tok = st.sample_candidates(smp[0], [my_cand] + bufs)
                 toks.landed(k - 1 - N, S2, src=tok)
             my_cand = cand_now
@@ -376,7 +404,8 @@ class PipelineHead:
             kk[1] += 1
             if self.tick_log is not None:
                 self.tick_log.append((meta.kind if meta is not None else 0, hs,
-                                      t2 - t1, t3 - t2, t4 - t3, t6 - t5, now - t6))
+                                      t2 - t1, t3 - t2, t4 - t3, t6 - t5, now - t6,
+                                      tt() - c0 - wait_c))
             self.host_s += hs
             self.ticks += 1
             self.stats.busy_s += now - t0

@@ -30,8 +30,12 @@ def _free_port():
 
 
 def _patch_null_compute():
-    """Stage compute / candidates / sampling replaced by views of preallocated buffers."""
+    """Stage compute / candidates / sampling replaced by views of preallocated buffers.
+    Candidates are 8 per rank (the requests use top_k 8): the head's host work does not
+    depend on the width, but 64-wide candidates from 7 ranks put ~2 MB of loopback TCP
+    per tick on this 8-core container (RCCL over xGMI on the GPU node)."""
     from distributed_llm_inferencing_amd.parallel import pipeline as P
+    P.CAND = 8
 
     def compute(self, meta, data):
         if meta.num_seqs == 0:
@@ -97,7 +101,7 @@ def _worker(rank, world, port, q, batch, n_req):
     eng = P.DistributedPipelineEngine("llama-null8", "cpu", max_batch=batch, max_model_len=64,
                                       num_blocks=24576, dtype=torch.float32,
                                       max_prefill_tokens=batch * 8)
-    sp = SamplingParams(max_length=40, temperature=0.8, top_k=50, top_p=0.95, ignore_eos=True)
+    sp = SamplingParams(max_length=40, temperature=0.8, top_k=8, top_p=0.95, ignore_eos=True)
     rng = np.random.default_rng(0)
     prompts = [rng.integers(3, 1000, size=8).tolist() for _ in range(n_req)]
     if rank == 0:
@@ -107,6 +111,10 @@ def _worker(rank, world, port, q, batch, n_req):
         eng.head.tick_log = []
         outs = eng.generate(prompts, sp)                # timed session
         dec = sorted(t[1] for t in eng.head.tick_log if t[0] == 2)
+        dec_cpu = sorted(t[7] for t in eng.head.tick_log if t[0] == 2)
+        dec_ph = np.array([t[2:7] for t in eng.head.tick_log if t[0] == 2])
+        ph_p50 = dict(zip(("finish", "schedule", "ctrl", "head_ops", "compute"),
+                          np.round(1e3 * np.median(dec_ph, axis=0), 4).tolist()))
         ticks, host_s = eng.head.ticks, eng.head.host_s
         dec_s, dec_n = eng.head.host_by_kind[2]
         phases = dict(eng.head.phase_s)
@@ -131,6 +139,9 @@ def _worker(rank, world, port, q, batch, n_req):
         res = dict(rank=0, ticks=ticks, host_ms=1e3 * host_s / max(1, ticks),
                    decode_ticks=dec_n, decode_host_ms=1e3 * dec_s / max(1, dec_n),
                    decode_host_ms_p50=1e3 * dec[len(dec) // 2],
+                   decode_cpu_ms_p50=1e3 * dec_cpu[len(dec_cpu) // 2],
+                   decode_cpu_ms=1e3 * sum(dec_cpu) / max(1, len(dec_cpu)),
+                   decode_phase_ms_p50=ph_p50,
                    allocs=counter.counts, n_out=len(outs),
                    toks=sum(len(o.output_ids) for o in outs), ctrl=eng.channel.ctrl_kind,
                    vp=eng.vocab_parallel, M=eng.microbatches,
