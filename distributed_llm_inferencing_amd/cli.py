@@ -18,6 +18,10 @@ launcher for an 8-GPU MI355X box.
                     §2.5 "DP replicas"); every replica head registers as a node and the
                     master's dispatcher load-balances across them (least in flight)
     shard-model     --model_name M --num_shards N [--output_dir D] [--policy even|hbm|balanced]
+    join-pipeline   --model M --shard-dir D --nodes URL0,URL1,... [--rendezvous tcp://H:P]
+                    assign shard i of an export to node i over the worker API (/load_shard
+                    with a "pipeline" spec): the N worker processes form one RCCL ring and
+                    node 0 serves the model
     loadgen         --master URL --model M [--requests N] [--concurrency C | --rate R]
                     end-to-end load through the master API: tokens/s, p50/p99 latency
     bench           ... (bench.py)
@@ -169,6 +173,44 @@ def _serve_cluster(argv):
             p.terminate()
 
 
+def _join_pipeline(argv):
+    import argparse
+    import json
+
+    import requests
+    ap = argparse.ArgumentParser("dli join-pipeline")
+    ap.add_argument("--model", required=True)
+    ap.add_argument("--shard-dir", required=True, help="<output_dir>/<model> of shard-model")
+    ap.add_argument("--nodes", required=True, help="comma-separated worker URLs, stage order")
+    ap.add_argument("--rendezvous", default="tcp://127.0.0.1:29650")
+    ap.add_argument("--auth-key", default=os.environ.get("AUTH_KEY", ""))
+    ap.add_argument("--timeout", type=float, default=600.0)
+    a = ap.parse_args(argv)
+    nodes = [u.rstrip("/") for u in a.nodes.split(",") if u]
+    hdr = {"Authorization": f"Bearer {a.auth_key}"} if a.auth_key else {}
+    spec = {"init_method": a.rendezvous, "world_size": len(nodes)}
+    for i, u in enumerate(nodes):
+        r = requests.post(f"{u}/load_shard", headers=hdr, timeout=30, json={
+            "model_name": a.model, "shard_id": i, "pipeline": spec,
+            "shard_path": os.path.join(a.shard_dir, f"shard_{i}")})
+        print(f"{u}: {r.status_code} {r.json().get('message')}")
+        if r.status_code != 200:
+            return 1
+    t0 = time.time()
+    while time.time() - t0 < a.timeout:
+        states = [requests.get(f"{u}/health", headers=hdr, timeout=10).json()
+                  .get("pipeline", {}).get("state") for u in nodes]
+        if all(s == "serving" for s in states):
+            print(json.dumps({"model": a.model, "stages": len(nodes), "head": nodes[0]}))
+            return 0
+        if "failed" in states:
+            print(f"join failed: {states}")
+            return 1
+        time.sleep(1)
+    print(f"join timed out: {states}")
+    return 1
+
+
 def main(argv=None):
     argv = list(sys.argv[1:] if argv is None else argv)
     if not argv or argv[0] in ("-h", "--help"):
@@ -190,6 +232,8 @@ def main(argv=None):
     if cmd == "shard-model":
         from .shard.writer import main as m
         return m(rest)
+    if cmd == "join-pipeline":
+        return _join_pipeline(rest)
     if cmd == "loadgen":
         from .loadgen import main as m
         return m(rest)

@@ -276,8 +276,13 @@ class PipeChannel:
             self.ring = None
 
 
-def init_distributed(backend: Optional[str] = None, device: Optional[torch.device] = None):
-    """Initialise torch.distributed from torchrun env vars (127.0.0.1 rendezvous).
+def init_distributed(backend: Optional[str] = None, device: Optional[torch.device] = None,
+                     init_method: Optional[str] = None, world_size: Optional[int] = None,
+                     rank: Optional[int] = None):
+    """Initialise torch.distributed from torchrun env vars (127.0.0.1 rendezvous), or from an
+    explicit ``init_method`` (``tcp://host:port``) + ``world_size`` + ``rank``: a worker that
+    joins a pipeline when the master assigns it a shard (``/load_shard`` with a "pipeline"
+    spec, ``worker/server.py``).
 
     Failure detection: data-plane operations get a bounded timeout
     (``DLI_PP_TIMEOUT_S``, default 600 s), so a stage that dies mid-session turns a blocked
@@ -297,5 +302,7 @@ def init_distributed(backend: Optional[str] = None, device: Optional[torch.devic
     kw = {"timeout": timedelta(seconds=float(os.environ.get("DLI_PP_TIMEOUT_S", "600")))}
     if backend == "nccl" and device is not None:
         kw["device_id"] = device
+    if init_method is not None:
+        kw.update(init_method=init_method, world_size=int(world_size), rank=int(rank))
     dist.init_process_group(backend=backend, **kw)
     return dist.get_rank(), dist.get_world_size()

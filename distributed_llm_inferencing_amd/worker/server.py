@@ -83,6 +83,8 @@ class WorkerState:
         self.shards: Dict[str, Dict[int, dict]] = {}     # model -> shard_id -> record
         self.shard_pipes: Dict[tuple, object] = {}     # (model, shard ids) -> EngineService
         self.weights_source: Dict[str, str] = {}
+        self.pipeline: Optional[dict] = None            # ring this worker joined via /load_shard
+        self._pipe_engine = None
         self.lock = threading.RLock()
         os.makedirs(settings.model_cache_dir, exist_ok=True)
 
@@ -116,6 +118,9 @@ class WorkerState:
 
     def unload_model(self, name: str):
         with self.lock:
+            if (self.pipeline is not None and self._pipe_engine is not None
+                    and name == getattr(self, "pipeline_model", None)):
+                self._leave_pipeline()
             svc = self.services.pop(name, None)
             if svc is not None:
                 svc.close()
@@ -146,6 +151,99 @@ class WorkerState:
                 self.tokenizers[name] = load_tokenizer(cfg, tok_dir)
             self.shards[name][shard_id] = rec
             return True
+
+    def join_pipeline(self, name: str, shard_id: int, path: str, spec: dict) -> bool:
+        """``/load_shard`` with a "pipeline" spec (the shard's layers go
+        onto this GPU and the worker joins the pipeline communicator). Every node of the
+        ring gets one such call: rank = shard id, ``world_size`` = the shard count of the
+        export (``metadata.json``), rendezvous at ``init_method`` (``tcp://host:port``). The
+        join runs in the background: the master posts to all N nodes before any of them can
+        finish the rendezvous. Rank 0 then serves the model as a pipeline head and reports
+        every stage as its shard (the master routes the model's requests to it); the other
+        ranks run their stage loop until the head unloads the model. /health shows the
+        state ("joining" -> "serving" | "failed")."""
+        meta = read_metadata(path, name, shard_id)
+        world = int(spec.get("world_size") or meta.get("num_shards") or 0)
+        init_method = spec.get("init_method")
+        if world < 2 or not init_method:
+            raise ValueError("pipeline spec needs init_method and world_size >= 2")
+        if not 0 <= shard_id < world:
+            raise ValueError(f"shard {shard_id} outside a {world}-stage pipeline")
+        with self.lock:
+            if self.pipeline is not None and self.pipeline["state"] in ("joining", "serving"):
+                if (self.pipeline["model_name"], self.pipeline["rank"]) == (name, shard_id):
+                    return False
+                raise ValueError(f"this worker already serves stage {self.pipeline['rank']} "
+                                 f"of {self.pipeline['model_name']}")
+            self.pipeline = {"model_name": name, "rank": shard_id, "world_size": world,
+                             "init_method": init_method, "state": "joining", "error": None}
+        shard_dir = os.path.dirname(path.rstrip("/"))
+        threading.Thread(target=self._join, args=(name, shard_id, world, init_method,
+                                                  shard_dir), daemon=True,
+                         name=f"dli-join-{name}-{shard_id}").start()
+        return True
+
+    def _join(self, name, rank, world, init_method, shard_dir):
+        from ..parallel.pipeline import DistributedPipelineEngine
+        from ..parallel.transport import init_distributed
+        from .service import PipelineService
+        rec = self.pipeline
+        try:
+            cuda = self.device.type == "cuda"
+            if cuda:
+                torch.cuda.set_device(self.device)
+            init_distributed(device=self.device if cuda else None, init_method=init_method,
+                             world_size=world, rank=rank)
+            kw = self.engine_kwargs
+            eng = DistributedPipelineEngine(name, self.device, max_batch=kw["max_batch"],
+                                            max_model_len=kw["max_model_len"],
+                                            num_blocks=kw["num_blocks"], shard_dir=shard_dir,
+                                            dtype=_shard_dtype(shard_dir, rank))
+            eng.warmup()
+            self._pipe_engine = eng
+            if rank == 0:
+                with self.lock:
+                    self.tokenizers[name] = eng.head.tok
+                    self.pipeline_shards = [
+                        {"model_name": name, "shard_id": p.shard_id,
+                         "path": os.path.join(shard_dir, f"shard_{p.shard_id}"),
+                         "metadata": read_metadata(os.path.join(shard_dir,
+                                                                f"shard_{p.shard_id}"),
+                                                   name, p.shard_id)}
+                        for p in eng.plans]
+                    self.pipeline_service = PipelineService(eng, name=name.replace("/", "_"))
+                    self.pipeline_model = name
+                    rec["state"] = "serving"
+                return
+            rec["state"] = "serving"
+            eng.serve()                  # until the head shuts the ring down
+            import torch.distributed as dist
+            dist.barrier()
+            eng.channel.close()
+            dist.destroy_process_group()
+            rec["state"] = "stopped"
+        except BaseException as e:  # noqa: BLE001 — reported by /health
+            log.error("pipeline join (%s stage %d/%d) failed: %s", name, rank, world, e)
+            rec["state"], rec["error"] = "failed", str(e)
+
+    def _leave_pipeline(self):
+        """Rank 0: unload of the pipeline model shuts the whole ring down."""
+        svc = getattr(self, "pipeline_service", None)
+        eng = self._pipe_engine
+        if svc is not None:
+            svc.close()
+        if eng is not None and eng.head is not None:
+            eng.shutdown()
+            import torch.distributed as dist
+            dist.barrier()
+            eng.channel.close()
+            dist.destroy_process_group()
+        self.pipeline_service = None
+        self.pipeline_model = None
+        self.pipeline_shards = []
+        self._pipe_engine = None
+        if self.pipeline is not None:
+            self.pipeline["state"] = "stopped"
 
     def shard_pipeline(self, name: str, shard_ids):
         """A loopback pipeline over the listed loaded shards (they must cover every layer),
@@ -207,6 +305,19 @@ class WorkerState:
                 "device": self.device_str, **extra}
 
 
+def _shard_dtype(shard_dir: str, rank: int) -> torch.dtype:
+    """Compute dtype of an exported stage = the dtype its weights were written in (the
+    data plane carries activations of that dtype between stages)."""
+    from safetensors import safe_open
+    f = os.path.join(shard_dir, f"shard_{rank}", "model.safetensors")
+    if not os.path.exists(f):
+        return torch.bfloat16
+    with safe_open(f, "pt") as h:
+        keys = list(h.keys())
+        code = h.get_slice(keys[0]).get_dtype() if keys else "BF16"   # header only
+    return {"F32": torch.float32, "F16": torch.float16}.get(code, torch.bfloat16)
+
+
 def request_params(data: dict):
     """(SamplingParams, timeout) of an /inference body: the reference's generate() call
     (worker/app.py:297-305: do_sample, T 0.8, top-k 50, top-p 0.95, max_length incl. the
@@ -256,8 +367,9 @@ def create_worker_app(settings: Optional[Settings] = None, device: Optional[str]
         shard_info = [{"model_name": m, "shard_id": sid, "path": r["path"],
                        "metadata": r["metadata"]}
                       for m, sh in st.shards.items() for sid, r in sh.items()]
-        shard_info += getattr(st, "pipeline_shards", [])
-        return jsonify({"status": "healthy", "resources": st.resources(),
+        shard_info += getattr(st, "pipeline_shards", None) or []
+        extra = {"pipeline": st.pipeline} if st.pipeline is not None else {}
+        return jsonify({"status": "healthy", "resources": st.resources(), **extra,
                         "loaded_models": list(st.services.keys()),
                         "loaded_tokenizers": list(st.tokenizers.keys()),
                         "loaded_shards": shard_info})
@@ -287,7 +399,14 @@ def create_worker_app(settings: Optional[Settings] = None, device: Optional[str]
             return jsonify({"status": "error",
                             "message": "Model name, shard ID, and shard path are required"}), 400
         try:
-            fresh = st.load_shard(name, int(sid), str(path))
+            if isinstance(data.get("pipeline"), dict):
+                fresh = st.join_pipeline(name, int(sid), str(path), data["pipeline"])
+                if fresh:
+                    return jsonify({"status": "success",
+                                    "message": f"Shard {sid} of model {name} is joining the "
+                                               f"pipeline", "pipeline": st.pipeline})
+            else:
+                fresh = st.load_shard(name, int(sid), str(path))
         except Exception as e:  # noqa: BLE001
             return jsonify({"status": "error", "message": f"Failed to load shard: {e}"}), 500
         if not fresh:
@@ -327,6 +446,12 @@ def create_worker_app(settings: Optional[Settings] = None, device: Optional[str]
                 # pipeline head (serve-pipeline / one DP replica of serve-cluster): every
                 # stage of this model runs on this rank's pipeline, with or without shard_ids
                 out = svc.generate(prompt, params, timeout=timeout + 30)
+            elif (st.pipeline is not None and st.pipeline["model_name"] == name
+                  and st.pipeline["rank"] != 0):
+                return jsonify({"status": "error",
+                                "message": f"Inference failed: this node is stage "
+                                           f"{st.pipeline['rank']} of the {name} pipeline; "
+                                           f"requests enter at its stage-0 node"}), 409
             elif shard_ids:
                 svc = st.shard_pipeline(name, [int(s) for s in shard_ids])
                 out = svc.generate(prompt, params, timeout=timeout + 30)

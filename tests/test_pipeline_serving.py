@@ -209,3 +209,83 @@ def test_load_model_reads_model_cache(tmp_path):
                     max_model_len=128, num_blocks=64)
     assert rnd.generate(["abc"], SamplingParams(max_length=16, temperature=0))[0].all_ids \
         != want.all_ids                                   # really not the default init
+
+
+def _wait_http(url, timeout=120):
+    import requests
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        try:
+            return requests.get(url, timeout=2).json()
+        except Exception:  # noqa: BLE001
+            time.sleep(0.3)
+    raise TimeoutError(url)
+
+
+def test_load_shard_joins_pipeline_ring(tmp_path):
+    """W5: two independently started worker processes receive /load_shard with a
+    "pipeline" spec, rendezvous (gloo here, RCCL on GPUs) and serve the exported shards as
+    one 2-stage ring; requests go to the stage-0 node, which reports both shards; unloading
+    the model there shuts the ring down on both nodes."""
+    import subprocess
+    import sys
+
+    import requests
+    from distributed_llm_inferencing_amd.shard.writer import export_shards
+    from distributed_llm_inferencing_amd.worker.server import create_worker_app
+    paths = export_shards("llama-tiny", 2, str(tmp_path / "shards"), dtype=torch.float32,
+                          log=lambda *a: None)
+    ports = [_free_port(), _free_port()]
+    rdv = _free_port()
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", USE_GPU="0",
+               OMP_NUM_THREADS="2", MODEL_CACHE_DIR=str(tmp_path / "cache"))
+    procs = [subprocess.Popen([sys.executable, "-m", "distributed_llm_inferencing_amd.worker.server",
+                               "--host", "127.0.0.1", "--port", str(p)], env=env,
+                              stdout=subprocess.DEVNULL,
+                              stderr=open(tmp_path / f"worker{p}.log", "w"))
+             for p in ports]
+    try:
+        urls = [f"http://127.0.0.1:{p}" for p in ports]
+        for u in urls:
+            _wait_http(f"{u}/health")
+        # a repeated /load_shard of the same stage is idempotent; join-pipeline (the CLI the
+        # operator uses) assigns shard i to node i and waits for every stage to serve
+        from distributed_llm_inferencing_amd.cli import main as cli_main
+        spec = {"init_method": f"tcp://127.0.0.1:{rdv}", "world_size": 2}
+        r = requests.post(f"{urls[1]}/load_shard", json={
+            "model_name": "llama-tiny", "shard_id": 1, "shard_path": str(paths[1]),
+            "pipeline": spec}, timeout=30)
+        assert r.status_code == 200 and r.json()["pipeline"]["state"] == "joining", r.text
+        assert cli_main(["join-pipeline", "--model", "llama-tiny", "--shard-dir",
+                         str(paths[0].parent), "--nodes", ",".join(urls), "--rendezvous",
+                         spec["init_method"], "--timeout", "240"]) == 0
+        hs = [requests.get(f"{u}/health", timeout=5).json() for u in urls]
+        states = [h["pipeline"]["state"] for h in hs]
+        assert states == ["serving", "serving"], hs
+        assert sorted(s["shard_id"] for s in hs[0]["loaded_shards"]) == [0, 1]
+        assert hs[1]["loaded_shards"] == []   # the master routes this model to stage 0
+        body = {"model_name": "llama-tiny", "prompt": "pipeline join", "max_length": 24,
+                "temperature": 0, "shard_ids": [0, 1]}
+        r0 = requests.post(f"{urls[0]}/inference", json=body, timeout=120)
+        assert r0.status_code == 200, r0.text
+        assert requests.post(f"{urls[1]}/inference", json=body, timeout=30).status_code == 409
+        # same shards through the single-process loopback path
+        app = create_worker_app(_settings(tmp_path), device="cpu")
+        c = app.test_client()
+        for i, p in enumerate(paths):
+            c.post("/load_shard", json={"model_name": "llama-tiny", "shard_id": i,
+                                        "shard_path": str(p)})
+        ref = c.post("/inference", json=body).get_json()
+        assert r0.json()["result"] == ref["result"]
+        assert requests.post(f"{urls[0]}/unload_model", json={"model_name": "llama-tiny"},
+                             timeout=60).status_code == 200
+        t0 = time.time()
+        while requests.get(f"{urls[1]}/health", timeout=5).json()["pipeline"]["state"] \
+                != "stopped":
+            assert time.time() - t0 < 60
+            time.sleep(0.3)
+    finally:
+        for p in procs:
+            p.terminate()
+        for p in procs:
+            p.wait(timeout=30)
