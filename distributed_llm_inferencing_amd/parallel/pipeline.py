@@ -210,27 +210,32 @@ class _TokenRing:
             self.host = torch.empty((M, max_batch), dtype=torch.int32, pin_memory=True)
             self.ev = [torch.cuda.Event() for _ in range(M)]
         self.n = [0] * M
+        self.rows = list(self.dev.unbind(0))          # per-slot views, made once
+        self.host_rows = list(self.host.unbind(0)) if self.cuda else None
 
     def slot(self, start_tick: int, n: int) -> torch.Tensor:
-        return self.dev[start_tick % self.M, :n]
+        return self.rows[start_tick % self.M][:n]
 
     def landed(self, start_tick: int, n: int, src: Optional[torch.Tensor] = None) -> None:
         """Tokens of microbatch ``start_tick`` are in (or, with ``src``, copied into) their
         device slot: start the host copy."""
         j = start_tick % self.M
-        if src is not None and src.data_ptr() != self.dev[j].data_ptr():
-            self.dev[j, :n].copy_(src[:n].to(self.dev.device), non_blocking=True)
+        row = self.rows[j]
+        if src is not None and src.data_ptr() != row.data_ptr():
+            if src.device != row.device:
+                src = src.to(row.device)
+            row[:n].copy_(src if src.shape[0] == n else src[:n], non_blocking=True)
         self.n[j] = n
         if self.cuda:
-            self.host[j, :n].copy_(self.dev[j, :n], non_blocking=True)
+            self.host_rows[j][:n].copy_(row[:n], non_blocking=True)
             self.ev[j].record()
 
     def get(self, start_tick: int) -> np.ndarray:
         j = start_tick % self.M
         if self.cuda:
             self.ev[j].synchronize()
-            return self.host[j, :self.n[j]].numpy()
-        return self.dev[j, :self.n[j]].numpy()
+            return self.host_rows[j][:self.n[j]].numpy()
+        return self.rows[j][:self.n[j]].numpy()
 
 
 class PipelineHead:

@@ -47,11 +47,19 @@ def _roctx():
     return _ROCTX
 
 
-@contextlib.contextmanager
+_NULL_RANGE = contextlib.nullcontext()
+
+
 def trace_range(name: str):
+    """roctx range around a block; a shared no-op context when tracing is off (this wraps
+    per-tick pipeline operations: no generator per call on the hot path)."""
     if not enabled():
-        yield
-        return
+        return _NULL_RANGE
+    return _roctx_range(name)
+
+
+@contextlib.contextmanager
+def _roctx_range(name: str):
     lib = _roctx()
     if lib is not None:
         lib.roctxRangePushA(name.encode())
