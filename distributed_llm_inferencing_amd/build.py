@@ -8,8 +8,9 @@ repo snapshot; they are git-ignored):
 * ``lib/libdli_runtime.so`` — the host-side C++ runtime in ``csrc/runtime``: paged-KV block
   allocator + batched block-table / slot builders (``block_manager.cpp``), the decode fast
   path of the continuous-batching scheduler (``decode_core.cpp``), the safetensors weight
-  loader with pinned staging + hipMemcpyAsync (``safetensors_loader.cpp``) and the
-  pipeline's shared-memory control ring (``shm_ring.cpp``).
+  loader with pinned staging + hipMemcpyAsync (``safetensors_loader.cpp``), the
+  pipeline's shared-memory control ring (``shm_ring.cpp``) and its optional RCCL data
+  plane (``comm.cpp``: grouped ncclSend/ncclRecv on the compute stream, ``DLI_PP_COMM=rccl``).
 
 Each library is stamped with a digest of its sources + flags (``<lib>.sha1``); the loaders
 (``ops/_native.py``, ``runtime/__init__.py``) rebuild a library whose stamp does not match
