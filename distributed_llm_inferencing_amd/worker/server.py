@@ -233,9 +233,10 @@ class WorkerState:
         if svc is not None:
             svc.close()
         if eng is not None and eng.head is not None:
-            eng.shutdown()
             import torch.distributed as dist
-            dist.barrier()
+            if svc is None or svc.error is None:      # a broken ring gets no goodbye
+                eng.shutdown()
+                dist.barrier()
             eng.channel.close()
             dist.destroy_process_group()
         self.pipeline_service = None
