@@ -153,6 +153,9 @@ def main():
     ap.add_argument("--max-model-len", type=int, default=512)
     ap.add_argument("--shard-dir", default=None,
                     help="N>1 pp: load each stage from <dir>/shard_<rank>/ (shard-model output)")
+    ap.add_argument("--pp-prefill-chunks", type=int, default=2,
+                    help="N>1 pp: admit each microbatch's prompts over this many prefill "
+                         "steps (smaller ring-fill bubble at the start of a wave)")
     ap.add_argument("--mode", default="auto", choices=["auto", "pp", "ep", "tp", "dp"],
                     help="N>1: pp = layer-sharded pipeline (dense, default), ep = expert "
                          "parallel (MoE), tp = tensor-parallel ablation, dp = independent "

@@ -779,9 +779,16 @@ def bench_pipeline(args, world: int, rank: int, make_prompts):
         device = torch.device("cuda", local)
     else:
         device = torch.device("cpu")
+    # prefill admission in C steps per microbatch (bench --pp-prefill-chunks, default 2): the
+    # wave starts with every stage filling the ring, and stage r idles r ticks of prefill
+    # length — the GPipe bubble (N-1)/(C*M+N-1) of the prefill phase. At N = 8 (M = 11, a
+    # 16k-token prefill tick ~21 ms on a 4-layer stage) one step per microbatch idles ~150 ms
+    # per ~1.3 s wave; two steps of 8k tokens halve that. Decode ticks are unchanged.
+    chunks = max(1, int(getattr(args, "pp_prefill_chunks", 2)))
     eng = DistributedPipelineEngine(args.model, device, max_batch=args.batch,
                                     max_model_len=args.max_model_len,
-                                    max_prefill_tokens=max(args.batch * args.prompt_len, 8192),
+                                    max_prefill_tokens=max(args.batch * args.prompt_len // chunks,
+                                                           4096),
                                     shard_dir=getattr(args, "shard_dir", None))
     world = eng.world
     eng.warmup()
