@@ -15,6 +15,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("dir")
 ap.add_argument("top", nargs="?", type=int, default=25)
 ap.add_argument("--tail-ms", type=float, default=None)
+ap.add_argument("--gaps", type=int, default=0,
+                help="also list the N longest GPU-idle gaps (kernel before -> kernel after)")
 a = ap.parse_args()
 d = Path(a.dir)
 tr = list(d.glob("*kernel_trace.csv"))
@@ -52,3 +54,18 @@ if ev:
     busy += cur_e - cur_s
     span = ev[-1][1] - ev[0][0]
     print(f"trace span {span/1e6:.1f} ms, GPU busy (union) {busy/1e6:.1f} ms = {100*busy/span:.1f}%")
+    if a.gaps:
+        gaps, end, prev = [], ev[0][1], ev[0][2]
+        t0 = ev[0][0]
+        for s_, e_, n_ in ev[1:]:
+            if s_ > end:
+                gaps.append((s_ - end, prev, n_, end - t0))
+            if e_ > end:
+                end, prev = e_, n_
+        gaps.sort(reverse=True)
+        idle = sum(g[0] for g in gaps)
+        print(f"idle gaps: {len(gaps)}, total {idle/1e6:.2f} ms; "
+              f"> 100 us: {sum(1 for g in gaps if g[0] > 1e5)} "
+              f"({sum(g[0] for g in gaps if g[0] > 1e5)/1e6:.2f} ms)")
+        for g, before, after, at in gaps[:a.gaps]:
+            print(f"  {g/1e3:9.1f} us at {at/1e6:8.2f} ms  after {before[:44]}  before {after[:44]}")
