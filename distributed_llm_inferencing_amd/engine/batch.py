@@ -42,7 +42,7 @@ class StepMeta:
     # chunked prefill (not on the wire): True for rows whose chunk completes the prompt; the
     # token sampled for any other row is discarded. None = every row samples.
     sample_mask: Optional[np.ndarray] = None
-    # mixed step (single stage, not on the wire): the first num_decode sequences are decode
+    # mixed step (header word 9 on the wire): the first num_decode sequences are decode
     # rows (one token each, attended by the decode kernel), the rest prefill chunks
     num_decode: int = 0
     # columns of block_tables that hold blocks (the scheduler knows it; pack trims to it)
@@ -76,6 +76,7 @@ class StepMeta:
                           self.microbatch, self.step_id]
             header[7] = 1
             header[8] = max(int(self.table_width_full), int(self.table_used))
+            header[9] = int(self.num_decode)
             return header, self.packed_payload
         tables = self.block_tables
         width = 0 if tables is None else int(tables.shape[1])
@@ -124,6 +125,7 @@ class StepMeta:
         header[:7] = [self.kind, S, T, mb, payload.shape[0], self.microbatch, self.step_id]
         header[7] = 1 if self.input_ids is not None else 0
         header[8] = width
+        header[9] = int(self.num_decode)          # mixed step: leading one-token decode rows
         return header, payload
 
     @staticmethod
@@ -153,7 +155,7 @@ class StepMeta:
                         input_ids=input_ids if header[7] else None, positions=positions,
                         slot_mapping=slots, seq_lens=seq_lens, context_lens=ctx,
                         block_tables=bt, temperature=temp, top_k=topk, top_p=topp, seeds=seeds,
-                        microbatch=micro, step_id=step)
+                        microbatch=micro, step_id=step, num_decode=int(header[9]))
 
 
 def _i32(a, n):

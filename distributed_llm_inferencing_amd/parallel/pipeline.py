@@ -619,7 +619,13 @@ class DistributedPipelineEngine:
                                if vocab_parallel is None else vocab_parallel)
         self.microbatches = num_microbatches(self.world, self.vocab_parallel)
         max_model_len = min(max_model_len, self.cfg.max_position)
-        max_tokens = max(max_prefill_tokens, max_model_len, max_batch)
+        # mixed steps (DLI_MIXED_STEPS, default on): a prefill step of a microbatch that is
+        # decoding also carries that microbatch's decode rows (one token each), so its
+        # running sequences do not sit out the admission; such a step holds up to
+        # max_prefill_tokens + max_batch tokens (every rank sizes for it, whatever the head
+        # decides)
+        self.mixed_steps = os.environ.get("DLI_MIXED_STEPS", "1") == "1"
+        max_tokens = max(max_prefill_tokens + max_batch, max_model_len)
         self.stage, self.plans, nb, tw = build_stage(
             self.cfg, self.rank, self.world, self.device, max_batch, max_model_len, block_size,
             policy=policy, seed=seed, use_graphs=use_graphs, num_blocks=num_blocks, dtype=dtype,
@@ -634,7 +640,8 @@ class DistributedPipelineEngine:
                               num_microbatches=self.microbatches,
                               eos_token_id=self.cfg.eos_token_id,
                               max_model_len=max_model_len, table_width=tw,
-                              native_decode=os.environ.get("DLI_NATIVE_SCHED", "1") == "1")
+                              native_decode=os.environ.get("DLI_NATIVE_SCHED", "1") == "1",
+                              mixed_steps=self.mixed_steps)
             tok_path = None
             if shard_dir is not None and (Path(shard_dir) / "tokenizer").exists():
                 tok_path = str(Path(shard_dir) / "tokenizer")

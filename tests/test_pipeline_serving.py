@@ -109,10 +109,13 @@ def _admit_worker(rank, world, port, q):
         def track(key, fut):
             fut.add_done_callback(lambda f: done.setdefault(key, (time.perf_counter(),
                                                                   f.result())))
-        for i, p in enumerate(PROMPTS[:4]):
-            track(("long", i), svc.submit(p, long_sp))
-        while eng.head.stats.decode_steps < 10:           # the session is running
-            time.sleep(0.005)
+        # the long requests arrive in three groups, so each of the M = 3 microbatches is
+        # decoding when the short ones arrive (admission goes to the least-loaded one)
+        for grp, until in (((0, 1), 2), ((2,), 4), ((3,), 10)):
+            for i in grp:
+                track(("long", i), svc.submit(PROMPTS[i], long_sp))
+            while eng.head.stats.decode_steps < until:    # the session is running
+                time.sleep(0.005)
         for i, p in enumerate(PROMPTS[4:]):
             track(("short", i), svc.submit(p, short_sp))
         while len(done) < 6:
@@ -121,7 +124,7 @@ def _admit_worker(rank, world, port, q):
             time.sleep(0.01)
         time.sleep(0.2)
         res = {k: (t, o.all_ids) for k, (t, o) in done.items()}
-        q.put((res, svc.sessions))
+        q.put((res, svc.sessions, eng.head.sched.num_mixed))
         svc.close()
         eng.shutdown()
     dist.barrier()
@@ -131,9 +134,12 @@ def _admit_worker(rank, world, port, q):
 
 def test_pipeline_service_admits_requests_into_running_session():
     q, procs = _spawn(_admit_worker, 2)
-    res, sessions = q.get(timeout=300)
+    res, sessions, mixed = q.get(timeout=300)
     _join(procs)
     assert sessions == 1                                   # the late requests joined it
+    # the late prompts were prefilled in mixed steps: the running microbatch's decode rows
+    # rode along (header word 9 tells every stage where the decode rows end)
+    assert mixed >= 1
     last_long = max(t for (kind, _), (t, _) in res.items() if kind == "long")
     assert all(t < last_long for (kind, _), (t, _) in res.items() if kind == "short")
     ref = LLMEngine("llama-tiny", device="cpu", dtype=torch.float32, max_batch=8,
