@@ -3,7 +3,10 @@
 HF transformers AutoModelForCausalLM.generate, batch 1, requests served one at a time
 (1 sync gunicorn worker, worker/Dockerfile:45), do_sample T=0.8 top_k=50 top_p=0.95,
 max_length=100 including a 32-token synthetic prompt, random-init weights, bf16 on GPU.
-Writes profiles/reference_strategy.json (bench.py divides by it for vs_baseline)."""
+Writes profiles/reference_strategy.json (bench.py divides by it for vs_baseline).
+
+``--batch B`` runs the same HF ``generate`` on B prompts at once instead (not the
+reference's strategy: a like-for-like comparator for bench.py's batch-512 wave).""" 
 import argparse
 import json
 import statistics
@@ -21,6 +24,8 @@ def main():
     ap.add_argument("--prompt-len", type=int, default=32)
     ap.add_argument("--max-length", type=int, default=100)
     ap.add_argument("--out", default="profiles/reference_strategy.json")
+    ap.add_argument("--batch", type=int, default=1,
+                    help="prompts per generate call (1 = the reference's strategy)")
     a = ap.parse_args()
     import sys
     sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
@@ -39,8 +44,8 @@ def main():
     rng = np.random.default_rng(0)
     lats, toks = [], 0
     for r in range(a.requests + 1):
-        ids = torch.tensor([rng.integers(1000, cfg.vocab_size - 1000, a.prompt_len).tolist()],
-                           device="cuda")
+        ids = torch.tensor([rng.integers(1000, cfg.vocab_size - 1000, a.prompt_len).tolist()
+                            for _ in range(a.batch)], device="cuda")
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         with torch.no_grad():
@@ -52,8 +57,11 @@ def main():
         if r == 0:
             continue  # warmup
         lats.append(dt)
-        toks += out.shape[1] - a.prompt_len
-    res = {"metric": "output tokens/sec (reference strategy: HF generate, batch 1, serial)",
+        toks += a.batch * (out.shape[1] - a.prompt_len)
+    res = {"metric": ("output tokens/sec (reference strategy: HF generate, batch 1, serial)"
+                      if a.batch == 1 else
+                      f"output tokens/sec (HF generate, {a.batch} prompts per call)"),
+           "batch": a.batch,
            "value": toks / sum(lats), "p50_latency_s": statistics.median(lats),
            "requests": a.requests, "model": a.model, "transformers": tf.__version__,
            "torch": torch.__version__, "device": torch.cuda.get_device_name(0)}
