@@ -15,6 +15,7 @@ import socket
 import threading
 import time
 
+import pytest
 import torch
 import torch.multiprocessing as mp
 
@@ -89,9 +90,9 @@ def test_gloo_ring_serves_shard_files(tmp_path):
 
 
 # ----------------------------------------------------------------------------- admission
-def _admit_worker(rank, world, port, q):
+def _admit_worker(rank, world, port, q, vp):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
-                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), DLI_PP_VOCAB_PARALLEL=vp)
     torch.set_num_threads(1)
     import torch.distributed as dist
     from distributed_llm_inferencing_amd.parallel.pipeline import DistributedPipelineEngine
@@ -104,27 +105,30 @@ def _admit_worker(rank, world, port, q):
         svc = PipelineService(eng, name="pp")
         long_sp = SamplingParams(max_length=90, do_sample=False, ignore_eos=True)
         short_sp = SamplingParams(max_length=12, do_sample=False, ignore_eos=True)
+        M = eng.microbatches
         done = {}
 
         def track(key, fut):
             fut.add_done_callback(lambda f: done.setdefault(key, (time.perf_counter(),
                                                                   f.result())))
-        # the long requests arrive in three groups, so each of the M = 3 microbatches is
-        # decoding when the short ones arrive (admission goes to the least-loaded one)
-        for grp, until in (((0, 1), 2), ((2,), 4), ((3,), 10)):
-            for i in grp:
-                track(("long", i), svc.submit(PROMPTS[i], long_sp))
-            while eng.head.stats.decode_steps < until:    # the session is running
+        # one long request per microbatch, arriving one after another (admission goes to
+        # the least-loaded microbatch), so every microbatch is decoding when the short
+        # requests arrive
+        for i in range(M):
+            track(("long", i), svc.submit(ADMIT_PROMPTS[i], long_sp))
+            while eng.head.stats.decode_steps < 2 * i + 2:  # the session is running
                 time.sleep(0.005)
-        for i, p in enumerate(PROMPTS[4:]):
-            track(("short", i), svc.submit(p, short_sp))
-        while len(done) < 6:
+        while eng.head.stats.decode_steps < 2 * M + 6:
+            time.sleep(0.005)
+        for i in range(2):
+            track(("short", i), svc.submit(ADMIT_PROMPTS[M + i], short_sp))
+        while len(done) < M + 2:
             time.sleep(0.01)
         while svc.sessions < 1:
             time.sleep(0.01)
         time.sleep(0.2)
         res = {k: (t, o.all_ids) for k, (t, o) in done.items()}
-        q.put((res, svc.sessions, eng.head.sched.num_mixed))
+        q.put((res, svc.sessions, eng.head.sched.num_mixed, M, eng.vocab_parallel))
         svc.close()
         eng.shutdown()
     dist.barrier()
@@ -132,23 +136,30 @@ def _admit_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_pipeline_service_admits_requests_into_running_session():
-    q, procs = _spawn(_admit_worker, 2)
-    res, sessions, mixed = q.get(timeout=300)
+ADMIT_PROMPTS = PROMPTS + [[11, 12, 13, 14, 15], [42] * 6, [8, 9]]
+
+
+@pytest.mark.parametrize("vp", ["0", "1"])
+def test_pipeline_service_admits_requests_into_running_session(vp):
+    """Requests arriving mid-session join it; they are prefilled in MIXED steps (the
+    running microbatch's decode rows ride along; header word 9 tells every stage where the
+    decode rows end), with the tail LM head and with the vocab-parallel head; greedy
+    tokens equal the single-stage engine's."""
+    q, procs = _spawn(_admit_worker, 2, vp)
+    res, sessions, mixed, M, vp_on = q.get(timeout=300)
     _join(procs)
+    assert vp_on == (vp == "1")
     assert sessions == 1                                   # the late requests joined it
-    # the late prompts were prefilled in mixed steps: the running microbatch's decode rows
-    # rode along (header word 9 tells every stage where the decode rows end)
     assert mixed >= 1
     last_long = max(t for (kind, _), (t, _) in res.items() if kind == "long")
     assert all(t < last_long for (kind, _), (t, _) in res.items() if kind == "short")
     ref = LLMEngine("llama-tiny", device="cpu", dtype=torch.float32, max_batch=8,
                     max_model_len=128, num_blocks=128)
-    longs = [o.all_ids for o in ref.generate(PROMPTS[:4], SamplingParams(
+    longs = [o.all_ids for o in ref.generate(ADMIT_PROMPTS[:M], SamplingParams(
         max_length=90, do_sample=False, ignore_eos=True))]
-    shorts = [o.all_ids for o in ref.generate(PROMPTS[4:], SamplingParams(
+    shorts = [o.all_ids for o in ref.generate(ADMIT_PROMPTS[M:M + 2], SamplingParams(
         max_length=12, do_sample=False, ignore_eos=True))]
-    assert [res[("long", i)][1] for i in range(4)] == longs
+    assert [res[("long", i)][1] for i in range(M)] == longs
     assert [res[("short", i)][1] for i in range(2)] == shorts
 
 
