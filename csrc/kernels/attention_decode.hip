@@ -26,47 +26,20 @@
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 
-// MINW = 4 waves per SIMD: <= 128 VGPRs, so every item of a 512-sequence batch (4096 waves)
-// is resident at once (measured 7 % faster than the 166-VGPR / 2-waves build at ctx 66)
-template <int HD, int MINW>
-__global__ void __launch_bounds__(256, MINW) decode_attn_kernel(
-    u16* __restrict__ out, const u16* __restrict__ q, int q_stride,
-    const u16* __restrict__ k_cache, const u16* __restrict__ v_cache,
-    const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ context_lens,
-    int B, int hq, int hkv, int block_size, float scale_log2, int num_splits, int split_tokens,
+// The tile loop shared by the plain and the fused kernel: one wave = one (sequence, kv head,
+// split) item with its Q^T fragments already in registers.
+template <int HD>
+__device__ __forceinline__ void decode_attn_core(
+    const bf16x8 (&qf)[HD / 32], u16* vt, int lane, int b, int kvh, int split, int G, int ctx,
+    int s_begin, int s_end, u16* __restrict__ out, const u16* __restrict__ k_cache,
+    const u16* __restrict__ v_cache, const int* __restrict__ block_tables, int max_blocks,
+    int hq, int hkv, int block_size, float scale_log2, int num_splits,
     float* __restrict__ ws_o, float* __restrict__ ws_ml) {
-  constexpr int KK = HD / 32;     // MFMA k-steps over head_dim
   constexpr int DB = HD / 16;     // 16-wide output column blocks (= V pieces per lane)
+  constexpr int KK = HD / 32;
   constexpr int VROW = HD + 16;   // padded LDS row of the V tile, in u16
   constexpr int VCH = HD / 8;     // 16-B chunks per V row
-  __shared__ __attribute__((aligned(16))) u16 vtile_all[DEC_WAVES][DEC_TILE * VROW];
-  u16* vt = vtile_all[threadIdx.x >> 6];
-  const int lane = threadIdx.x & 63;
-  // one WAVE per work item (sequence, kv head, KV split): no LDS, no barriers, so every
-  // resident wave of the chip streams a different (seq, head) pair concurrently
-  const int item = blockIdx.x * DEC_WAVES + (threadIdx.x >> 6);
-  if (item >= B * hkv * num_splits) return;                    // wave-uniform exit
-  const int split = item % num_splits;
-  const int bh = item / num_splits;
-  const int kvh = bh % hkv, b = bh / hkv;
   const int col = lane & 15, grp = lane >> 4;
-  const int G = hq / hkv;
-  const int ctx = context_lens[b];
-  const int s_begin = split * split_tokens;
-  const int s_end = min(ctx, s_begin + split_tokens);
-
-  // Q^T fragments (B operand): head = col, dims 32kk + 8grp .. +7
-  bf16x8 qf[KK];
-  {
-    const bool valid = col < G;
-    const u16* qp = q + (long)b * q_stride + (long)(kvh * G + (valid ? col : 0)) * HD;
-#pragma unroll
-    for (int kk = 0; kk < KK; ++kk) {
-      uint4 v = valid ? *reinterpret_cast<const uint4*>(qp + kk * 32 + grp * 8)
-                      : make_uint4(0, 0, 0, 0);
-      qf[kk] = *reinterpret_cast<bf16x8*>(&v);
-    }
-  }
   const int* bt = block_tables + (long)b * max_blocks;
   // the split's block ids, one per lane, read once per 64-block window (token -> block by a
   // lane shuffle): the per-tile K/V loads no longer wait on a dependent block-table load
@@ -199,7 +172,142 @@ __global__ void __launch_bounds__(256, MINW) decode_attn_kernel(
         ws_ml[base * 2 + 1] = lr;
       }
     }
+  }}
+
+// MINW = 4 waves per SIMD: <= 128 VGPRs, so every item of a 512-sequence batch (4096 waves)
+// is resident at once (measured 7 % faster than the 166-VGPR / 2-waves build at ctx 66)
+template <int HD, int MINW>
+__global__ void __launch_bounds__(256, MINW) decode_attn_kernel(
+    u16* __restrict__ out, const u16* __restrict__ q, int q_stride,
+    const u16* __restrict__ k_cache, const u16* __restrict__ v_cache,
+    const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ context_lens,
+    int B, int hq, int hkv, int block_size, float scale_log2, int num_splits, int split_tokens,
+    float* __restrict__ ws_o, float* __restrict__ ws_ml) {
+  constexpr int KK = HD / 32;     // MFMA k-steps over head_dim
+  constexpr int VROW = HD + 16;   // padded LDS row of the V tile, in u16
+  __shared__ __attribute__((aligned(16))) u16 vtile_all[DEC_WAVES][DEC_TILE * VROW];
+  u16* vt = vtile_all[threadIdx.x >> 6];
+  const int lane = threadIdx.x & 63;
+  // one WAVE per work item (sequence, kv head, KV split): no LDS, no barriers, so every
+  // resident wave of the chip streams a different (seq, head) pair concurrently
+  const int item = blockIdx.x * DEC_WAVES + (threadIdx.x >> 6);
+  if (item >= B * hkv * num_splits) return;                    // wave-uniform exit
+  const int split = item % num_splits;
+  const int bh = item / num_splits;
+  const int kvh = bh % hkv, b = bh / hkv;
+  const int col = lane & 15, grp = lane >> 4;
+  const int G = hq / hkv;
+  const int ctx = context_lens[b];
+  const int s_begin = split * split_tokens;
+  const int s_end = min(ctx, s_begin + split_tokens);
+
+  // Q^T fragments (B operand): head = col, dims 32kk + 8grp .. +7
+  bf16x8 qf[KK];
+  {
+    const bool valid = col < G;
+    const u16* qp = q + (long)b * q_stride + (long)(kvh * G + (valid ? col : 0)) * HD;
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      uint4 v = valid ? *reinterpret_cast<const uint4*>(qp + kk * 32 + grp * 8)
+                      : make_uint4(0, 0, 0, 0);
+      qf[kk] = *reinterpret_cast<bf16x8*>(&v);
+    }
   }
+  decode_attn_core<HD>(qf, vt, lane, b, kvh, split, G, ctx, s_begin, s_end, out, k_cache,
+                       v_cache, block_tables, max_blocks, hq, hkv, block_size, scale_log2,
+                       num_splits, ws_o, ws_ml);
+}
+
+// Fused variant for the decode graph (one KV split per item): the QKV GEMM's split-K fp32
+// slabs go straight into the attention wave instead of through dli_splitk_rope_cache.
+// Prologue of item (sequence b, kv head h): lane l sums the slabs of this token's k and v
+// for dims l and l + 64 of head h, rounds to bf16, rotates k (RoPE) and writes both into
+// the paged cache at slot_mapping[b]; then each lane builds its Q^T fragments (head col of
+// the GQA group, dims 32kk + 8grp .. +7 and their RoPE partners 64 apart, which the same
+// lane holds) from the slabs. Numerics equal the unfused kernels: sum -> bf16 -> rotate ->
+// bf16. The q rows never go to memory, and one kernel per layer and its slab pass are gone.
+template <int SPL>
+__global__ void __launch_bounds__(256, 4) decode_attn_fused_kernel(
+    u16* __restrict__ out, const float* __restrict__ ws, int N,
+    const int* __restrict__ positions, const int* __restrict__ slot_mapping,
+    const float* __restrict__ cos_sin, u16* __restrict__ k_cache, u16* __restrict__ v_cache,
+    const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ context_lens,
+    int B, int hq, int hkv, int block_size, float scale_log2) {
+  constexpr int HD = 128, HALF = 64, KK = HD / 32, VROW = HD + 16;
+  __shared__ __attribute__((aligned(16))) u16 vtile_all[DEC_WAVES][DEC_TILE * VROW];
+  u16* vt = vtile_all[threadIdx.x >> 6];
+  const int lane = threadIdx.x & 63;
+  const int item = blockIdx.x * DEC_WAVES + (threadIdx.x >> 6);
+  if (item >= B * hkv) return;                                 // wave-uniform exit
+  const int kvh = item % hkv, b = item / hkv;
+  const int col = lane & 15, grp = lane >> 4;
+  const int G = hq / hkv;
+  const int ctx = context_lens[b];
+  const float* cs = cos_sin + (long)positions[b] * HD;
+  const long rowoff = (long)b * N;
+  const long splitstride = (long)B * N;
+  // ---- this token's k (rotated) and v -> paged cache (lane: dims lane, lane + 64)
+  const int slot = slot_mapping[b];
+  if (slot >= 0) {
+    const float* kp = ws + rowoff + (long)(hq + kvh) * HD;
+    const float* vp = ws + rowoff + (long)(hq + hkv + kvh) * HD;
+    float k1 = 0.f, k2 = 0.f, v1 = 0.f, v2 = 0.f;
+#pragma unroll
+    for (int s = 0; s < SPL; ++s) {
+      k1 += kp[s * splitstride + lane];
+      k2 += kp[s * splitstride + HALF + lane];
+      v1 += vp[s * splitstride + lane];
+      v2 += vp[s * splitstride + HALF + lane];
+    }
+    k1 = bf2f(f2bf(k1)); k2 = bf2f(f2bf(k2));
+    const float co = cs[lane], si = cs[HALF + lane];
+    const int blk = slot / block_size, off = slot - blk * block_size;
+    const long dst = (((long)blk * hkv + kvh) * block_size + off) * HD;
+    k_cache[dst + lane] = f2bf(k1 * co - k2 * si);
+    k_cache[dst + HALF + lane] = f2bf(k2 * co + k1 * si);
+    v_cache[dst + lane] = f2bf(v1);
+    v_cache[dst + HALF + lane] = f2bf(v2);
+  }
+  // the tile loop below reads this row back (other lanes of this wave): order the stores
+  // before those loads
+  __threadfence_block();
+  // ---- Q^T fragments: head col of the group, dims 32kk + 8grp .. +7 (kk < 2: first half,
+  // its RoPE partner is fragment kk + 2 of the same lane)
+  bf16x8 qf[KK];
+  if (col < G) {
+    const float* qp = ws + rowoff + (long)(kvh * G + col) * HD;
+#pragma unroll
+    for (int kp2 = 0; kp2 < KK / 2; ++kp2) {
+      const int d1 = 32 * kp2 + 8 * grp;
+      float x1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, x2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int s = 0; s < SPL; ++s) {
+        const float4* a = reinterpret_cast<const float4*>(qp + s * splitstride + d1);
+        const float4* c = reinterpret_cast<const float4*>(qp + s * splitstride + HALF + d1);
+        const float4 a0 = a[0], a1 = a[1], c0 = c[0], c1 = c[1];
+        x1[0] += a0.x; x1[1] += a0.y; x1[2] += a0.z; x1[3] += a0.w;
+        x1[4] += a1.x; x1[5] += a1.y; x1[6] += a1.z; x1[7] += a1.w;
+        x2[0] += c0.x; x2[1] += c0.y; x2[2] += c0.z; x2[3] += c0.w;
+        x2[4] += c1.x; x2[5] += c1.y; x2[6] += c1.z; x2[7] += c1.w;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float q1 = bf2f(f2bf(x1[j])), q2 = bf2f(f2bf(x2[j]));
+        const float co = cs[d1 + j], si = cs[HALF + d1 + j];
+        qf[kp2][j] = (__bf16)(q1 * co - q2 * si);
+        qf[kp2 + 2][j] = (__bf16)(q2 * co + q1 * si);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      uint4 z = make_uint4(0, 0, 0, 0);
+      qf[kk] = *reinterpret_cast<bf16x8*>(&z);
+    }
+  }
+  decode_attn_core<HD>(qf, vt, lane, b, kvh, 0, G, ctx, 0, ctx, out, k_cache, v_cache,
+                       block_tables, max_blocks, hq, hkv, block_size, scale_log2, 1, nullptr,
+                       nullptr);
 }
 
 // Software-pipelined variant: a wave walks a list of work units (item = (sequence, kv head,
@@ -536,6 +644,28 @@ extern "C" int dli_decode_attention(void* out, const void* q, int q_stride, cons
     else
       decode_reduce_kernel<64><<<blocks, 256, 0, st>>>((u16*)out, ws_o, ws_ml, B, hq, num_splits);
   }
+  DLI_RETURN_LAUNCH();
+}
+
+// Fused split-K QKV reduce + RoPE + KV-cache write + decode attention (one KV split, head
+// dim 128, RoPE models): ws = the QKV GEMM's fp32 slabs [splits, B, (hq + 2 hkv) * 128].
+extern "C" int dli_decode_attention_fused(void* out, const float* ws, int splits,
+                                          const int* positions, const int* slot_mapping,
+                                          const float* cos_sin, void* k_cache, void* v_cache,
+                                          const int* block_tables, int max_blocks,
+                                          const int* context_lens, int B, int hq, int hkv,
+                                          int hd, int block_size, float scale, hipStream_t st) {
+  if (B <= 0) return 0;
+  if (hd != 128 || hq % hkv || hq / hkv > 16 || block_size % 16 || (splits != 2 && splits != 4))
+    return (int)hipErrorInvalidValue;
+  const int N = (hq + 2 * hkv) * hd;
+  const float scale_log2 = scale * 1.4426950408889634f;
+  dim3 grid((int)(((long)B * hkv + DEC_WAVES - 1) / DEC_WAVES));
+#define DLI_DAF(S) decode_attn_fused_kernel<S><<<grid, 64 * DEC_WAVES, 0, st>>>(                \
+      (u16*)out, ws, N, positions, slot_mapping, cos_sin, (u16*)k_cache, (u16*)v_cache,      \
+      block_tables, max_blocks, context_lens, B, hq, hkv, block_size, scale_log2)
+  if (splits == 2) DLI_DAF(2); else DLI_DAF(4);
+#undef DLI_DAF
   DLI_RETURN_LAUNCH();
 }
 

@@ -7,6 +7,7 @@ All functions take/return torch tensors and launch on torch's current stream.
 from __future__ import annotations
 
 import math
+import os
 import time
 from typing import Optional
 
@@ -213,6 +214,37 @@ def linear_rope_cache(x, w, positions, slot_mapping, cos_sin, k_cache, v_cache, 
                  _p(slot_mapping), _p(cos_sin), _p(k_cache), _p(v_cache), hq, hkv, hd, bs,
                  int(use_rope), _st())
     return qkv
+
+
+def linear_rope_attention(x, w, positions, slot_mapping, cos_sin, k_cache, v_cache,
+                          block_tables, context_lens, max_context: int, hq, hkv, hd, scale):
+    """Decode step, one fused pass after the QKV GEMM: the split-K slabs are reduced, q and k
+    rotated, k/v written to the paged cache and attention computed by ONE kernel per layer
+    (``dli_decode_attention_fused``) instead of ``linear_rope_cache`` + ``decode_attention``.
+    Returns the attention output [B, hq*hd], or None where the fused kernel does not apply
+    (the caller then runs the two-kernel path): unsplit QKV plans, KV-split attention (short
+    batches / long contexts: its merge workspace is the GEMM's slab workspace), the
+    pipelined long-context kernel, head dim != 128. ``DLI_FUSED_ROPE_ATTN=0`` turns it off."""
+    if os.environ.get("DLI_FUSED_ROPE_ATTN", "1") != "1" or hd != 128 or k_cache is None:
+        return None
+    p = _splitk_plan(x, w)
+    if p is None or p.splits not in (2, 4):
+        return None
+    B, K = x.shape
+    if decode_num_splits(B, hkv, max_context) != 1:
+        return None
+    if -(-max_context // 32) * 32 >= 768 or os.environ.get("DLI_DECODE_PIPE") == "1":
+        return None                       # dli_decode_attention picks the pipelined kernel
+    Nn = w.shape[0]
+    ws = G.workspace(x.device, p.splits * B * Nn * 4)
+    _native_call("dli_gemm", _p(x), x.stride(0), _p(w), w.stride(-2), None, Nn, B, Nn, K,
+                 0, p.tile, p.splits, None, _p(ws), None, 1, _st())
+    out = torch.empty(B, hq * hd, dtype=x.dtype, device=x.device)
+    _native_call("dli_decode_attention_fused", _p(out), _p(ws), p.splits, _p(positions),
+                 _p(slot_mapping), _p(cos_sin), _p(k_cache), _p(v_cache), _p(block_tables),
+                 block_tables.stride(0), _p(context_lens), B, hq, hkv, hd, k_cache.shape[2],
+                 scale, _st())
+    return out
 
 
 def feed_ids(ids, src, feed):

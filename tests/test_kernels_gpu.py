@@ -253,6 +253,50 @@ def test_decode_attention_paged(gpu, hq, hkv, hd, bs, lens):
             ops.decode_pipelined(old)
 
 
+@pytest.mark.parametrize("splits", [2, 4])
+@pytest.mark.parametrize("hq,hkv", [(32, 8), (8, 1)])
+def test_fused_rope_attention(gpu, monkeypatch, hq, hkv, splits):
+    """dli_decode_attention_fused (split-K QKV reduce + RoPE + KV write + attention in one
+    kernel) == linear_rope_cache + decode_attention: the same cache bytes, the same output,
+    and the output matches the fp32 reference."""
+    hd, bs = 128, 16
+    lens = [1, 5, 33, 100, 200, 17]
+    B = len(lens)
+    nblk = sum(-(-n // bs) for n in lens) + 8
+    qkv_all, pos_all, slots_all, kc, vc, tables = _paged_setup(gpu, lens, hq, hkv, hd, bs, nblk)
+    cs = R.rope_cos_sin(2048, hd, 500000.0, device=gpu)
+    ops.rope_and_cache(qkv_all, pos_all, slots_all, cs, kc, vc, hq, hkv, hd)  # older tokens
+    last = torch.tensor(np.cumsum(lens) - 1, device=gpu, dtype=torch.long)
+    pos, slots = pos_all[last].contiguous(), slots_all[last].contiguous()
+    ctx = torch.tensor(lens, device=gpu, dtype=torch.int32)
+    K = 1024
+    N = (hq + 2 * hkv) * hd
+    x, w = rnd(B, K, dev=gpu), rnd(N, K, dev=gpu, scale=0.05)
+    scale = 1 / math.sqrt(hd)
+    G.set_plan(B, N, K, "splitk", G.GemmPlan("dli", 0, splits))
+    try:
+        kc1, vc1 = kc.clone(), vc.clone()
+        qkv = ops.linear_rope_cache(x, w, pos, slots, cs, kc1, vc1, hq, hkv, hd)
+        ref2 = ops.decode_attention(qkv, kc1, vc1, tables, ctx, max(lens), hq, hkv, hd, scale)
+        monkeypatch.setenv("DLI_FUSED_ROPE_ATTN", "1")
+        kc2, vc2 = kc.clone(), vc.clone()
+        out = ops.linear_rope_attention(x, w, pos, slots, cs, kc2, vc2, tables, ctx,
+                                        max(lens), hq, hkv, hd, scale)
+    finally:
+        G.clear_plans()
+    assert out is not None
+    torch.cuda.synchronize()
+    assert torch.equal(kc2, kc1) and torch.equal(vc2, vc1)
+    close(out, ref2, rtol=1e-2, atol=1e-2)
+    # fp32 reference of the whole chain
+    qkv_r = R.linear(x, w)
+    kc3, vc3 = kc.clone(), vc.clone()
+    R.rope_and_cache(qkv_r, pos, slots, cs, kc3, vc3, hq, hkv, hd)
+    q = qkv_r[:, : hq * hd].reshape(B, hq, hd)
+    ref = R.decode_attention(q, kc3, vc3, tables, ctx, scale).reshape(B, -1)
+    close(out, ref, rtol=2e-2, atol=2e-2)
+
+
 def test_sampling_greedy_and_support(gpu):
     torch.manual_seed(5)
     B, V = 64, 128256
