@@ -13,6 +13,9 @@
 //                                                with the transposing ds_read_b64_tr_b16, as
 //                                                in the prefill kernel)
 // With >1 split the per-split (m, l, O) go to a workspace merged by a second kernel.
+// decode_attn_fused_kernel (the decode-graph default) runs the same tile loop after a
+// prologue that replaces dli_splitk_rope_cache: the QKV GEMM's split-K slabs are reduced,
+// q/k rotated and k/v written to the paged cache inside the attention wave.
 //
 // Layouts: q rows of stride q_stride (the fused QKV buffer), k_cache and v_cache
 // [nblk,Hkv,bs,hd] (token-major: the per-step cache write is a contiguous row),
