@@ -84,3 +84,26 @@ def test_mixed_steps_other_families(model):
     eng = _engine(True, True, model=model)
     assert _run(eng, params) == want
     assert eng.stats.mixed_steps > 0
+
+
+def test_mixed_step_metadata_survives_the_wire():
+    """A mixed step crosses pipeline stages as packed metadata: the decode-row count rides
+    in header word 9 (both the generic and the native-decode packing paths)."""
+    import numpy as np
+
+    from distributed_llm_inferencing_amd.engine.batch import PREFILL, StepMeta
+    S, T = 3, 7
+    m = StepMeta(kind=PREFILL, seq_ids=[4, 9, 11], input_ids=np.arange(T, dtype=np.int32),
+                 positions=np.arange(T, dtype=np.int32), slot_mapping=np.arange(T, dtype=np.int32),
+                 seq_lens=np.array([1, 1, 5], np.int32), context_lens=np.array([9, 4, 5], np.int32),
+                 block_tables=np.array([[1, 2], [3, 0], [4, 0]], np.int32),
+                 temperature=np.full(S, 0.8, np.float32), top_k=np.full(S, 50, np.int32),
+                 top_p=np.full(S, 0.95, np.float32), seeds=np.arange(S, dtype=np.int64),
+                 microbatch=2, step_id=17, num_decode=2)
+    h, p = m.pack()
+    assert int(h[9]) == 2
+    u = StepMeta.unpack(h, p)
+    assert u.num_decode == 2 and u.kind == PREFILL and u.seq_ids == [4, 9, 11]
+    assert np.array_equal(u.block_tables, m.block_tables)
+    m.num_decode = 0
+    assert StepMeta.unpack(*m.pack()).num_decode == 0
