@@ -593,6 +593,15 @@ extern "C" int dli_decode_set_pipe(int v) {
   return old;
 }
 
+// the mode the next dli_decode_attention call applies (the env default resolved)
+extern "C" int dli_decode_get_pipe() {
+  if (g_decode_pipe < 0) {
+    const char* e = getenv("DLI_DECODE_PIPE");
+    g_decode_pipe = e ? atoi(e) : 2;
+  }
+  return g_decode_pipe;
+}
+
 extern "C" int dli_decode_attention(void* out, const void* q, int q_stride, const void* k_cache,
                                     const void* v_cache, const int* block_tables, int max_blocks,
                                     const int* context_lens, int B, int hq, int hkv, int hd,

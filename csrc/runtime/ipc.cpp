@@ -1,0 +1,348 @@
+// Device-memory mailbox transport between the processes of one node (hipIpc): the
+// pipeline / expert-parallel data plane without RCCL ("loopback transport
+// (same C++ interface): stage-ranks on one GPU exchange via device memcpy / IPC handles").
+// The reference has no data plane at all — its "shards" exchange nothing
+// (master/dashboard/views.py:318-355, worker/app.py:332-372).
+//
+// Every directed edge src -> dst owns one mailbox in dst's HBM plus two flag words that
+// work as binary semaphores: READY (in dst's flag page) and FREE (in src's page, initially
+// 1). A message goes
+//
+//   src stream: wait FREE == 1; FREE = 0; hipMemcpyAsync(mailbox <- payload); READY = 1
+//   dst stream: wait READY == 1; READY = 0; hipMemcpyAsync(target <- mailbox); FREE = 1
+//
+// (waits = hipStreamWaitValue64 Eq, stores = hipStreamWriteValue64; the copy is an xGMI peer
+// write on an 8-GPU node, a local D2D copy when the ranks share one GPU). No sequence number
+// lives on the host, so an exchange captured in a hipGraph is correct on every replay, and
+// eager and captured exchanges interleave freely. The sender runs at most one message ahead
+// per edge, which the anti-diagonal pipeline schedule never needs to exceed: every wait
+// depends on a strictly earlier tick, so it cannot deadlock.
+//
+// All of it is enqueued on the caller's stream (the stage's compute stream): the send is
+// ordered after the kernels that produced the payload and the receive before the kernels
+// that read the target, with no events, no side stream and no host wait. Matching is strictly
+// FIFO per edge, the same rule RCCL applies (tags are ignored), so a schedule that works
+// here has RCCL's ordering.
+//
+// Flag words live either in device memory (exported with the mailbox) or in a POSIX
+// shared-memory page registered with HIP ("host" flags): then the host can observe how far
+// every queue has got and ABORT a ring whose peer died by setting every flag it could be
+// waiting on (dli_ipc_abort), which a device-only wait could never be released from.
+//
+// C ABI (ctypes): 0 / >= 0 on success, negative hipError_t (or -1000 - reason) on failure.
+#include <fcntl.h>
+#include <hip/hip_runtime.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace {
+
+constexpr size_t kFlagStride = 16;   // words between flags (128 B: one flag per line)
+
+struct Edge {                        // one peer, both directions
+  // outbound (me -> peer)
+  uint8_t* peer_mailbox = nullptr;   // peer's mailbox for my messages (mapped)
+  uint64_t* peer_ready = nullptr;    // peer's READY word for me (mapped)
+  uint64_t* my_free = nullptr;       // my FREE word for this edge (peer sets it)
+  long long out_bytes = 0;           // mailbox capacity
+  // inbound (peer -> me)
+  uint8_t* my_mailbox = nullptr;
+  uint64_t* my_ready = nullptr;
+  uint64_t* peer_free = nullptr;     // the peer's FREE word for messages to me (mapped)
+  long long in_bytes = 0;
+};
+
+struct Endpoint {
+  int world = 0, rank = 0;
+  bool host_flags = false;
+  uint8_t* mailbox = nullptr;        // local, all inbound edges
+  size_t mailbox_bytes = 0;
+  uint64_t* flags = nullptr;         // local flag page (device or registered host memory)
+  uint64_t* flags_dev = nullptr;     // its device address
+  size_t flag_bytes = 0;
+  std::vector<long long> cap;        // mailbox bytes per edge [src * world + dst]
+  std::vector<Edge> edge;
+  std::vector<void*> opened;         // mapped peer allocations (device flags / mailboxes)
+  std::vector<uint64_t*> host_pages; // host flag mode: every rank's page, mapped here
+  std::string shm_prefix;
+  uint64_t sends = 0, recvs = 0, bytes_out = 0;
+};
+
+inline Endpoint* E(void* h) { return reinterpret_cast<Endpoint*>(h); }
+inline int herr(hipError_t e) { return e == hipSuccess ? 0 : -(int)e; }
+
+// flag page of rank r: READY[src] for every src, then FREE[dst] for every dst
+inline size_t ready_word(int src) { return (size_t)src * kFlagStride; }
+inline size_t free_word(const Endpoint* e, int dst) {
+  return ((size_t)e->world + dst) * kFlagStride;
+}
+inline size_t mailbox_off(const Endpoint* e, int dst, int src) {
+  size_t off = 0;
+  for (int s = 0; s < src; ++s) off += (size_t)e->cap[s * e->world + dst];
+  return off;
+}
+
+std::string page_name(const std::string& prefix, int r) {
+  return prefix + "_" + std::to_string(r);
+}
+
+uint64_t* map_host_page(const std::string& name, size_t bytes, bool create) {
+  int fd = shm_open(name.c_str(), create ? (O_CREAT | O_EXCL | O_RDWR) : O_RDWR, 0600);
+  if (fd < 0) return nullptr;
+  if (create && ftruncate(fd, (off_t)bytes) != 0) {
+    close(fd);
+    return nullptr;
+  }
+  void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) return nullptr;
+  if (hipHostRegister(p, bytes, hipHostRegisterMapped) != hipSuccess) {
+    munmap(p, bytes);
+    return nullptr;
+  }
+  return reinterpret_cast<uint64_t*>(p);
+}
+
+uint64_t* dev_addr(uint64_t* host) {
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, host, 0) != hipSuccess) return nullptr;
+  return reinterpret_cast<uint64_t*>(d);
+}
+
+void set_word(uint64_t* w, uint64_t v) {
+  reinterpret_cast<std::atomic<uint64_t>*>(w)->store(v, std::memory_order_release);
+}
+
+}  // namespace
+
+extern "C" {
+
+int dli_ipc_handle_bytes() { return (int)sizeof(hipIpcMemHandle_t); }
+
+// Allocate this rank's inbound mailboxes and flag page. cap: world x world matrix of mailbox
+// bytes (row = src, col = dst; 0 = no edge), identical on every rank. host_prefix: shm page
+// name prefix (rank r's page is "<prefix>_<r>"), or "" for device flags.
+void* dli_ipc_create(int world, int rank, const long long* cap, const char* host_prefix) {
+  if (world < 1 || rank < 0 || rank >= world) return nullptr;
+  auto* e = new Endpoint();
+  e->world = world;
+  e->rank = rank;
+  e->cap.assign(cap, cap + (size_t)world * world);
+  e->edge.resize(world);
+  e->host_flags = host_prefix != nullptr && host_prefix[0] != '\0';
+  for (int s = 0; s < world; ++s) e->mailbox_bytes += (size_t)e->cap[s * world + rank];
+  if (e->mailbox_bytes && hipMalloc(&e->mailbox, e->mailbox_bytes) != hipSuccess) {
+    delete e;
+    return nullptr;
+  }
+  e->flag_bytes = ((2 * (size_t)world * kFlagStride * 8 + 4095) / 4096) * 4096;
+  // FREE words start at 1 (every mailbox empty), READY words at 0
+  std::vector<uint64_t> init(e->flag_bytes / 8, 0);
+  for (int d = 0; d < world; ++d) init[free_word(e, d)] = 1;
+  if (e->host_flags) {
+    e->shm_prefix = host_prefix;
+    const std::string name = page_name(e->shm_prefix, rank);
+    shm_unlink(name.c_str());
+    uint64_t* p = map_host_page(name, e->flag_bytes, true);
+    if (p == nullptr) {
+      (void)hipFree(e->mailbox);
+      delete e;
+      return nullptr;
+    }
+    std::memcpy(p, init.data(), e->flag_bytes);
+    e->flags = p;
+    e->flags_dev = dev_addr(p);
+    e->host_pages.assign(world, nullptr);
+    e->host_pages[rank] = p;
+  } else {
+    if (hipMalloc(reinterpret_cast<void**>(&e->flags), e->flag_bytes) != hipSuccess ||
+        hipMemcpy(e->flags, init.data(), e->flag_bytes, hipMemcpyHostToDevice) != hipSuccess) {
+      (void)hipFree(e->mailbox);
+      delete e;
+      return nullptr;
+    }
+    e->flags_dev = e->flags;
+  }
+  (void)hipDeviceSynchronize();
+  return e;
+}
+
+// This rank's IPC handles into `out` (2 * dli_ipc_handle_bytes()): the mailbox (zeros if it
+// has none) and, in device-flag mode, the flag page (zeros in host-flag mode).
+int dli_ipc_handles(void* h, void* out) {
+  auto* e = E(h);
+  const size_t hb = sizeof(hipIpcMemHandle_t);
+  auto* o = reinterpret_cast<uint8_t*>(out);
+  std::memset(o, 0, 2 * hb);
+  if (e->mailbox) {
+    hipIpcMemHandle_t mh;
+    const int r = herr(hipIpcGetMemHandle(&mh, e->mailbox));
+    if (r) return r;
+    std::memcpy(o, &mh, hb);
+  }
+  if (!e->host_flags) {
+    hipIpcMemHandle_t fh;
+    const int r = herr(hipIpcGetMemHandle(&fh, e->flags));
+    if (r) return r;
+    std::memcpy(o + hb, &fh, hb);
+  }
+  return 0;
+}
+
+// Map every connected peer's mailbox + flags. handles: world * 2 * handle_bytes, rank-major,
+// as written by dli_ipc_handles on each rank.
+int dli_ipc_connect(void* h, const void* handles) {
+  auto* e = E(h);
+  const size_t hb = sizeof(hipIpcMemHandle_t);
+  const auto* base = reinterpret_cast<const uint8_t*>(handles);
+  const int W = e->world, me = e->rank;
+  for (int p = 0; p < W; ++p) {
+    if (p == me) continue;
+    const bool out = e->cap[me * W + p] > 0, in = e->cap[p * W + me] > 0;
+    if (!out && !in) continue;
+    uint8_t* pmail = nullptr;
+    uint64_t* pflags = nullptr;
+    if (out) {
+      hipIpcMemHandle_t mh;
+      std::memcpy(&mh, base + (size_t)p * 2 * hb, hb);
+      void* ptr = nullptr;
+      const int r = herr(hipIpcOpenMemHandle(&ptr, mh, hipIpcMemLazyEnablePeerAccess));
+      if (r) return r;
+      e->opened.push_back(ptr);
+      pmail = reinterpret_cast<uint8_t*>(ptr);
+    }
+    if (e->host_flags) {
+      uint64_t* hp = map_host_page(page_name(e->shm_prefix, p), e->flag_bytes, false);
+      if (hp == nullptr) return -1001;
+      e->host_pages[p] = hp;
+      pflags = dev_addr(hp);
+      if (pflags == nullptr) return -1002;
+    } else {
+      hipIpcMemHandle_t fh;
+      std::memcpy(&fh, base + (size_t)p * 2 * hb + hb, hb);
+      void* ptr = nullptr;
+      const int r = herr(hipIpcOpenMemHandle(&ptr, fh, hipIpcMemLazyEnablePeerAccess));
+      if (r) return r;
+      e->opened.push_back(ptr);
+      pflags = reinterpret_cast<uint64_t*>(ptr);
+    }
+    Edge& g = e->edge[p];
+    if (out) {
+      g.out_bytes = e->cap[me * W + p];
+      g.peer_mailbox = pmail + mailbox_off(e, p, me);
+      g.peer_ready = pflags + ready_word(me);
+      g.my_free = e->flags_dev + free_word(e, p);
+    }
+    if (in) {
+      g.in_bytes = e->cap[p * W + me];
+      g.my_mailbox = e->mailbox + mailbox_off(e, me, p);
+      g.my_ready = e->flags_dev + ready_word(p);
+      g.peer_free = pflags + free_word(e, me);
+    }
+  }
+  return 0;
+}
+
+// One exchange, enqueued on `stream`: every send, then every receive (see the protocol at
+// the top). A message larger than its edge's mailbox is refused (-1003) before anything is
+// enqueued; a zero-byte message still hands the mailbox over once.
+int dli_ipc_exchange(void* h, void* stream, int n_send, void* const* send_ptrs,
+                     const long long* send_bytes, const int* send_peers, int n_recv,
+                     void* const* recv_ptrs, const long long* recv_bytes,
+                     const int* recv_peers) {
+  auto* e = E(h);
+  auto s = (hipStream_t)stream;
+  for (int i = 0; i < n_send; ++i) {
+    const Edge& g = e->edge[send_peers[i]];
+    if (g.peer_ready == nullptr || send_bytes[i] > g.out_bytes) return -1003;
+  }
+  for (int i = 0; i < n_recv; ++i) {
+    const Edge& g = e->edge[recv_peers[i]];
+    if (g.my_ready == nullptr || recv_bytes[i] > g.in_bytes) return -1003;
+  }
+  int r = 0;
+  for (int i = 0; i < n_send && r == 0; ++i) {
+    const Edge& g = e->edge[send_peers[i]];
+    r = herr(hipStreamWaitValue64(s, g.my_free, 1, hipStreamWaitValueEq));
+    if (!r) r = herr(hipStreamWriteValue64(s, g.my_free, 0, 0));
+    if (!r && send_bytes[i] > 0)
+      r = herr(hipMemcpyAsync(g.peer_mailbox, send_ptrs[i], (size_t)send_bytes[i],
+                              hipMemcpyDeviceToDevice, s));
+    if (!r) r = herr(hipStreamWriteValue64(s, g.peer_ready, 1, 0));
+    e->sends++;
+    e->bytes_out += (uint64_t)send_bytes[i];
+  }
+  for (int i = 0; i < n_recv && r == 0; ++i) {
+    const Edge& g = e->edge[recv_peers[i]];
+    r = herr(hipStreamWaitValue64(s, g.my_ready, 1, hipStreamWaitValueEq));
+    if (!r) r = herr(hipStreamWriteValue64(s, g.my_ready, 0, 0));
+    if (!r && recv_bytes[i] > 0)
+      r = herr(hipMemcpyAsync(recv_ptrs[i], g.my_mailbox, (size_t)recv_bytes[i],
+                              hipMemcpyDeviceToDevice, s));
+    if (!r) r = herr(hipStreamWriteValue64(s, g.peer_free, 1, 0));
+    e->recvs++;
+  }
+  return r;
+}
+
+// Host flag mode: 1 when a message from `peer` sits in my mailbox, not yet taken by my queue
+// (a host-side progress probe); -1 in device-flag mode.
+long long dli_ipc_pending(void* h, int peer) {
+  auto* e = E(h);
+  if (!e->host_flags) return -1;
+  return (long long)reinterpret_cast<std::atomic<uint64_t>*>(e->flags + ready_word(peer))
+      ->load(std::memory_order_acquire);
+}
+
+// Release whatever this rank's queue waits on (a dead peer): set every READY and FREE word
+// of this rank to 1. A queue resets a word after each wait, so a caller draining a stream
+// repeats this until the stream is idle. Host flags: CPU stores. Device flags: a blocking
+// hipMemcpy, which can queue behind the blocked stream on a shared hardware queue (host
+// flags are the mode that can always abort).
+int dli_ipc_abort(void* h) {
+  auto* e = E(h);
+  const size_t n = 2 * (size_t)e->world;
+  if (e->host_flags) {
+    for (size_t i = 0; i < n; ++i) set_word(e->flags + i * kFlagStride, 1);
+    return 0;
+  }
+  std::vector<uint64_t> v(e->flag_bytes / 8, 0);
+  for (size_t i = 0; i < n; ++i) v[i * kFlagStride] = 1;
+  return herr(hipMemcpy(e->flags, v.data(), e->flag_bytes, hipMemcpyHostToDevice));
+}
+
+void dli_ipc_stats(void* h, long long* out3) {
+  auto* e = E(h);
+  out3[0] = (long long)e->sends;
+  out3[1] = (long long)e->recvs;
+  out3[2] = (long long)e->bytes_out;
+}
+
+int dli_ipc_host_flags(void* h) { return E(h)->host_flags ? 1 : 0; }
+
+void dli_ipc_destroy(void* h) {
+  auto* e = E(h);
+  if (e == nullptr) return;
+  for (void* p : e->opened) (void)hipIpcCloseMemHandle(p);
+  if (e->host_flags) {
+    for (auto* p : e->host_pages) {
+      if (p == nullptr) continue;
+      (void)hipHostUnregister(p);
+      munmap(p, e->flag_bytes);
+    }
+    shm_unlink(page_name(e->shm_prefix, e->rank).c_str());
+  } else if (e->flags) {
+    (void)hipFree(e->flags);
+  }
+  if (e->mailbox) (void)hipFree(e->mailbox);
+  delete e;
+}
+
+}  // extern "C"

@@ -209,10 +209,11 @@ class Scheduler:
         # sequences' decode rows too (one token each, ahead of the prompt rows), so admitting
         # prompts or prefilling a chunk no longer stalls the running sequences for a step and
         # their rows ride on the prefill's (compute-bound) GEMMs instead of costing a separate
-        # weight-streaming decode step. Single-stage engines only (the pipeline wire format
-        # has no decode/prefill split).
+        # weight-streaming decode step. Pipelines use them too: the decode-row count crosses
+        # the stages in header word 9 of the packed step metadata (StepMeta.pack).
         self.mixed_steps = bool(mixed_steps)
         self.num_mixed = 0
+        self.num_preempted = 0
         self._next_id = 0
         self._step = 0
         self._deadlines = 0
@@ -314,6 +315,8 @@ class Scheduler:
         victim.state = SeqState.WAITING
         victim.num_prefilled = 0
         victim.num_preemptions += 1
+        victim.preempt_step = self._step
+        self.num_preempted += 1
         self.waiting.appendleft(victim)
         return True
 
@@ -342,8 +345,11 @@ class Scheduler:
         if self.mixed_steps and self.running[mb] and (self.waiting or self.prefilling[mb]):
             # the decode rows are scheduled first, against the sequences running before this
             # step's admissions (a prompt finishing its prefill here has no token to feed yet)
+            npre = self.num_preempted
             dec = self._decode(mb, inflight, allow_native=False)
-            pre = self._try_prefill(mb, mixed=True)
+            # a sequence the decode half just preempted may still be in the in-flight step:
+            # it is not re-admitted by this step's prefill half (it waits one step)
+            pre = self._try_prefill(mb, mixed=True) if self.num_preempted == npre else None
             if pre is None or dec is None:
                 return dec if pre is None else pre
             return self._merge(dec, pre)
@@ -751,6 +757,8 @@ class Scheduler:
             seq = self.seqs.get(sid)
             if seq is None or seq.state != SeqState.RUNNING or (mask is not None and not mask[i]):
                 continue
+            if meta.step_id < seq.preempt_step:
+                continue        # scheduled before the sequence was preempted: a stale token
             touched.add(seq.microbatch)
             t = int(tokens[i])
             seq.output_ids.append(t)

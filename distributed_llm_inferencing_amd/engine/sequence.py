@@ -60,6 +60,7 @@ class Sequence:
     finish_reason: Optional[str] = None
     seed: int = 0
     num_preemptions: int = 0
+    preempt_step: int = -1      # scheduler step id of the last preemption
     num_prefilled: int = 0  # tokens of all_ids() whose KV a scheduled prefill chunk writes
 
     @property

@@ -233,7 +233,8 @@ def linear_rope_attention(x, w, positions, slot_mapping, cos_sin, k_cache, v_cac
     B, K = x.shape
     if decode_num_splits(B, hkv, max_context) != 1:
         return None
-    if -(-max_context // 32) * 32 >= 768 or os.environ.get("DLI_DECODE_PIPE") == "1":
+    mode = int(N.require_native().dli_decode_get_pipe())
+    if mode == 1 or (mode == 2 and -(-max_context // 32) * 32 >= 768):
         return None                       # dli_decode_attention picks the pipelined kernel
     Nn = w.shape[0]
     ws = G.workspace(x.device, p.splits * B * Nn * 4)

@@ -293,7 +293,12 @@ def init_distributed(backend: Optional[str] = None, device: Optional[torch.devic
     (``worker/service.PipelineService``); the master's failure detector routes new requests
     to the remaining replicas."""
     if dist.is_initialized():
-        return dist.get_rank(), dist.get_world_size()
+        r, w = dist.get_rank(), dist.get_world_size()
+        if (rank is not None and int(rank) != r) or (world_size is not None
+                                                     and int(world_size) != w):
+            raise RuntimeError(f"a process group (rank {r} of {w}) already exists; asked for "
+                               f"rank {rank} of {world_size}: destroy it first")
+        return r, w
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29511")
     if backend is None:

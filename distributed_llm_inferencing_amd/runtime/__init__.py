@@ -78,6 +78,16 @@ _SIGS = {
     "dli_comm_init": ([_P, _P, _I, _I], _I),
     "dli_comm_destroy": ([_P], _I),
     "dli_comm_exchange": ([_P, _P, _I, _P, _P, _P, _I, _P, _P, _P], _I),
+    "dli_ipc_handle_bytes": ([], _I),
+    "dli_ipc_create": ([_I, _I, _P, ctypes.c_char_p], _P),
+    "dli_ipc_handles": ([_P, _P], _I),
+    "dli_ipc_connect": ([_P, _P], _I),
+    "dli_ipc_exchange": ([_P, _P, _I, _P, _P, _P, _I, _P, _P, _P], _I),
+    "dli_ipc_pending": ([_P, _I], _LL),
+    "dli_ipc_abort": ([_P], _I),
+    "dli_ipc_stats": ([_P, _P], None),
+    "dli_ipc_host_flags": ([_P], _I),
+    "dli_ipc_destroy": ([_P], None),
 }
 
 
@@ -494,6 +504,89 @@ class RcclComm:
         if self._h is not None:
             lib().dli_comm_destroy(self._h)
             self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+def _pack_io(items):
+    n = len(items)
+    ptrs = (ctypes.c_void_p * max(n, 1))(*[t.data_ptr() for t, _ in items])
+    nbytes = (ctypes.c_longlong * max(n, 1))(*[t.numel() * t.element_size() for t, _ in items])
+    peers = (ctypes.c_int * max(n, 1))(*[int(p) for _, p in items])
+    return n, ptrs, nbytes, peers
+
+
+class IpcEndpoint:
+    """Device-memory mailbox transport of one rank (``csrc/runtime/ipc.cpp``): one mailbox
+    per directed edge in the receiver's HBM, filled by a stream-ordered copy and handed over
+    by ``hipStreamWriteValue64`` / ``hipStreamWaitValue64`` binary semaphores (no host-side
+    sequence numbers, so captured exchanges replay correctly). FIFO per edge (RCCL's
+    matching rule), everything enqueued on the caller's stream.
+
+    Setup is three steps so the caller can move the handles over any side channel:
+    ``ep = IpcEndpoint(world, rank, cap)``; gather ``ep.handles()`` from every rank;
+    ``ep.connect(all_handles)``. ``cap[src][dst]`` = mailbox bytes of edge src -> dst
+    (0 = no edge), the same matrix on every rank. ``host_prefix``: keep the flag words in
+    POSIX shared-memory pages (host-visible progress; ``abort()`` releases a dead peer's
+    waits)."""
+
+    def __init__(self, world: int, rank: int, cap, host_prefix: str = ""):
+        L = lib()
+        m = np.ascontiguousarray(np.asarray(cap, dtype=np.int64).reshape(world, world))
+        self.cap = m
+        self._h = L.dli_ipc_create(int(world), int(rank), _np_ptr(m), host_prefix.encode())
+        if not self._h:
+            raise RuntimeError("IPC endpoint: allocation failed")
+        self.world, self.rank = world, rank
+        self.host_flags = bool(L.dli_ipc_host_flags(self._h))
+
+    def handles(self) -> bytes:
+        hb = lib().dli_ipc_handle_bytes()
+        buf = ctypes.create_string_buffer(2 * hb)
+        r = lib().dli_ipc_handles(self._h, buf)
+        if r < 0:
+            raise RuntimeError(f"hipIpcGetMemHandle failed (hipError {-r})")
+        return buf.raw
+
+    def connect(self, all_handles: Sequence[bytes]) -> None:
+        blob = b"".join(bytes(h) for h in all_handles)
+        buf = ctypes.create_string_buffer(blob, len(blob))
+        r = lib().dli_ipc_connect(self._h, buf)
+        if r != 0:
+            raise RuntimeError(f"IPC connect failed ({r}: hipIpcOpenMemHandle / shm map)")
+
+    def exchange(self, sends, recvs, stream: int) -> None:
+        """``sends`` / ``recvs`` = [(device tensor, peer)], enqueued on ``stream``."""
+        ns, sp, sb, spe = _pack_io(sends)
+        nr, rp, rb, rpe = _pack_io(recvs)
+        r = lib().dli_ipc_exchange(self._h, ctypes.c_void_p(stream), ns, sp, sb, spe, nr, rp,
+                                   rb, rpe)
+        if r != 0:
+            raise RuntimeError(f"IPC exchange failed ({r})" + (
+                ": message larger than the edge's slot" if r == -1003 else ""))
+
+    def pending(self, peer: int) -> int:
+        """Host-flag mode: 1 while a message from ``peer`` waits in this rank's mailbox."""
+        return int(lib().dli_ipc_pending(self._h, int(peer)))
+
+    def abort(self) -> None:
+        r = lib().dli_ipc_abort(self._h)
+        if r != 0:
+            raise RuntimeError(f"IPC abort failed ({r})")
+
+    def stats(self) -> Dict[str, int]:
+        out = (ctypes.c_longlong * 3)()
+        lib().dli_ipc_stats(self._h, out)
+        return {"sends": out[0], "recvs": out[1], "bytes_out": out[2]}
+
+    def close(self) -> None:
+        h, self._h = getattr(self, "_h", None), None
+        if h and _lib is not None:
+            _lib.dli_ipc_destroy(h)
 
     def __del__(self):
         try:

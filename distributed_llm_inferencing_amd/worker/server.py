@@ -78,6 +78,14 @@ class WorkerState:
                                   max_model_len=2048 if gpu else 512,
                                   num_blocks=None if gpu else 512)
         self.engine_kwargs.update(engine_kwargs or {})
+        if gpu and self.engine_kwargs.get("num_blocks") is None:
+            # a worker may serve several models (/load_model per name): each engine's KV
+            # pool is capped at max_batch x max_model_len tokens (DLI_KV_MAX_TOKENS
+            # overrides) so the first model cannot take the HBM the next one's weights need
+            kw = self.engine_kwargs
+            kw.setdefault("max_kv_tokens",
+                          int(os.environ.get("DLI_KV_MAX_TOKENS", "0") or 0)
+                          or kw["max_batch"] * kw["max_model_len"])
         self.services: Dict[str, object] = {}           # model_name -> service
         self.tokenizers: Dict[str, object] = {}
         self.shards: Dict[str, Dict[int, dict]] = {}     # model -> shard_id -> record
@@ -188,6 +196,7 @@ class WorkerState:
         from ..parallel.transport import init_distributed
         from .service import PipelineService
         rec = self.pipeline
+        eng = None
         try:
             cuda = self.device.type == "cuda"
             if cuda:
@@ -225,6 +234,17 @@ class WorkerState:
         except BaseException as e:  # noqa: BLE001 — reported by /health
             log.error("pipeline join (%s stage %d/%d) failed: %s", name, rank, world, e)
             rec["state"], rec["error"] = "failed", str(e)
+            # a retry with a new spec must rendezvous afresh, not reuse this group
+            eng = eng or self._pipe_engine
+            self._pipe_engine = None
+            try:
+                if eng is not None:
+                    eng.channel.close()
+                import torch.distributed as dist
+                if dist.is_initialized():
+                    dist.destroy_process_group()
+            except Exception as e2:  # noqa: BLE001
+                log.warning("pipeline teardown after a failed join: %s", e2)
 
     def _leave_pipeline(self):
         """Rank 0: unload of the pipeline model shuts the whole ring down."""

@@ -120,6 +120,7 @@ class PipelineService:
         self._lock = threading.Lock()
         self.error: Optional[BaseException] = None
         self._futs = {}
+        self._carry = None               # the request that started a session, admitted first
         self.sessions = 0
         self._t = threading.Thread(target=self._run, name=f"dli-pipe-{name}", daemon=True)
         self._t.start()
@@ -136,6 +137,9 @@ class PipelineService:
         return fut
 
     def _fail_pending(self):
+        if self._carry is not None:
+            self._carry[3].set_exception(RuntimeError(f"pipeline {self.name} failed: {self.error}"))
+            self._carry = None
         while True:
             try:
                 _rid, _p, _s, fut = self._inbox.get_nowait()
@@ -147,13 +151,17 @@ class PipelineService:
         return self.submit(prompt, params).result(timeout=timeout)
 
     def _admit(self) -> int:
-        """Tick boundary: move every queued request into the running head scheduler."""
+        """Tick boundary: move every queued request into the running head scheduler, in
+        arrival order (the request that woke the session first)."""
         n = 0
         while True:
-            try:
-                rid, prompt, params, fut = self._inbox.get_nowait()
-            except queue.Empty:
-                return n
+            if self._carry is not None:
+                (rid, prompt, params, fut), self._carry = self._carry, None
+            else:
+                try:
+                    rid, prompt, params, fut = self._inbox.get_nowait()
+                except queue.Empty:
+                    return n
             try:
                 self.engine.add_request(prompt, params, request_id=rid)
                 self._futs[rid] = fut
@@ -171,10 +179,9 @@ class PipelineService:
         head = self.engine.head
         while not self._stop.is_set():
             try:
-                item = self._inbox.get(timeout=0.05)
+                self._carry = self._inbox.get(timeout=0.05)   # admitted by the first tick
             except queue.Empty:
                 continue
-            self._inbox.put(item)            # admitted by the session's first tick
             try:
                 # continuous admission: requests that arrive while the ring is running join
                 # it at the next tick; each finished request is answered the tick it finishes

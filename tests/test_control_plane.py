@@ -347,21 +347,32 @@ def test_loadgen_end_to_end(tmp_path, master):
     """Load generator through the public master API: concurrent clients, every request
     completes; the worker batches them (continuous batching across HTTP requests)."""
     from distributed_llm_inferencing_amd.loadgen import LoadGen
+    # all 6 clients' requests in flight at once (one dispatcher slot each), so the worker
+    # batches them into shared steps; polling every 0.1 s (the reference UI polls every 2 s)
+    # keeps the pollers from competing with the engine thread for the GIL on a loaded host.
+    # Root cause of the earlier flake: 2 dispatcher slots serialised the 12 requests into 6
+    # rounds of a 2-row batch, which took > 120 s under CPU contention.
+    master.extensions["dli"].shutdown()
+    master = create_master_app(settings(tmp_path, master_db=str(tmp_path / "lg.sqlite3")),
+                               start_background=True, dispatch_workers=6, health_interval=0.5)
     w = Server(create_worker_app(settings(tmp_path), device="cpu", engine_kwargs=SMALL))
     ms = Server(master)
     try:
         requests.post(f"{ms.url}/api/nodes/add/", data={"hostname": "cpu0",
                                                        "ip_address": "127.0.0.1",
                                                        "port": w.port}, timeout=10)
-        lg = LoadGen(ms.url, "gpt2-tiny", poll_s=0.02, timeout_s=120)
+        lg = LoadGen(ms.url, "gpt2-tiny", poll_s=0.1, timeout_s=240)
         wall = lg.closed_loop([f"hello {i}" for i in range(12)], concurrency=6)
         rep = lg.report(wall)
-        assert rep["completed"] == 12 and rep["failed"] == 0
+        assert rep["completed"] == 12 and rep["failed"] == 0, (rep, [
+            master.extensions["dli"].store.get_request(r["id"]) for r in lg.results
+            if r["status"] != "completed"][:3])
         assert rep["p50_latency_s"] <= rep["p99_latency_s"]
         assert rep["requests_per_s"] > 0
     finally:
         ms.close()
         w.close()
+        master.extensions["dli"].shutdown()
 
 
 def test_worker_health_reports_failed_pipeline(worker):

@@ -107,3 +107,20 @@ def test_mixed_step_metadata_survives_the_wire():
     assert np.array_equal(u.block_tables, m.block_tables)
     m.num_decode = 0
     assert StepMeta.unpack(*m.pack()).num_decode == 0
+
+
+@pytest.mark.parametrize("lookahead", [True, False])
+def test_mixed_steps_under_preemption(lookahead):
+    """KV pressure with mixed steps + lookahead + a non-empty waiting queue: a sequence the
+    decode half of a mixed step preempts must not be re-admitted by that same step's prefill
+    half (its in-flight token would then be applied twice). Outputs must equal an
+    unconstrained run's."""
+    n = sum(len(w) for w in WAVES)
+    params = [SamplingParams(max_length=60, do_sample=False, ignore_eos=True) for _ in range(n)]
+    want = _run(_engine(False, False), params)
+    eng = LLMEngine("llama-tiny", device="cpu", dtype=torch.float32, max_batch=8,
+                    max_model_len=128, num_blocks=14, block_size=16, max_prefill_tokens=4096,
+                    mixed_steps=True, lookahead=lookahead)
+    got = _run(eng, params)
+    assert eng.scheduler.num_preempted > 0 and eng.stats.mixed_steps > 0
+    assert got == want
