@@ -48,6 +48,17 @@ def _baseline_value():
     return None
 
 
+def _like_for_like_value():
+    """HF ``generate`` on 512 prompts per call on MI355X (scripts/bench_reference.py --batch
+    512): the batched comparator for the batch-512 row (``vs_baseline`` divides by the
+    reference's own strategy, batch 1 serialised)."""
+    p = ROOT / "profiles" / "r2_s4" / "hf_generate_b512.json"
+    try:
+        return float(json.loads(p.read_text())["value"])
+    except Exception:  # noqa: BLE001
+        return None
+
+
 def make_prompts(n, prompt_len, vocab, seed):
     rng = np.random.default_rng(seed)
     lo, hi = (1000, vocab - 1000) if vocab > 4000 else (3, vocab - 1)
@@ -184,6 +195,8 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": round(tok_s / base, 3) if base else None,
+        "baseline_note": "vs_baseline = value / the reference's strategy measured on MI355X "
+                         "(HF generate, batch 1, serialised: profiles/reference_strategy.json)",
         "dtype": "bf16",
         "data": "synthetic prompts, random-init weights",
         "p50_latency_s": round(p50, 4) if p50 is not None else None,
@@ -192,6 +205,10 @@ def main():
                    "parallelism": res["parallelism"],
                    "sampling": "T=0.8 top_k=50 top_p=0.95"},
     }
+    lfl = _like_for_like_value()
+    if lfl and a.model == "llama3-8b":
+        # like-for-like batch: HF generate over 512 prompts per call on the same GPU
+        line["vs_hf_batched_generate"] = round(tok_s / lfl, 3)
     print(json.dumps(line), flush=True)
 
 

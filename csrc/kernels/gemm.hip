@@ -47,6 +47,28 @@ __device__ __forceinline__ void store_pair_or_one(void* C, int ldc, int row, int
   }
 }
 
+// fp32 split-K partial stores: 0 plain (the line stays dirty in the XCD's L2 and is written
+// back at the kernel boundary, MI355X_MICROARCH.md price row 'boundary'), 1 nontemporal,
+// 2 sc1 (write-through: the bytes leave L2 while the GEMM still computes), 3 sc0 sc1.
+__device__ int g_slab_store = 0;
+extern "C" int dli_gemm_set_slab_store(int mode) {
+  int old = 0;
+  (void)hipMemcpyFromSymbol(&old, HIP_SYMBOL(g_slab_store), sizeof(int));
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_slab_store), &mode, sizeof(int));
+  return old;
+}
+__device__ __forceinline__ void slab_store(float* p, float v, int mode) {
+  if (mode == 1) {
+    __builtin_nontemporal_store(v, p);
+  } else if (mode == 2) {
+    asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+  } else if (mode == 3) {
+    asm volatile("global_store_dword %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+  } else {
+    *p = v;
+  }
+}
+
 // s_waitcnt vmcnt(N) with expcnt/lgkmcnt left at their maxima (gfx9 encoding)
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -216,6 +238,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(
   const bool split = gridDim.y > 1;
   if (split) {
     float* slab = ws + (long)ks * M * N;
+    const int sm = g_slab_store;
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -225,7 +248,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
           const int col = n0 + wn * TN + 16 * j + fr;
-          if (col < N) slab[(long)(row0 + row) * N + col] = acc[i][j][r];
+          if (col < N) slab_store(slab + (long)(row0 + row) * N + col, acc[i][j][r], sm);
         }
       }
     return;
@@ -536,6 +559,7 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(
   const int wr0 = m0 + 128 * g, wc0 = n0 + 64 * gw;
   if (gridDim.y > 1) {
     float* slab = ws + (long)ks * M * N;
+    const int sm = g_slab_store;
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -545,7 +569,7 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int col = wc0 + 16 * j + fr;
-          if (col < N) slab[(long)(row0 + row) * N + col] = acc[i][j][r];
+          if (col < N) slab_store(slab + (long)(row0 + row) * N + col, acc[i][j][r], sm);
         }
       }
     return;
@@ -774,6 +798,7 @@ __global__ void __launch_bounds__(512) gemm8p224_kernel(
   const int wr0 = m0 + 128 * g + 64 * wm, wc0 = n0 + 112 * wn;
   if (gridDim.y > 1) {
     float* slab = ws + (long)ks * M * N;
+    const int sm = g_slab_store;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -783,7 +808,7 @@ __global__ void __launch_bounds__(512) gemm8p224_kernel(
 #pragma unroll
         for (int j = 0; j < 7; ++j) {
           const int col = wc0 + 16 * j + fr;
-          if (col < N) slab[(long)(row0 + row) * N + col] = acc[i][j][r];
+          if (col < N) slab_store(slab + (long)(row0 + row) * N + col, acc[i][j][r], sm);
         }
       }
     return;

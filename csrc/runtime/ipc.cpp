@@ -37,7 +37,9 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <chrono>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -59,9 +61,35 @@ struct Edge {                        // one peer, both directions
   long long in_bytes = 0;
 };
 
+// Payload copies: a plain vectorised copy kernel on the caller's stream (default) or
+// hipMemcpyAsync (DLI_IPC_COPY=memcpy). The kernel keeps a hop to one launch on the compute
+// queue; hipMemcpyAsync between IPC-mapped buffers may be routed to an SDMA engine, measured
+// at ~40 GB/s for 4 MB messages on one MI355X (profiles/r3/ipc_probe_*.jsonl).
+__global__ void __launch_bounds__(256) ipc_copy_kernel(uint4* __restrict__ dst,
+                                                       const uint4* __restrict__ src, long n16,
+                                                       uint32_t* __restrict__ dtail,
+                                                       const uint32_t* __restrict__ stail,
+                                                       int ntail) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride],
+                d = src[i + 3 * stride];
+    dst[i] = a;
+    dst[i + stride] = b;
+    dst[i + 2 * stride] = c;
+    dst[i + 3 * stride] = d;
+  }
+  for (; i < n16; i += stride) dst[i] = src[i];
+  if (blockIdx.x == 0 && (int)threadIdx.x < ntail) dtail[threadIdx.x] = stail[threadIdx.x];
+}
+
 struct Endpoint {
   int world = 0, rank = 0;
   bool host_flags = false;
+  bool copy_kernel = true;
+  hipStream_t abort_stream = nullptr; // device-flag abort: its own (SDMA) queue
+  uint64_t* abort_src = nullptr;      // pinned page of FREE/READY = 1 patterns
   uint8_t* mailbox = nullptr;        // local, all inbound edges
   size_t mailbox_bytes = 0;
   uint64_t* flags = nullptr;         // local flag page (device or registered host memory)
@@ -120,6 +148,22 @@ void set_word(uint64_t* w, uint64_t v) {
   reinterpret_cast<std::atomic<uint64_t>*>(w)->store(v, std::memory_order_release);
 }
 
+int copy_async(const Endpoint* e, void* dst, const void* src, long long bytes, hipStream_t s) {
+  if (bytes <= 0) return 0;
+  if (!e->copy_kernel || ((uintptr_t)dst | (uintptr_t)src | (uintptr_t)bytes) % 4)
+    return herr(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToDevice, s));
+  const long n16 = bytes / 16;
+  const int ntail = (int)((bytes % 16) / 4);
+  long blocks = (n16 + 4 * 256 - 1) / (4 * 256);
+  if (blocks < 1) blocks = 1;
+  if (blocks > 2048) blocks = 2048;
+  ipc_copy_kernel<<<dim3((unsigned)blocks), dim3(256), 0, s>>>(
+      reinterpret_cast<uint4*>(dst), reinterpret_cast<const uint4*>(src), n16,
+      reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(dst) + n16 * 16),
+      reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(src) + n16 * 16), ntail);
+  return herr(hipGetLastError());
+}
+
 }  // namespace
 
 extern "C" {
@@ -137,6 +181,8 @@ void* dli_ipc_create(int world, int rank, const long long* cap, const char* host
   e->cap.assign(cap, cap + (size_t)world * world);
   e->edge.resize(world);
   e->host_flags = host_prefix != nullptr && host_prefix[0] != '\0';
+  const char* cm = getenv("DLI_IPC_COPY");
+  e->copy_kernel = !(cm != nullptr && std::string(cm) == "memcpy");
   for (int s = 0; s < world; ++s) e->mailbox_bytes += (size_t)e->cap[s * world + rank];
   if (e->mailbox_bytes && hipMalloc(&e->mailbox, e->mailbox_bytes) != hipSuccess) {
     delete e;
@@ -169,6 +215,15 @@ void* dli_ipc_create(int world, int rank, const long long* cap, const char* host
       return nullptr;
     }
     e->flags_dev = e->flags;
+    if (hipStreamCreateWithFlags(&e->abort_stream, hipStreamNonBlocking) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void**>(&e->abort_src), e->flag_bytes,
+                      hipHostMallocDefault) != hipSuccess) {
+      e->abort_stream = nullptr;
+      e->abort_src = nullptr;
+    } else {
+      std::memset(e->abort_src, 0, e->flag_bytes);
+      for (size_t i = 0; i < 2 * (size_t)world; ++i) e->abort_src[i * kFlagStride] = 1;
+    }
   }
   (void)hipDeviceSynchronize();
   return e;
@@ -272,9 +327,7 @@ int dli_ipc_exchange(void* h, void* stream, int n_send, void* const* send_ptrs,
     const Edge& g = e->edge[send_peers[i]];
     r = herr(hipStreamWaitValue64(s, g.my_free, 1, hipStreamWaitValueEq));
     if (!r) r = herr(hipStreamWriteValue64(s, g.my_free, 0, 0));
-    if (!r && send_bytes[i] > 0)
-      r = herr(hipMemcpyAsync(g.peer_mailbox, send_ptrs[i], (size_t)send_bytes[i],
-                              hipMemcpyDeviceToDevice, s));
+    if (!r) r = copy_async(e, g.peer_mailbox, send_ptrs[i], send_bytes[i], s);
     if (!r) r = herr(hipStreamWriteValue64(s, g.peer_ready, 1, 0));
     e->sends++;
     e->bytes_out += (uint64_t)send_bytes[i];
@@ -283,9 +336,7 @@ int dli_ipc_exchange(void* h, void* stream, int n_send, void* const* send_ptrs,
     const Edge& g = e->edge[recv_peers[i]];
     r = herr(hipStreamWaitValue64(s, g.my_ready, 1, hipStreamWaitValueEq));
     if (!r) r = herr(hipStreamWriteValue64(s, g.my_ready, 0, 0));
-    if (!r && recv_bytes[i] > 0)
-      r = herr(hipMemcpyAsync(recv_ptrs[i], g.my_mailbox, (size_t)recv_bytes[i],
-                              hipMemcpyDeviceToDevice, s));
+    if (!r) r = copy_async(e, recv_ptrs[i], g.my_mailbox, recv_bytes[i], s);
     if (!r) r = herr(hipStreamWriteValue64(s, g.peer_free, 1, 0));
     e->recvs++;
   }
@@ -303,19 +354,27 @@ long long dli_ipc_pending(void* h, int peer) {
 
 // Release whatever this rank's queue waits on (a dead peer): set every READY and FREE word
 // of this rank to 1. A queue resets a word after each wait, so a caller draining a stream
-// repeats this until the stream is idle. Host flags: CPU stores. Device flags: a blocking
-// hipMemcpy, which can queue behind the blocked stream on a shared hardware queue (host
-// flags are the mode that can always abort).
-int dli_ipc_abort(void* h) {
+// repeats this until the stream is idle. Host flags: CPU stores. Device flags: an H2D copy
+// of the pattern on the endpoint's own non-blocking stream (a DMA queue, not the blocked
+// compute queue), polled for up to timeout_s; -1004 when it did not complete.
+int dli_ipc_abort(void* h, double timeout_s) {
   auto* e = E(h);
   const size_t n = 2 * (size_t)e->world;
   if (e->host_flags) {
     for (size_t i = 0; i < n; ++i) set_word(e->flags + i * kFlagStride, 1);
     return 0;
   }
-  std::vector<uint64_t> v(e->flag_bytes / 8, 0);
-  for (size_t i = 0; i < n; ++i) v[i * kFlagStride] = 1;
-  return herr(hipMemcpy(e->flags, v.data(), e->flag_bytes, hipMemcpyHostToDevice));
+  if (e->abort_stream == nullptr) return -1005;
+  int r = herr(hipMemcpyAsync(e->flags, e->abort_src, e->flag_bytes, hipMemcpyHostToDevice,
+                              e->abort_stream));
+  if (r) return r;
+  const auto t0 = std::chrono::steady_clock::now();
+  while (hipStreamQuery(e->abort_stream) == hipErrorNotReady) {
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s)
+      return -1004;
+    usleep(200);
+  }
+  return 0;
 }
 
 void dli_ipc_stats(void* h, long long* out3) {
@@ -341,6 +400,8 @@ void dli_ipc_destroy(void* h) {
   } else if (e->flags) {
     (void)hipFree(e->flags);
   }
+  if (e->abort_stream) (void)hipStreamDestroy(e->abort_stream);
+  if (e->abort_src) (void)hipHostFree(e->abort_src);
   if (e->mailbox) (void)hipFree(e->mailbox);
   delete e;
 }

@@ -44,6 +44,7 @@ _SIGS = {
     "dli_prefill_set_min_len": [I],
     "dli_decode_set_pipe": [I],
     "dli_decode_get_pipe": [],
+    "dli_gemm_set_slab_store": [I],
     "dli_prefill_attention_paged": [P, I, P, I, P, P, P, P, P, I, I, I, I, I, I, I, F, P],
     "dli_sample": [P, P, L, I, I, P, P, P, P, P],
     "dli_topk_rows": [P, P, P, L, I, I, I, I, P],

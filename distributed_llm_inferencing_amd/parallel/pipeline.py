@@ -631,8 +631,14 @@ class DistributedPipelineEngine:
             policy=policy, seed=seed, use_graphs=use_graphs, num_blocks=num_blocks, dtype=dtype,
             vocab_parallel=self.vocab_parallel, microbatches=self.microbatches,
             max_tokens=max_tokens, shard_dir=shard_dir)
+        esz = torch.empty(0, dtype=dtype).element_size()
+        D = self.cfg.hidden_size
+        # mailbox sizes of the IPC data plane: a whole step's hidden rows on r -> r + 1; the
+        # tail's final hidden / tokens and the candidates on every other edge
         self.channel = PipeChannel(self.device, dtype=dtype,
-                                   ctrl_bytes=ctrl_slot_bytes(max_batch, max_tokens, tw))
+                                   ctrl_bytes=ctrl_slot_bytes(max_batch, max_tokens, tw),
+                                   msg_bytes=(max_tokens * D * esz,
+                                              max(max_batch * D * esz, max_batch * 8 * CAND)))
         self.head = None
         if self.rank == 0:
             bm = BlockManager(nb, block_size)

@@ -69,12 +69,20 @@ class PipeChannel:
     a spinning receive in front of a send."""
 
     def __init__(self, device: torch.device, dtype=torch.bfloat16,
-                 ctrl_bytes: int = 1 << 20, ctrl: Optional[str] = None):
+                 ctrl_bytes: int = 1 << 20, ctrl: Optional[str] = None,
+                 msg_bytes: Tuple[int, int] = (64 << 20, 8 << 20),
+                 comm: Optional[str] = None):
         self.rank = dist.get_rank()
         self.world = dist.get_world_size()
         self.device = torch.device(device)
         self.dtype = dtype
-        self.nccl = dist.get_backend() == "nccl"
+        # data plane: "torch" (torch.distributed p2p), "rccl" (comm.cpp on the compute
+        # stream) or "ipc" (device mailboxes, ipc.cpp; on CPU its host model, fifo.py)
+        self.comm = comm or os.environ.get("DLI_PP_COMM", "torch")
+        if self.comm not in ("torch", "rccl", "ipc"):
+            raise ValueError(f"DLI_PP_COMM={self.comm}: expected torch | rccl | ipc")
+        self.nccl = dist.get_backend() == "nccl" or (self.comm == "ipc"
+                                                     and self.device.type == "cuda")
         # collective over all ranks (called once per engine). Idle serving ranks block on
         # the control plane between sessions: no timeout that could fire while idle.
         self.ctrl_group = dist.new_group(backend="gloo", timeout=timedelta(days=365))
@@ -100,10 +108,15 @@ class PipeChannel:
             if int(r.item()) != self.prev:
                 raise RuntimeError(f"pipeline ring check failed on rank {self.rank}")
         # DLI_PP_COMM=rccl: the data plane on this module's own RCCL communicator
-        # (csrc/runtime/comm.cpp), enqueued on the compute stream; default: torch.distributed
+        # (csrc/runtime/comm.cpp), enqueued on the compute stream; DLI_PP_COMM=ipc: device
+        # mailboxes (csrc/runtime/ipc.cpp), also on the compute stream, or on CPU the same
+        # protocol on shared-memory mailboxes (fifo.py); default: torch.distributed
         self.rccl = None
-        if self.world > 1 and self.nccl and os.environ.get("DLI_PP_COMM", "torch") == "rccl":
+        self.ipc = None
+        if self.world > 1 and self.comm == "rccl" and dist.get_backend() == "nccl":
             self._init_rccl()
+        if self.world > 1 and self.comm == "ipc":
+            self._init_ipc(*msg_bytes)
 
     # ------------------------------------------------------------------ setup
     def _init_rccl(self) -> None:
@@ -117,6 +130,41 @@ class PipeChannel:
                            torch.cuda.current_stream(self.device).cuda_stream)
         if int(r.item()) != self.prev:
             raise RuntimeError(f"RCCL ring check failed on rank {self.rank}")
+
+    def _init_ipc(self, big: int, small: int) -> None:
+        """Mailboxes: ``big`` bytes on the activation edges r -> r + 1, ``small`` on the rest
+        (tail -> every rank: final hidden / tokens, every rank -> 0: candidates)."""
+        from .fifo import mailbox_caps
+        cap = mailbox_caps(self.world, big, small)
+        box = [f"/dli_pp_{os.environ.get('MASTER_PORT', '0')}_{os.getpid()}_{next(_ring_ids)}"
+               if self.rank == 0 else None]
+        dist.broadcast_object_list(box, src=0, group=self.ctrl_group)
+        prefix = box[0]
+        if self.device.type == "cuda":
+            from ..runtime import IpcEndpoint
+            host = os.environ.get("DLI_IPC_FLAGS", "device") == "host"
+            ep = IpcEndpoint(self.world, self.rank, cap, host_prefix=prefix if host else "")
+            hs = [None] * self.world
+            dist.all_gather_object(hs, ep.handles(), group=self.ctrl_group)
+            dist.barrier(group=self.ctrl_group)
+            ep.connect(hs)
+        else:
+            from .fifo import ShmMailboxTransport
+            ep = ShmMailboxTransport(self.world, self.rank, cap, prefix)
+            dist.barrier(group=self.ctrl_group)
+            ep.connect()
+        dist.barrier(group=self.ctrl_group)
+        self.ipc = ep
+        self.data_device = self.device
+        t = torch.full((1,), float(self.rank), device=self.device)
+        r = torch.empty(1, device=self.device)
+        self.ipc.exchange([(t, self.next)], [(r, self.prev)], self._stream())
+        if int(r.item()) != self.prev:
+            raise RuntimeError(f"IPC ring check failed on rank {self.rank}")
+
+    def _stream(self) -> int:
+        return (torch.cuda.current_stream(self.device).cuda_stream
+                if self.device.type == "cuda" else 0)
 
     def _init_ctrl(self, mode: str) -> None:
         hosts = [None] * self.world
@@ -227,6 +275,14 @@ class PipeChannel:
         RCCL: every Work is waited on the CURRENT stream — a stream dependency, not a host
         wait — so the next kernels on this stream (the consumer replay, or the replay that
         rewrites a sent static output) run after the transfer. gloo: a host wait."""
+        if self.ipc is not None:             # stream-ordered mailboxes, FIFO per edge
+            with trace_range("pp.exchange"):
+                self.ipc.exchange(
+                    [(t.contiguous(), peer) for t, peer, _ in sends
+                     if t is not None and t.numel()],
+                    [(b, peer) for b, peer, _ in recvs if b.numel()], self._stream())
+            self.exchanges += 1
+            return
         if self.rccl is not None:            # stream-ordered, no waits (comm.cpp)
             with trace_range("pp.exchange"):
                 self.rccl.exchange(
@@ -269,6 +325,11 @@ class PipeChannel:
         if getattr(self, "rccl", None) is not None:
             self.rccl.close()
             self.rccl = None
+        if getattr(self, "ipc", None) is not None:
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
+            self.ipc.close()
+            self.ipc = None
         if self.ring is not None:
             if self.rank == 0:
                 self.ring.close()

@@ -84,7 +84,7 @@ _SIGS = {
     "dli_ipc_connect": ([_P, _P], _I),
     "dli_ipc_exchange": ([_P, _P, _I, _P, _P, _P, _I, _P, _P, _P], _I),
     "dli_ipc_pending": ([_P, _I], _LL),
-    "dli_ipc_abort": ([_P], _I),
+    "dli_ipc_abort": ([_P, ctypes.c_double], _I),
     "dli_ipc_stats": ([_P, _P], None),
     "dli_ipc_host_flags": ([_P], _I),
     "dli_ipc_destroy": ([_P], None),
@@ -573,8 +573,10 @@ class IpcEndpoint:
         """Host-flag mode: 1 while a message from ``peer`` waits in this rank's mailbox."""
         return int(lib().dli_ipc_pending(self._h, int(peer)))
 
-    def abort(self) -> None:
-        r = lib().dli_ipc_abort(self._h)
+    def abort(self, timeout_s: float = 5.0) -> None:
+        """Set every flag this rank's queue could be waiting on (a dead peer's mailboxes):
+        the blocked exchange completes (with stale payload) so the stream drains."""
+        r = lib().dli_ipc_abort(self._h, float(timeout_s))
         if r != 0:
             raise RuntimeError(f"IPC abort failed ({r})")
 

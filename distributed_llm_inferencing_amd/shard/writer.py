@@ -38,18 +38,33 @@ def model_dir(output_dir: str, model_name: str) -> Path:
 def export_shards(model_name: str, num_shards: int, output_dir: str = "model_shards",
                   policy: str = "even", seed: int = 0, params: Optional[Dict] = None,
                   dtype=torch.bfloat16, cfg: Optional[ModelConfig] = None,
-                  log=print) -> List[Path]:
+                  log=print, hf_dir: Optional[str] = None) -> List[Path]:
+    """``hf_dir``: shard a HF ``save_pretrained`` checkpoint (the reference's sharder loads
+    the HF model, shard_model.py:37): each stage reads only its own tensors from it."""
     from safetensors.torch import save_file
+    if hf_dir is not None:
+        from ..models.hf import config_from_hf
+        cfg = config_from_hf(json.loads((Path(hf_dir) / "config.json").read_text()),
+                             model_name)
     cfg = cfg or get_config(model_name)
     plans = plan_stages(cfg, num_shards, policy)
     root = model_dir(output_dir, model_name)
     root.mkdir(parents=True, exist_ok=True)
-    load_tokenizer(cfg).save_pretrained(str(root / "tokenizer"))
+    load_tokenizer(cfg, hf_dir).save_pretrained(str(root / "tokenizer"))
     paths = []
     for p in plans:
         log(f"Shard {p.shard_id} will contain layers {p.start_layer} to {p.end_layer - 1}")
         shapes = W.stage_param_shapes(cfg, p.start_layer, p.end_layer, p.first, p.last)
-        if params is None:
+        if hf_dir is not None:
+            from ..models.hf import load_hf_dir
+            _, sd = load_hf_dir(hf_dir, "cpu", dtype, model_name,
+                                layers=range(p.start_layer, p.end_layer), first=p.first,
+                                last=p.last)
+            missing = set(shapes) - set(sd)
+            if missing:
+                raise ValueError(f"{hf_dir}: stage {p.shard_id} lacks {sorted(missing)[:3]}")
+            sd = {k: sd[k] for k in shapes}
+        elif params is None:
             sd = W.random_init(shapes, "cpu", dtype, seed)
         else:
             sd = {k: params[k].to(dtype).contiguous() for k in shapes}
@@ -87,10 +102,22 @@ def load_shard(shard_path: str, device="cpu") -> Tuple[ModelConfig, dict, Dict[s
     return cfg, meta, params
 
 
-def load_cached_model(cache_dir: str, model_name: str, device="cpu"):
+def load_cached_model(cache_dir: str, model_name: str, device="cpu",
+                      dtype: Optional[torch.dtype] = None):
     """Whole-model weights from the model cache, or None when the cache holds none:
-    ``<cache>/<model>/model.safetensors`` + ``config.json``, or every ``shard_<i>/`` of an
-    export (merged). Returns (config, params on `device`, tokenizer dir or None)."""
+    a HF checkpoint (``save_pretrained`` directory or hub-cache snapshot, ``models/hf.py``;
+    the reference's ``from_pretrained(cache_dir=MODEL_CACHE_DIR)``, worker/app.py:117-124),
+    ``<cache>/<model>/model.safetensors`` + our ``config.json``, or every ``shard_<i>/`` of
+    an export (merged). Returns (config, params on `device`, tokenizer dir or None)."""
+    from ..models.hf import find_hf_dir, load_hf_dir
+    hf = find_hf_dir(cache_dir, model_name)
+    if hf is not None:
+        dev = torch.device(device)
+        dt = dtype or (torch.bfloat16 if dev.type == "cuda" else torch.float32)
+        cfg, params = load_hf_dir(hf, device, dt, model_name)
+        tok = str(hf) if any((hf / f).exists() for f in ("tokenizer.json",
+                                                         "tokenizer_config.json")) else None
+        return cfg, params, tok
     root = model_dir(cache_dir, model_name)
     if not root.is_dir():
         return None
@@ -138,12 +165,16 @@ def main(argv=None):
     ap.add_argument("--output_dir", "--output-dir", default="model_shards")
     ap.add_argument("--policy", default="even", choices=["even", "hbm", "balanced"])
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--from-hf", "--from_hf", dest="from_hf", default=None,
+                    help="shard this HF save_pretrained checkpoint directory instead of a "
+                         "random init")
     ap.add_argument("--register", default=None,
                     help="master URL: register each shard (node ids via --nodes)")
     ap.add_argument("--nodes", default="", help="comma-separated node ids, one per shard")
     a = ap.parse_args(argv)
     print(f"Sharding model {a.model_name} into {a.num_shards} shards")
-    paths = export_shards(a.model_name, a.num_shards, a.output_dir, a.policy, a.seed)
+    paths = export_shards(a.model_name, a.num_shards, a.output_dir, a.policy, a.seed,
+                          hf_dir=a.from_hf)
     print(f"Model {a.model_name} sharded successfully into {a.num_shards} shards")
     print(f"Shards are stored in {model_dir(a.output_dir, a.model_name)}")
     if a.register:

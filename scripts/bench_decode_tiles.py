@@ -25,8 +25,13 @@ def main():
     ap.add_argument("--m", type=int, default=512)
     ap.add_argument("--shapes", default="o,qkv")
     ap.add_argument("--iters", type=int, default=6)
+    ap.add_argument("--slab-store", type=int, default=0,
+                    help="split-K partial stores: 0 plain, 1 nt, 2 sc1, 3 sc0 sc1")
+    ap.add_argument("--top", type=int, default=0, help="print only the N fastest plans")
     a = ap.parse_args()
     from distributed_llm_inferencing_amd import ops
+    from distributed_llm_inferencing_amd.ops import _native as NT
+    NT.require_native().dli_gemm_set_slab_store(a.slab_store)
     from distributed_llm_inferencing_amd.ops import gemm as G
     dev = torch.device("cuda")
     for name in a.shapes.split(","):
@@ -51,10 +56,11 @@ def main():
                 rows.append({"shape": name, "tile": p.tile, "splits": p.splits,
                              "error": str(e)[:80]})
                 continue
-            rows.append({"shape": name, "M": a.m, "tile": p.tile, "bm_bn": G.TILES[p.tile],
+            rows.append({"shape": name, "M": a.m, "slab_store": a.slab_store, "tile": p.tile,
+                         "bm_bn": G.TILES[p.tile],
                          "splits": p.splits, "us": round(ms * 1e3, 2),
                          "tflops": round(2 * a.m * N * K / (ms * 1e-3) / 1e12, 1)})
-        for r in sorted(rows, key=lambda r: r.get("us", 1e9)):
+        for r in sorted(rows, key=lambda r: r.get("us", 1e9))[:a.top or None]:
             print(json.dumps(r), flush=True)
         del ws_
 

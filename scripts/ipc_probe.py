@@ -42,7 +42,8 @@ def main():
 
     def report(name, **kw):
         if rank == 0:
-            rec = {"check": name, "flags": a.flags, **kw}
+            rec = {"check": name, "flags": a.flags,
+                   "copy": os.environ.get("DLI_IPC_COPY", "kernel"), **kw}
             print(json.dumps(rec), flush=True)
             results.append(rec)
 
@@ -138,7 +139,7 @@ def main():
             report("graph", captured=False, error=err, ok=False)
         dist.barrier()
 
-    if a.flags == "host" and world >= 2:
+    if world >= 2:
         # rank 0 waits on a message rank 1 never sends; the host sees nothing pending, aborts
         r = torch.empty(16, dtype=torch.int32, device=dev)
         if rank == 0:
@@ -149,11 +150,16 @@ def main():
             time.sleep(1.0)
             stuck = not ev.query()
             t0 = time.perf_counter()
+            err = None
             while not ev.query() and time.perf_counter() - t0 < 10:
-                ep.abort()
+                try:
+                    ep.abort(timeout_s=2.0)
+                except RuntimeError as e:
+                    err = str(e)
+                    break
                 time.sleep(0.01)
             report("abort", pending_before=before, stuck_before_abort=stuck,
-                   released=ev.query(), ok=stuck and ev.query())
+                   released=ev.query(), error=err, ok=stuck and ev.query())
         dist.barrier()
     torch.cuda.synchronize(dev)
     dist.barrier()

@@ -1,0 +1,168 @@
+"""Tag-blind FIFO data plane (parallel/fifo.py, the host model of csrc/runtime/ipc.cpp).
+
+gloo matches point-to-point messages by (peer, tag); RCCL and the device mailboxes match by
+issue order per (src, dst) and ignore tags. These tests run every multi-rank schedule
+through the shared-memory mailbox transport, which enforces the RCCL rule (and asserts
+equal sizes), so an ordering bug that gloo would hide fails here on CPU:
+
+* the transport itself: FIFO per edge, size mismatch detected, mailbox capacity enforced;
+* the layer-sharded pipeline at N = 2..8, tail head and vocab-parallel head, mixed steps,
+  chunked prefill: token-identical to the single-stage engine.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from distributed_llm_inferencing_amd.engine import SamplingParams
+from distributed_llm_inferencing_amd.engine.llm_engine import LLMEngine
+
+PROMPTS = [[5, 6, 7, 8], [9, 10, 11], [1, 2, 3, 4, 5, 6, 7], [100, 200], [7] * 9, [3, 4], [8] * 3]
+LONG = [list(range(3, 3 + 40)), [11] * 37]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _env(rank, world, port, **kw):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), DLI_PP_COMM="ipc", **kw)
+    torch.set_num_threads(1)
+
+
+def _spawn(target, world, *args, n_results=1, timeout=300):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = [q.get(timeout=timeout) for _ in range(n_results)]
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    return res
+
+
+# ------------------------------------------------------------------------------ transport
+def _transport_worker(rank, world, port, q):
+    _env(rank, world, port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    from distributed_llm_inferencing_amd.parallel.fifo import (FifoMismatch,
+                                                               ShmMailboxTransport, mailbox_caps)
+    ep = ShmMailboxTransport(world, rank, mailbox_caps(world, 4096, 4096),
+                             f"/dli_fifo_t_{port}", timeout_s=20)
+    dist.barrier()
+    ep.connect()
+    dist.barrier()
+    out = {}
+    nxt, prv = (rank + 1) % world, (rank - 1) % world
+    # FIFO: three messages of different sizes on one edge, received in send order
+    msgs = [torch.arange(n, dtype=torch.int32) + 100 * rank for n in (3, 17, 5)]
+    got = [torch.empty(n, dtype=torch.int32) for n in (3, 17, 5)]
+    for m, g in zip(msgs, got):          # one message per exchange: the mailbox holds one
+        ep.exchange([(m, nxt)], [(g, prv)])
+    out["fifo"] = all(torch.equal(g, torch.arange(g.numel(), dtype=torch.int32) + 100 * prv)
+                      for g in got)
+    # order divergence: rank 0 sends 8 then 4 ints, rank 1 receives 4 then 8
+    if world == 2:
+        try:
+            if rank == 0:
+                ep.exchange([(torch.zeros(8, dtype=torch.int32), 1)], [])
+                ep.exchange([(torch.zeros(4, dtype=torch.int32), 1)], [])
+                out["mismatch"] = None
+            else:
+                ep.exchange([], [(torch.empty(4, dtype=torch.int32), 0)])
+                out["mismatch"] = None
+        except FifoMismatch as e:
+            out["mismatch"] = str(e)
+        except TimeoutError as e:
+            out["mismatch"] = "timeout: " + str(e)
+    try:
+        ep.send(torch.zeros(2048, dtype=torch.int32), nxt)
+        out["cap"] = None
+    except ValueError as e:
+        out["cap"] = str(e)
+    q.put((rank, out))
+    dist.barrier()
+    ep.close()
+    dist.destroy_process_group()
+
+
+def test_fifo_transport_orders_and_checks_sizes():
+    res = dict(_spawn(_transport_worker, 2, n_results=2))
+    assert res[0]["fifo"] and res[1]["fifo"]
+    assert "differs between the two ranks" in res[1]["mismatch"]
+    assert "exceeds the mailbox" in res[0]["cap"]
+
+
+# ------------------------------------------------------------------------------ pipeline
+def _pp_worker(rank, world, port, q, vp, mixed, chunk):
+    _env(rank, world, port, DLI_PP_VOCAB_PARALLEL=vp, DLI_MIXED_STEPS=mixed)
+    import torch.distributed as dist
+    from distributed_llm_inferencing_amd.parallel.pipeline import DistributedPipelineEngine
+    eng = DistributedPipelineEngine("llama-tiny", "cpu", max_batch=4, max_model_len=64,
+                                    num_blocks=256, dtype=torch.float32,
+                                    max_prefill_tokens=chunk)
+    assert eng.channel.ipc is not None
+    if rank == 0:
+        res = []
+        greedy = SamplingParams(max_length=20, do_sample=False, ignore_eos=True)
+        res.append([o.all_ids for o in eng.generate(PROMPTS, greedy)])
+        res.append([o.all_ids for o in eng.generate(PROMPTS, SamplingParams(
+            max_length=20, seed=11, ignore_eos=True))])
+        # continuous admission: prompts (some longer than the prefill chunk) join a running
+        # session, so mixed prefill+decode steps and chunk steps cross the ring
+        from distributed_llm_inferencing_amd.worker.service import PipelineService
+        svc = PipelineService(eng, name="pp")
+        futs = [svc.submit(p, SamplingParams(max_length=56, do_sample=False, ignore_eos=True))
+                for p in PROMPTS[:3]]
+        import time
+        t0 = time.monotonic()
+        while eng.head.stats.decode_steps < 3 and time.monotonic() - t0 < 60:
+            time.sleep(0.005)             # the first prompts are decoding
+        futs += [svc.submit(p, SamplingParams(max_length=56, do_sample=False, ignore_eos=True))
+                 for p in LONG + PROMPTS[3:] + PROMPTS * world]
+        res.append([f.result(timeout=200).all_ids for f in futs])
+        svc.close()
+        res.append(eng.vocab_parallel)
+        res.append(eng.head.sched.num_mixed)
+        res.append(eng.channel.ipc.stats())
+        eng.shutdown()
+        q.put(res)
+    else:
+        eng.serve()
+    dist.barrier()
+    eng.channel.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,vp,mixed,chunk", [(2, "0", "1", 16384), (3, "0", "1", 16),
+                                                  (2, "1", "0", 16384), (4, "auto", "1", 16),
+                                                  (8, "auto", "1", 16), (8, "0", "0", 16384)])
+def test_pipeline_over_fifo_mailboxes_matches_single_stage(world, vp, mixed, chunk):
+    (res,) = _spawn(_pp_worker, world, vp, mixed, chunk)
+    eng = LLMEngine("llama-tiny", device="cpu", dtype=torch.float32, max_batch=8,
+                    max_model_len=64, num_blocks=64)
+    assert res[0] == [o.all_ids for o in eng.generate(PROMPTS, SamplingParams(
+        max_length=20, do_sample=False, ignore_eos=True))]
+    assert res[1] == [o.all_ids for o in eng.generate(PROMPTS, SamplingParams(
+        max_length=20, seed=11, ignore_eos=True))]
+    ref = [o.all_ids for o in eng.generate(PROMPTS[:3] + LONG + PROMPTS[3:] + PROMPTS * world,
+                                           SamplingParams(
+        max_length=56, do_sample=False, ignore_eos=True))]
+    assert res[2] == ref
+    assert res[3] == (vp == "1" or (vp == "auto" and world >= 4))
+    if mixed == "1":
+        assert res[4] > 0                     # mixed steps crossed the ring
+    assert res[5]["sends"] > 0 and res[5]["recvs"] > 0

@@ -31,8 +31,8 @@ def _env(rank, world, port, **extra):
                       DLI_SAME_DEVICE="1", DLI_GEMM_AUTOTUNE="0", **extra)
 
 
-def _pp_worker(rank, world, port, q, vp):
-    _env(rank, world, port, DLI_PP_VOCAB_PARALLEL=vp)
+def _pp_worker(rank, world, port, q, vp, comm="torch"):
+    _env(rank, world, port, DLI_PP_VOCAB_PARALLEL=vp, DLI_PP_COMM=comm)
     import torch.distributed as dist
     from distributed_llm_inferencing_amd.parallel.pipeline import DistributedPipelineEngine
     eng = DistributedPipelineEngine("llama-tiny", "cuda", max_batch=8, max_model_len=64,
@@ -40,11 +40,13 @@ def _pp_worker(rank, world, port, q, vp):
     if rank == 0:
         res = [[o.all_ids for o in eng.generate(PROMPTS, sp)] for sp in (GREEDY, SAMPLED)]
         res.append(eng.vocab_parallel)
+        res.append(eng.channel.ipc.stats() if eng.channel.ipc is not None else None)
         eng.shutdown()
         q.put(res)
     else:
         eng.serve()
     dist.barrier()
+    eng.channel.close()
     dist.destroy_process_group()
 
 
@@ -82,6 +84,26 @@ def test_pipeline_two_ranks_on_gpu_match_single_stage(gpu, vp):
     finally:
         del os.environ["DLI_GEMM_AUTOTUNE"]
     assert res[2] == (vp == "1")
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world,vp", [(2, "0"), (2, "1"), (4, "1")])
+def test_pipeline_over_ipc_mailboxes_on_gpu(gpu, world, vp):
+    """The device data plane with N ranks on ONE GPU: every activation / token / candidate
+    message goes through hipIpc-mapped mailboxes (stream-ordered copies +
+    hipStreamWaitValue64 / WriteValue64 semaphores, csrc/runtime/ipc.cpp), token-identical
+    to the single-stage engine."""
+    (res,) = _run(_pp_worker, world, vp, "ipc")
+    os.environ["DLI_GEMM_AUTOTUNE"] = "0"
+    try:
+        eng = LLMEngine("llama-tiny", device="cuda", max_batch=8, max_model_len=64,
+                        num_blocks=64)
+        assert res[0] == [o.all_ids for o in eng.generate(PROMPTS, GREEDY)]
+        assert res[1] == [o.all_ids for o in eng.generate(PROMPTS, SAMPLED)]
+    finally:
+        del os.environ["DLI_GEMM_AUTOTUNE"]
+    assert res[2] == (vp == "1")
+    assert res[3]["sends"] > 0 and res[3]["recvs"] > 0 and res[3]["bytes_out"] > 0
 
 
 def _ep_worker(rank, world, port, q):
