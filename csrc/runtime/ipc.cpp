@@ -84,8 +84,33 @@ __global__ void __launch_bounds__(256) ipc_copy_kernel(uint4* __restrict__ dst,
   if (blockIdx.x == 0 && (int)threadIdx.x < ntail) dtail[threadIdx.x] = stail[threadIdx.x];
 }
 
+// Semaphore waits / signals as kernels, used while a stream is being captured into a
+// hipGraph (stream write/wait-value operations captured into a graph were measured to lose
+// their ordering against the copy kernels on replay: profiles/r3/ipc_probe_*.jsonl, check
+// "graph"). One lane polls with acquire loads and a bounded wall-clock budget, so every wave
+// finishes even if the peer never signals (then *err is set and the caller's host sees it).
+__global__ void ipc_wait_kernel(uint64_t* flag, uint64_t* err, unsigned long long budget) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long t0 = wall_clock64();
+  while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != 1ull) {
+    __builtin_amdgcn_s_sleep(4);
+    if (wall_clock64() - t0 > budget) {
+      __hip_atomic_store(err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
+    }
+  }
+  __hip_atomic_store(flag, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void ipc_signal_kernel(uint64_t* flag) {
+  if (threadIdx.x == 0) __hip_atomic_store(flag, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 struct Endpoint {
   int world = 0, rank = 0;
+  int sync_mode = 0;                  // 0: stream ops, graph capture -> kernels; 1: kernels
+  unsigned long long wait_budget = 0; // wall-clock ticks a wait kernel polls at most
+  uint64_t* err_word = nullptr;       // set by a wait kernel that ran out of budget
   bool host_flags = false;
   bool copy_kernel = true;
   hipStream_t abort_stream = nullptr; // device-flag abort: its own (SDMA) queue
@@ -184,11 +209,25 @@ void* dli_ipc_create(int world, int rank, const long long* cap, const char* host
   const char* cm = getenv("DLI_IPC_COPY");
   e->copy_kernel = !(cm != nullptr && std::string(cm) == "memcpy");
   for (int s = 0; s < world; ++s) e->mailbox_bytes += (size_t)e->cap[s * world + rank];
-  if (e->mailbox_bytes && hipMalloc(&e->mailbox, e->mailbox_bytes) != hipSuccess) {
+  if (e->mailbox_bytes && (hipMalloc(&e->mailbox, e->mailbox_bytes) != hipSuccess ||
+                           hipMemset(e->mailbox, 0, e->mailbox_bytes) != hipSuccess)) {
     delete e;
     return nullptr;
   }
-  e->flag_bytes = ((2 * (size_t)world * kFlagStride * 8 + 4095) / 4096) * 4096;
+  e->flag_bytes = (((2 * (size_t)world + 1) * kFlagStride * 8 + 4095) / 4096) * 4096;
+  const char* sm = getenv("DLI_IPC_SYNC");
+  e->sync_mode = (sm != nullptr && std::string(sm) == "kernel") ? 1 : 0;
+  {
+    int khz = 0;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess ||
+        khz <= 0)
+      khz = 100000;
+    const char* bs = getenv("DLI_IPC_WAIT_S");
+    const double secs = bs ? atof(bs) : 120.0;
+    e->wait_budget = (unsigned long long)(secs * 1000.0 * khz);
+  }
   // FREE words start at 1 (every mailbox empty), READY words at 0
   std::vector<uint64_t> init(e->flag_bytes / 8, 0);
   for (int d = 0; d < world; ++d) init[free_word(e, d)] = 1;
@@ -205,6 +244,7 @@ void* dli_ipc_create(int world, int rank, const long long* cap, const char* host
     std::memcpy(p, init.data(), e->flag_bytes);
     e->flags = p;
     e->flags_dev = dev_addr(p);
+    e->err_word = e->flags_dev + 2 * (size_t)world * kFlagStride;
     e->host_pages.assign(world, nullptr);
     e->host_pages[rank] = p;
   } else {
@@ -215,6 +255,7 @@ void* dli_ipc_create(int world, int rank, const long long* cap, const char* host
       return nullptr;
     }
     e->flags_dev = e->flags;
+    e->err_word = e->flags + 2 * (size_t)world * kFlagStride;
     if (hipStreamCreateWithFlags(&e->abort_stream, hipStreamNonBlocking) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void**>(&e->abort_src), e->flag_bytes,
                       hipHostMallocDefault) != hipSuccess) {
@@ -322,22 +363,42 @@ int dli_ipc_exchange(void* h, void* stream, int n_send, void* const* send_ptrs,
     const Edge& g = e->edge[recv_peers[i]];
     if (g.my_ready == nullptr || recv_bytes[i] > g.in_bytes) return -1003;
   }
+  bool kern = e->sync_mode == 1;
+  if (!kern) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive)
+      kern = true;
+  }
+  // wait until *w == 1 then reset it; signal *w = 1
+  auto wait = [&](uint64_t* w) -> int {
+    if (kern) {
+      ipc_wait_kernel<<<1, 64, 0, s>>>(w, e->err_word, e->wait_budget);
+      return herr(hipGetLastError());
+    }
+    int r = herr(hipStreamWaitValue64(s, w, 1, hipStreamWaitValueEq));
+    return r ? r : herr(hipStreamWriteValue64(s, w, 0, 0));
+  };
+  auto signal = [&](uint64_t* w) -> int {
+    if (kern) {
+      ipc_signal_kernel<<<1, 64, 0, s>>>(w);
+      return herr(hipGetLastError());
+    }
+    return herr(hipStreamWriteValue64(s, w, 1, 0));
+  };
   int r = 0;
   for (int i = 0; i < n_send && r == 0; ++i) {
     const Edge& g = e->edge[send_peers[i]];
-    r = herr(hipStreamWaitValue64(s, g.my_free, 1, hipStreamWaitValueEq));
-    if (!r) r = herr(hipStreamWriteValue64(s, g.my_free, 0, 0));
+    r = wait(g.my_free);
     if (!r) r = copy_async(e, g.peer_mailbox, send_ptrs[i], send_bytes[i], s);
-    if (!r) r = herr(hipStreamWriteValue64(s, g.peer_ready, 1, 0));
+    if (!r) r = signal(g.peer_ready);
     e->sends++;
     e->bytes_out += (uint64_t)send_bytes[i];
   }
   for (int i = 0; i < n_recv && r == 0; ++i) {
     const Edge& g = e->edge[recv_peers[i]];
-    r = herr(hipStreamWaitValue64(s, g.my_ready, 1, hipStreamWaitValueEq));
-    if (!r) r = herr(hipStreamWriteValue64(s, g.my_ready, 0, 0));
+    r = wait(g.my_ready);
     if (!r) r = copy_async(e, recv_ptrs[i], g.my_mailbox, recv_bytes[i], s);
-    if (!r) r = herr(hipStreamWriteValue64(s, g.peer_free, 1, 0));
+    if (!r) r = signal(g.peer_free);
     e->recvs++;
   }
   return r;
@@ -375,6 +436,20 @@ int dli_ipc_abort(void* h, double timeout_s) {
     usleep(200);
   }
   return 0;
+}
+
+// 1 when a wait kernel ran out of its wall-clock budget (a peer stopped signalling).
+int dli_ipc_error(void* h) {
+  auto* e = E(h);
+  if (e->host_flags)
+    return reinterpret_cast<std::atomic<uint64_t>*>(e->flags + 2 * (size_t)e->world * kFlagStride)
+               ->load(std::memory_order_acquire) ? 1 : 0;
+  if (e->abort_stream == nullptr) return -1;
+  uint64_t v = 0;
+  if (hipMemcpyAsync(&v, e->err_word, 8, hipMemcpyDeviceToHost, e->abort_stream) != hipSuccess ||
+      hipStreamSynchronize(e->abort_stream) != hipSuccess)
+    return -1;
+  return v ? 1 : 0;
 }
 
 void dli_ipc_stats(void* h, long long* out3) {

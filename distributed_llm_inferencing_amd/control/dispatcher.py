@@ -9,8 +9,10 @@ and error strings here, with these fixes:
 * selection by placement then load: nodes whose loaded shards cover the model first,
   then the active node with the fewest requests in flight from this master (ties -> lowest
   id), instead of always the first node;
-* a connection failure retries the request on the next candidate node (up to
-  ``max_attempts``) and reports the node to the health monitor, instead of failing;
+* a connection failure, or a 503 from a node whose pipeline ring broke, retries the request
+  on the next candidate node (up to ``max_attempts``: another replica) and reports the node
+  to the health monitor, instead of failing (the reference fails over only at selection
+  time, views.py:99-105,389-391);
 * the worker's bearer token is sent when ``AUTH_KEY`` is configured (the reference never
   sends it, so enabling worker auth broke dispatch, SURVEY.md W2);
 * a fixed pool of consumer threads instead of one unbounded thread per submit.
@@ -207,6 +209,8 @@ class Dispatcher:
             self.store.mark_failed(rid, data.get("message", "Unknown error"))
             return False, None
         self._forget(node["id"])
+        if r.status_code == 503:               # the node's pipeline broke: next replica
+            return False, f"Node returned status code 503: {r.text[:300]}"
         self.store.mark_failed(rid, f"Node returned status code {r.status_code}: {r.text}")
         return False, None
 
@@ -383,6 +387,8 @@ class AsyncDispatcher(Dispatcher):
             await self._s(self.store.mark_failed, rid, data.get("message", "Unknown error"))
             return False, None
         self._forget(node["id"])
+        if st == 503:                          # the node's pipeline broke: next replica
+            return False, f"Node returned status code 503: {text[:300]}"
         await self._s(self.store.mark_failed, rid, f"Node returned status code {st}: {text}")
         return False, None
 

@@ -202,47 +202,88 @@ class DeviceBatch:
 
 
 def to_device(meta: StepMeta, device, pin: bool = True) -> DeviceBatch:
-    """One H2D copy of the packed payload, then device-side views/casts."""
+    """Every per-step array packed into ONE int32 host buffer (pinned on GPU), ONE H2D copy,
+    then device-side views: an eager prefill / mixed step pays a single transfer."""
     dev = torch.device(device)
     S, T = meta.num_seqs, meta.num_tokens
+    parts: list = []             # (name, int32 words, dtype, shape)
+    nwords = [0]
 
-    def t(a, dt):
+    def add(name, a, dt):
         if a is None:
-            return None
-        x = torch.from_numpy(np.ascontiguousarray(a))
-        if dev.type == "cuda":
-            x = x.pin_memory() if pin else x
-            return x.to(dev, non_blocking=True).to(dt)
-        return x.to(dt)
+            return
+        a = np.ascontiguousarray(a)
+        if dt == torch.int64:
+            a = a.astype(np.int64, copy=False)
+            nwords[0] += nwords[0] & 1                   # 8-byte aligned
+        elif dt == torch.float32:
+            a = a.astype(np.float32, copy=False)
+        else:
+            a = a.astype(np.int32, copy=False)
+        w = a.reshape(-1).view(np.int32)
+        parts.append((name, nwords[0], w, dt, a.shape))
+        nwords[0] += w.shape[0]
 
-    db = DeviceBatch(kind=meta.kind, num_seqs=S, num_tokens=T,
-                     input_ids=t(meta.input_ids, torch.int32),
-                     positions=t(meta.positions, torch.int32),
-                     slot_mapping=t(meta.slot_mapping, torch.int32),
-                     temperature=t(meta.temperature, torch.float32),
-                     top_k=t(meta.top_k, torch.int32), top_p=t(meta.top_p, torch.float32),
-                     seeds=t(meta.seeds, torch.int64))
+    add("input_ids", meta.input_ids, torch.int32)
+    add("positions", meta.positions, torch.int32)
+    add("slot_mapping", meta.slot_mapping, torch.int32)
+    add("temperature", meta.temperature, torch.float32)
+    add("top_k", meta.top_k, torch.int32)
+    add("top_p", meta.top_p, torch.float32)
+    add("seeds", meta.seeds, torch.int64)
+    nd = int(meta.num_decode) if meta.kind == PREFILL else 0
+    paged = False
     if meta.kind == PREFILL:
         lens = np.asarray(meta.seq_lens, dtype=np.int64)
         cu = np.zeros(S + 1, dtype=np.int32)
         cu[1:] = np.cumsum(lens)
-        db.cu_seqlens = t(cu, torch.int32)
+        add("cu_seqlens", cu, torch.int32)
+        add("last_token_idx", cu[1:] - 1, torch.int64)
+        paged = meta.block_tables is not None and np.shape(meta.block_tables)[1] > 0
+        if nd:
+            add("cu_seqlens_prefill", cu[nd:] - nd, torch.int32)
+    if meta.kind != PREFILL or paged:
+        add("block_tables", meta.block_tables, torch.int32)
+        add("context_lens", meta.context_lens, torch.int32)
+    buf = np.empty(max(1, nwords[0]), dtype=np.int32)
+    for _, o, w, _, _ in parts:
+        buf[o:o + w.shape[0]] = w
+    host = torch.from_numpy(buf)
+    if dev.type == "cuda":
+        if pin:
+            pinned = torch.empty(buf.shape, dtype=torch.int32, pin_memory=True)
+            pinned.numpy()[:] = buf
+            host = pinned
+        packed = host.to(dev, non_blocking=True)
+    else:
+        packed = host
+    v = {}
+    for name, o, w, dt, shape in parts:
+        x = packed[o:o + w.shape[0]]
+        if dt != torch.int32:
+            x = x.view(dt)
+        v[name] = x.view(shape) if len(shape) > 1 else x
+    db = DeviceBatch(kind=meta.kind, num_seqs=S, num_tokens=T,
+                     input_ids=v.get("input_ids"), positions=v.get("positions"),
+                     slot_mapping=v.get("slot_mapping"), temperature=v.get("temperature"),
+                     top_k=v.get("top_k"), top_p=v.get("top_p"), seeds=v.get("seeds"))
+    if meta.kind == PREFILL:
+        db.cu_seqlens = v["cu_seqlens"]
         db.max_seqlen = int(lens.max()) if S else 0
-        db.last_token_idx = t(cu[1:] - 1, torch.int64)
-        if meta.block_tables is not None and np.shape(meta.block_tables)[1] > 0:
+        db.last_token_idx = v["last_token_idx"]
+        if paged:
             # chunked prefill: queries attend over the paged cache (earlier chunks + this one)
-            db.block_tables = t(meta.block_tables, torch.int32)
-            db.context_lens = t(meta.context_lens, torch.int32)
+            db.block_tables = v["block_tables"]
+            db.context_lens = v["context_lens"]
             db.max_context = int(np.max(meta.context_lens)) if S else 0
-        nd = int(meta.num_decode)
         if nd:
             ctx = np.asarray(meta.context_lens)
             db.num_decode = nd
             db.max_context_decode = int(ctx[:nd].max())
-            db.cu_seqlens_prefill = t(cu[nd:] - nd, torch.int32)
+            db.cu_seqlens_prefill = v["cu_seqlens_prefill"]
             db.max_seqlen_prefill = int(lens[nd:].max()) if S > nd else 0
     else:
-        db.block_tables = t(meta.block_tables, torch.int32)
-        db.context_lens = t(meta.context_lens, torch.int32)
+        db.block_tables = v.get("block_tables")
+        db.context_lens = v.get("context_lens")
         db.max_context = int(np.max(meta.context_lens)) if S else 0
     return db

@@ -23,6 +23,7 @@ from .batch import DECODE, DeviceBatch, StepMeta, to_device
 from .kv_cache import KVCache
 
 DEFAULT_BUCKETS = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192, 256, 320, 384, 448, 512)
+HOST_RING = 4          # pinned metadata staging buffers per runner
 
 
 class StageRunner:
@@ -41,6 +42,12 @@ class StageRunner:
         self.buckets = sorted({b for b in buckets if b < max_batch} | {max_batch})
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_out: Dict[int, torch.Tensor] = {}
+        # pipeline data plane captured INTO the decode graphs (set_piped): pre(b) receives
+        # the bucket's input rows into hidden_in before the layers, post(b, out) sends the
+        # output after them, so a stage's decode tick is one H2D + one graph launch
+        self.piped = None
+        self.replays = 0
+        self.uploads = 0
         self._pool = None
         self.hidden_in = None
         if self.use_graphs:
@@ -62,9 +69,18 @@ class StageRunner:
             o += n
         self._nwords = o
         self.meta_dev = torch.zeros(o, dtype=torch.int32, device=self.device)
-        self.meta_host = torch.zeros(o, dtype=torch.int32).pin_memory()
-        self._host_np = self.meta_host.numpy()
-        self._upload_done = torch.cuda.Event()      # pinned buffer reuse guard
+        # a ring of pinned staging buffers: the host fills step k+1's metadata while step
+        # k's upload (stream-ordered behind step k's receive on a pipeline stage) is still
+        # pending; reusing a buffer waits only for the upload HOST_RING steps back, so a
+        # stage host runs up to HOST_RING - 1 ticks ahead of its GPU
+        self._ring = [torch.zeros(o, dtype=torch.int32).pin_memory() for _ in range(HOST_RING)]
+        self._ring_np = [t.numpy() for t in self._ring]
+        self._ring_ev = [torch.cuda.Event() for _ in range(HOST_RING)]
+        self._ring_used = [False] * HOST_RING
+        self._slot = 0
+        self.meta_host = self._ring[0]
+        self._host_np = self._ring_np[0]
+        self.host_waits = 0                          # fills that found their buffer busy
         self.hidden_in = None
         if not self.model.is_first:
             self.hidden_in = torch.zeros(B, self.model.cfg.hidden_size, dtype=torch.bfloat16,
@@ -93,7 +109,13 @@ class StageRunner:
                            seeds=self._view("seeds", b, torch.int64))
 
     def _fill_host(self, meta: StepMeta, b: int):
-        self._upload_done.synchronize()             # previous async H2D has consumed the buffer
+        j = self._slot = (self._slot + 1) % HOST_RING
+        if self._ring_used[j]:
+            ev = self._ring_ev[j]
+            if not ev.query():                       # its H2D (HOST_RING steps back) pending
+                self.host_waits += 1
+                ev.synchronize()
+        self.meta_host, self._host_np = self._ring[j], self._ring_np[j]
         h = self._host_np
         S = meta.num_seqs
 
@@ -130,13 +152,22 @@ class StageRunner:
         o, _ = self._off["tables"]
         n = o + b * self.W
         self.meta_dev[:n].copy_(self.meta_host[:n], non_blocking=True)
-        self._upload_done.record()
+        self.uploads += 1
+        self._ring_ev[self._slot].record()
+        self._ring_used[self._slot] = True
 
     def _bucket(self, S: int) -> int:
         for b in self.buckets:
             if b >= S:
                 return b
         raise ValueError(f"decode batch {S} exceeds max_batch {self.max_batch}")
+
+    def set_piped(self, pre, post) -> None:
+        """Capture ``pre(b)`` / ``post(b, out)`` (stream-ordered transport calls, e.g. the
+        IPC mailboxes) into every decode graph; graphs captured before are dropped."""
+        self.piped = (pre, post)
+        self.graphs.clear()
+        self.graph_out.clear()
 
     # ------------------------------------------------------------------ capture
     def _forward_static(self, b: int):
@@ -200,6 +231,7 @@ class StageRunner:
             if b in self.graphs:
                 continue
             # warmup: all rows padded (slot -1, ctx 0) -> no cache writes, no attention reads
+            torch.cuda.synchronize(self.device)      # no staged upload still reads the buffer
             h = self._host_np
             h[:] = 0
             for name, pad in (("slots", -1), ("topk", 1)):
@@ -218,7 +250,11 @@ class StageRunner:
             # its events while a stage captures; under the default global mode such a call
             # from another thread invalidates the capture (and aborts the watchdog)
             with torch.cuda.graph(g, pool=self._pool, capture_error_mode="thread_local"):
+                if self.piped is not None and self.piped[0] is not None:
+                    self.piped[0](b)
                 out = self._forward_static(b)
+                if self.piped is not None and self.piped[1] is not None:
+                    self.piped[1](b, out)
             if self._pool is None:
                 self._pool = g.pool()
             self.graphs[b] = g
@@ -255,9 +291,11 @@ class StageRunner:
             self._upload(b)
             if meta.feed_src is not None:
                 self._feed(self._view("ids", S), self._view("src", S), feed)
-            if self.hidden_in is not None and hidden.data_ptr() != self.hidden_in.data_ptr():
+            if (self.hidden_in is not None and hidden is not None
+                    and hidden.data_ptr() != self.hidden_in.data_ptr()):
                 self.hidden_in[:S].copy_(hidden[:S])
             self.graphs[b].replay()
+            self.replays += 1
             return self.graph_out[b][:S]
         db = to_device(meta, self.device)
         if meta.feed_src is not None:

@@ -134,6 +134,7 @@ class StageWorker:
         self.kv = KVCache(cfg, plan.end_layer - plan.start_layer, num_blocks, block_size,
                           self.device, dtype)
         self.runner = StageRunner(self.model, self.kv, max_batch, table_width, use_graphs)
+        self.tick_counts: Dict[int, int] = {}     # non-head ranks: steps run, by kind
 
     @property
     def is_last(self) -> bool:
@@ -439,7 +440,7 @@ class _StageBuffers:
         self.rx = ch.recv_buffer((stage.max_tokens, D))
         self.hf = (ch.recv_buffer((stage.max_batch, D))
                    if stage.vocab_parallel and not stage.is_last else None)
-        self.direct = ch.nccl or stage.device.type == "cpu"
+        self.direct = ch.nccl or stage.device.type == "cpu" or ch.ipc is not None
 
     def hidden_target(self, stage: StageWorker, meta: StepMeta) -> torch.Tensor:
         if self.direct:
@@ -453,15 +454,121 @@ class _StageBuffers:
         return self.rx[:T]
 
 
+def install_piped(stage: StageWorker, channel) -> bool:
+    """IPC data plane on a non-head GPU stage: capture the stage's receive (from r - 1) and
+    send (to r + 1; on a tail without the vocab-parallel head, its sampled tokens to rank 0)
+    INTO its decode graphs, so a decode tick costs one metadata H2D + one graph launch. The
+    mailbox semaphores inside a captured graph are wait / signal kernels
+    (csrc/runtime/ipc.cpp), which replay correctly because no sequence number is baked in."""
+    r, N = channel.rank, channel.world
+    run = stage.runner
+    if (channel.ipc is None or r == 0 or not run.use_graphs or run.hidden_in is None
+            or os.environ.get("DLI_PP_PIPED_GRAPHS", "1") != "1"):
+        return False
+    tail = r == N - 1
+    if tail and stage.vocab_parallel:
+        post = None                  # its per-step output (hf / fallback tokens) goes eagerly
+    elif tail:
+        def post(b, out):
+            channel.exchange([(out[:b], 0, 2)], [])
+    else:
+        def post(b, out):
+            channel.exchange([(out[:b], r + 1, 1)], [])
+
+    def pre(b):
+        channel.exchange([], [(run.hidden_in[:b], r - 1, 1)])
+    run.set_piped(pre, post)
+    return True
+
+
+def _serve_session_piped(stage: StageWorker, channel, bufs: _StageBuffers) -> int:
+    """``serve_session`` on the mailbox data plane (FIFO per edge, one message buffered per
+    edge): tick k = [side messages: this rank's candidates -> 0, the tail's deferred output;
+    the tail's final hidden <- N-1] then [receive x <- r-1, layers, send -> r+1] — the second
+    bracket is ONE graph replay on decode ticks (``install_piped``), the same three
+    operations issued eagerly on prefill ticks. Every wait depends on an earlier tick of a
+    peer, so the schedule cannot deadlock; the tag-blind CPU model of the mailboxes
+    (``fifo.py``) runs it at N = 2..8 in tests/test_fifo_transport.py."""
+    r, N, k = channel.rank, channel.world, 0
+    tail = r == N - 1
+    run = stage.runner
+    counts = stage.tick_counts
+    metas: Dict[int, Tuple[StepMeta, bool]] = {}
+    prev_out = None                 # tail + vocab-parallel head: my output of tick k-1
+    prev_vp = False
+    my_cand = None
+    while True:
+        if faults.active():
+            faults.check("pipeline.stage", tick=k)
+        meta = None
+        if k >= r:
+            h, p = channel.recv_ctrl()
+            kind = int(h[0])
+            if kind in (STOP, SHUTDOWN):
+                channel.flush()
+                return kind
+            if kind in (PREFILL, DECODE):
+                meta = StepMeta.unpack(h, p)
+                metas[k - r] = (meta, bool(h[H_VP]))
+        ret = metas.get(k - N)
+        smp = metas.get(k - 1 - N)
+        sends, recvs = [], []
+        if tail and prev_out is not None:
+            sends += ([(prev_out, q, 2) for q in range(N - 1)] if prev_vp
+                      else [(prev_out, 0, 2)])
+        if smp is not None and smp[1] and my_cand is not None:
+            sends.append((my_cand, 0, 3))
+        hf = None
+        if ret is not None and ret[1] and not tail:
+            hf = bufs.hf[:ret[0].num_seqs]
+            recvs.append((hf, N - 1, 2))
+        if sends or recvs:
+            channel.exchange(sends, recvs)
+        cand_now = None
+        if ret is not None and ret[1]:
+            cand_now = stage.candidates(prev_out if tail else hf)
+        my_cand = cand_now
+        prev_out, prev_vp = None, False
+        if meta is not None:
+            counts[meta.kind] = counts.get(meta.kind, 0) + 1
+            vp_m = metas[k - r][1]
+            if run.piped is not None and run.input_buffer(meta) is not None:
+                out = stage.compute(meta, None)            # receive + layers + send: 1 graph
+                if tail and stage.vocab_parallel:
+                    if not vp_m:
+                        out = stage.tokens_full(meta, out)
+                    prev_out, prev_vp = out, vp_m
+            else:
+                x = bufs.rx[:meta.num_tokens]
+                if x.shape[0] < meta.num_tokens:
+                    raise ValueError(f"step of {meta.num_tokens} tokens exceeds the stage "
+                                     f"receive buffer ({bufs.rx.shape[0]})")
+                channel.exchange([], [(x, r - 1, 1)])
+                out = stage.compute(meta, x)
+                if tail and not vp_m and stage.vocab_parallel:
+                    out = stage.tokens_full(meta, out)
+                if not tail:
+                    channel.exchange([(out, r + 1, 1)], [])
+                elif not stage.vocab_parallel:
+                    channel.exchange([(out, 0, 2)], [])
+                else:
+                    prev_out, prev_vp = out, vp_m
+        for old in [t for t in metas if t < k - 1 - N]:
+            del metas[old]
+        k += 1
+
+
 def serve_session(stage: StageWorker, channel, bufs: Optional[_StageBuffers] = None) -> int:
     """Non-head rank r: every tick of one head session; returns STOP or SHUTDOWN.
     Tick k: layers of the microbatch started at k - r (control message k - r, received in
     order), with the vocab-parallel head also the candidates of microbatch k - N; the tail
     returns either its final hidden (to every rank) or its sampled tokens (to rank 0). The
     host never waits on this GPU: receives, replays and sends are all stream-ordered."""
+    bufs = bufs or _StageBuffers(stage, channel)
+    if channel.ipc is not None:
+        return _serve_session_piped(stage, channel, bufs)
     r, N, k = channel.rank, channel.world, 0
     tail = r == N - 1
-    bufs = bufs or _StageBuffers(stage, channel)
     metas: Dict[int, Tuple[StepMeta, bool]] = {}
     prev_out = None                 # my layer output of tick k-1 (hidden / tokens / final hidden)
     prev_vp = False
@@ -656,6 +763,7 @@ class DistributedPipelineEngine:
         self._ids = 0
 
     def warmup(self):
+        install_piped(self.stage, self.channel)
         self.stage.runner.capture()
 
     def add_request(self, prompt, params: Optional[SamplingParams] = None, request_id=None):

@@ -100,8 +100,9 @@ class PipeChannel:
             # every rank joins one grouped ring exchange up front, so whatever point-to-point
             # communicator state RCCL builds lazily is built with all ranks present (the
             # session's first exchanges involve only some ranks)
-            t = torch.full((1,), float(self.rank), device=self.data_device)
-            r = torch.empty(1, device=self.data_device)
+            ck = self.device if dist.get_backend() == "nccl" else torch.device("cpu")
+            t = torch.full((1,), float(self.rank), device=ck)
+            r = torch.empty(1, device=ck)
             for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, t, self.next),
                                              dist.P2POp(dist.irecv, r, self.prev)]):
                 w.wait()

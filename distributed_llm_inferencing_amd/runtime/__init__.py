@@ -86,6 +86,7 @@ _SIGS = {
     "dli_ipc_pending": ([_P, _I], _LL),
     "dli_ipc_abort": ([_P, ctypes.c_double], _I),
     "dli_ipc_stats": ([_P, _P], None),
+    "dli_ipc_error": ([_P], _I),
     "dli_ipc_host_flags": ([_P], _I),
     "dli_ipc_destroy": ([_P], None),
 }
@@ -579,6 +580,10 @@ class IpcEndpoint:
         r = lib().dli_ipc_abort(self._h, float(timeout_s))
         if r != 0:
             raise RuntimeError(f"IPC abort failed ({r})")
+
+    def error(self) -> bool:
+        """A captured wait ran out of its budget (DLI_IPC_WAIT_S): a peer stopped."""
+        return lib().dli_ipc_error(self._h) == 1
 
     def stats(self) -> Dict[str, int]:
         out = (ctypes.c_longlong * 3)()

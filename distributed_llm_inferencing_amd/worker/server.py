@@ -42,7 +42,7 @@ from ..models.configs import get_config
 from ..shard.writer import load_shard, read_metadata, stage_plan_from_metadata
 from ..utils import faults
 from ..utils.log import setup_logging
-from .service import EngineService
+from .service import EngineService, PipelineFailed
 
 log = logging.getLogger("dli.worker")
 
@@ -183,6 +183,8 @@ class WorkerState:
                     return False
                 raise ValueError(f"this worker already serves stage {self.pipeline['rank']} "
                                  f"of {self.pipeline['model_name']}")
+            if self.pipeline is not None:           # failed / stopped: re-form from scratch
+                self._clear_pipeline()
             self.pipeline = {"model_name": name, "rank": shard_id, "world_size": world,
                              "init_method": init_method, "state": "joining", "error": None}
         shard_dir = os.path.dirname(path.rstrip("/"))
@@ -220,7 +222,8 @@ class WorkerState:
                                                                 f"shard_{p.shard_id}"),
                                                    name, p.shard_id)}
                         for p in eng.plans]
-                    self.pipeline_service = PipelineService(eng, name=name.replace("/", "_"))
+                    self.pipeline_service = PipelineService(
+                        eng, name=name.replace("/", "_"), on_failure=self._pipeline_failed)
                     self.pipeline_model = name
                     rec["state"] = "serving"
                 return
@@ -245,6 +248,60 @@ class WorkerState:
                     dist.destroy_process_group()
             except Exception as e2:  # noqa: BLE001
                 log.warning("pipeline teardown after a failed join: %s", e2)
+
+    def _abort_ring(self, eng) -> None:
+        """Tear down a broken ring's transports + process group without a goodbye: IPC
+        mailboxes are released (a queue blocked on a dead peer drains), RCCL communicators
+        are aborted rather than destroyed (a destroy would wait on the dead rank)."""
+        import torch.distributed as dist
+        ch = getattr(eng, "channel", None) if eng is not None else None
+        ipc = getattr(ch, "ipc", None)
+        if ipc is not None and hasattr(ipc, "abort"):
+            try:
+                ipc.abort()
+            except Exception as e:  # noqa: BLE001
+                log.warning("ipc abort: %s", e)
+        try:
+            if ch is not None:
+                ch.close()
+        except Exception as e:  # noqa: BLE001
+            log.warning("channel close after a ring failure: %s", e)
+        if dist.is_initialized():
+            try:
+                if dist.get_backend() == "nccl":
+                    from torch.distributed.distributed_c10d import _abort_process_group
+                    _abort_process_group()
+                else:
+                    dist.destroy_process_group()
+            except Exception as e:  # noqa: BLE001
+                log.warning("process group teardown after a ring failure: %s", e)
+
+    def _pipeline_failed(self, err) -> None:
+        """Head's session raised (PipelineService.on_failure): abort the ring, keep serving
+        503s (the service keeps its error) until a new pipeline spec re-forms it."""
+        log.error("pipeline %s failed: %s", getattr(self, "pipeline_model", None), err)
+        with self.lock:
+            self._abort_ring(self._pipe_engine)
+            self._pipe_engine = None
+            if self.pipeline is not None:
+                self.pipeline["state"], self.pipeline["error"] = "failed", str(err)
+        if self.device.type == "cuda":
+            torch.cuda.empty_cache()
+
+    def _clear_pipeline(self) -> None:
+        """Forget a failed / stopped ring before joining a new one."""
+        svc = getattr(self, "pipeline_service", None)
+        if svc is not None:
+            svc.close()
+        if self._pipe_engine is not None:
+            self._abort_ring(self._pipe_engine)
+        self.pipeline_service = None
+        self.pipeline_model = None
+        self.pipeline_shards = []
+        self._pipe_engine = None
+        self.pipeline = None
+        if self.device.type == "cuda":
+            torch.cuda.empty_cache()
 
     def _leave_pipeline(self):
         """Rank 0: unload of the pipeline model shuts the whole ring down."""
@@ -382,13 +439,17 @@ def create_worker_app(settings: Optional[Settings] = None, device: Optional[str]
         except faults.InjectedFault as e:
             return jsonify({"status": "error", "message": str(e)}), 503
         psvc = getattr(st, "pipeline_service", None)
-        if psvc is not None and psvc.error is not None:      # a stage of this ring died
+        if psvc is not None and getattr(psvc, "error", None) is not None:   # a stage died
             return jsonify({"status": "error",
                             "message": f"pipeline failed: {psvc.error}"}), 503
         shard_info = [{"model_name": m, "shard_id": sid, "path": r["path"],
                        "metadata": r["metadata"]}
                       for m, sh in st.shards.items() for sid, r in sh.items()]
-        shard_info += getattr(st, "pipeline_shards", None) or []
+        if os.environ.get("DLI_REPORT_PIPELINE_SHARDS", "1") == "1":
+            # a ring's head reports every stage as its shard (the master routes the model
+            # here); DP replicas of one model run with 0, as plain nodes the dispatcher
+            # balances (the reference's ModelShard rows are unique per (model, shard))
+            shard_info += getattr(st, "pipeline_shards", None) or []
         extra = {"pipeline": st.pipeline} if st.pipeline is not None else {}
         return jsonify({"status": "healthy", "resources": st.resources(), **extra,
                         "loaded_models": list(st.services.keys()),
@@ -466,7 +527,13 @@ def create_worker_app(settings: Optional[Settings] = None, device: Optional[str]
             if svc is not None and name == getattr(st, "pipeline_model", None):
                 # pipeline head (serve-pipeline / one DP replica of serve-cluster): every
                 # stage of this model runs on this rank's pipeline, with or without shard_ids
-                out = svc.generate(prompt, params, timeout=timeout + 30)
+                if getattr(svc, "error", None) is not None:   # broken ring: next replica retries
+                    return jsonify({"status": "error",
+                                    "message": f"pipeline failed: {svc.error}"}), 503
+                try:
+                    out = svc.generate(prompt, params, timeout=timeout + 30)
+                except PipelineFailed as e:
+                    return jsonify({"status": "error", "message": str(e)}), 503
             elif (st.pipeline is not None and st.pipeline["model_name"] == name
                   and st.pipeline["rank"] != 0):
                 return jsonify({"status": "error",

@@ -102,18 +102,26 @@ class EngineService:
         self._t.join(5)
 
 
+class PipelineFailed(RuntimeError):
+    """The request's pipeline ring broke (a stage died): retryable on another replica."""
+
+
 class PipelineService:
     """Same interface, backed by the rank-0 head of a DistributedPipelineEngine: a ring
     session runs while there is work, and requests join it at tick boundaries.
 
     A session that raises (a stage died, a link failed, the data-plane timeout fired) leaves
     the ring unusable: every pending and later request fails at once with that error, and
-    ``error`` is set so the worker's /health reports the node unhealthy (the master's failure
-    detector then takes it out of rotation) instead of hanging requests on a broken ring."""
+    ``error`` is set so the worker's /health and /inference answer 503 (the master's
+    dispatcher re-sends the request to another replica, its failure detector takes the node
+    out of rotation) instead of hanging requests on a broken ring. ``on_failure`` (the
+    worker) then aborts the communicator; the process stays up and a new ``/load_shard``
+    pipeline spec re-forms the ring with restarted or spare stage workers."""
 
-    def __init__(self, pipe_engine, name: str = "pipeline"):
+    def __init__(self, pipe_engine, name: str = "pipeline", on_failure=None):
         self.engine = pipe_engine
         self.name = name
+        self.on_failure = on_failure
         self._inbox: "queue.Queue[tuple]" = queue.Queue()
         self._stop = threading.Event()
         self._ids = 0
@@ -128,7 +136,7 @@ class PipelineService:
     def submit(self, prompt, params=None) -> Future:
         fut: Future = Future()
         if self.error is not None:
-            fut.set_exception(RuntimeError(f"pipeline {self.name} failed: {self.error}"))
+            fut.set_exception(PipelineFailed(f"pipeline {self.name} failed: {self.error}"))
             return fut
         with self._lock:
             self._ids += 1
@@ -138,14 +146,14 @@ class PipelineService:
 
     def _fail_pending(self):
         if self._carry is not None:
-            self._carry[3].set_exception(RuntimeError(f"pipeline {self.name} failed: {self.error}"))
+            self._carry[3].set_exception(PipelineFailed(f"pipeline {self.name} failed: {self.error}"))
             self._carry = None
         while True:
             try:
                 _rid, _p, _s, fut = self._inbox.get_nowait()
             except queue.Empty:
                 return
-            fut.set_exception(RuntimeError(f"pipeline {self.name} failed: {self.error}"))
+            fut.set_exception(PipelineFailed(f"pipeline {self.name} failed: {self.error}"))
 
     def generate(self, prompt, params=None, timeout=None):
         return self.submit(prompt, params).result(timeout=timeout)
@@ -187,13 +195,19 @@ class PipelineService:
                 # it at the next tick; each finished request is answered the tick it finishes
                 head.run_session(admit=self._admit, on_finished=self._resolve)
                 self.sessions += 1
-            except BaseException as e:  # noqa: BLE001 — the ring is broken: fail fast, for good
+            except BaseException as e:  # noqa: BLE001 — the ring is broken: fail fast
                 self.error = e
+                err = PipelineFailed(f"pipeline {self.name} failed: {e}")
                 for f in self._futs.values():
                     if not f.done():
-                        f.set_exception(e)
+                        f.set_exception(err)
                 self._futs.clear()
                 self._fail_pending()
+                if self.on_failure is not None:
+                    try:
+                        self.on_failure(e)
+                    except Exception:  # noqa: BLE001
+                        pass
                 return
 
     def stats(self) -> dict:

@@ -37,6 +37,10 @@ def _pp_worker(rank, world, port, q, vp, comm="torch"):
     from distributed_llm_inferencing_amd.parallel.pipeline import DistributedPipelineEngine
     eng = DistributedPipelineEngine("llama-tiny", "cuda", max_batch=8, max_model_len=64,
                                     num_blocks=256)
+    x0 = 0
+    if comm == "ipc":
+        eng.warmup()                  # captures the receive / send into the decode graphs
+        x0 = eng.channel.exchanges    # captured calls counted once, at capture
     if rank == 0:
         res = [[o.all_ids for o in eng.generate(PROMPTS, sp)] for sp in (GREEDY, SAMPLED)]
         res.append(eng.vocab_parallel)
@@ -45,6 +49,11 @@ def _pp_worker(rank, world, port, q, vp, comm="torch"):
         q.put(res)
     else:
         eng.serve()
+        from distributed_llm_inferencing_amd.engine.batch import DECODE, PREFILL
+        run = eng.stage.runner
+        q.put(("stage", rank, run.piped is not None, run.replays, run.uploads,
+               eng.stage.tick_counts.get(DECODE, 0), eng.stage.tick_counts.get(PREFILL, 0),
+               eng.channel.exchanges - x0))
     dist.barrier()
     eng.channel.close()
     dist.destroy_process_group()
@@ -58,7 +67,7 @@ def _run(target, world, *args):
     for p in procs:
         p.start()
     try:
-        n = world if target is _ep_worker else 1
+        n = world if (target is _ep_worker or "ipc" in args) else 1
         res = [q.get(timeout=240) for _ in range(n)]
     finally:
         for p in procs:
@@ -87,13 +96,24 @@ def test_pipeline_two_ranks_on_gpu_match_single_stage(gpu, vp):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("world,vp", [(2, "0"), (2, "1"), (4, "1")])
+@pytest.mark.parametrize("world,vp", [(2, "0"), (2, "1"), (4, "0"), (4, "1")])
 def test_pipeline_over_ipc_mailboxes_on_gpu(gpu, world, vp):
     """The device data plane with N ranks on ONE GPU: every activation / token / candidate
     message goes through hipIpc-mapped mailboxes (stream-ordered copies +
     hipStreamWaitValue64 / WriteValue64 semaphores, csrc/runtime/ipc.cpp), token-identical
     to the single-stage engine."""
-    (res,) = _run(_pp_worker, world, vp, "ipc")
+    out = _run(_pp_worker, world, vp, "ipc")
+    (res,) = [x for x in out if x[0] != "stage"]
+    stages = [x for x in out if x[0] == "stage"]
+    assert len(stages) == world - 1
+    for _, rank, piped, replays, uploads, dec, pre, exch in stages:
+        assert piped                                  # receive/send captured in the graphs
+        # one metadata H2D + one graph launch per decode tick, nothing else on the data
+        # plane: the only eager exchanges are the prefill ticks' receive + send (and the
+        # vocab-parallel side messages on the tail / candidates)
+        assert replays == dec and uploads == dec and dec > 0, (rank, replays, uploads, dec)
+        if vp == "0":
+            assert exch <= 2 * pre + 1, (rank, exch, pre)
     os.environ["DLI_GEMM_AUTOTUNE"] = "0"
     try:
         eng = LLMEngine("llama-tiny", device="cuda", max_batch=8, max_model_len=64,
