@@ -84,6 +84,65 @@ __global__ void __launch_bounds__(256) ipc_copy_kernel(uint4* __restrict__ dst,
   if (blockIdx.x == 0 && (int)threadIdx.x < ntail) dtail[threadIdx.x] = stail[threadIdx.x];
 }
 
+// ---- expert-parallel all-to-all on the mailboxes: row counts live on the device -------
+// A dispatch message on edge s -> p is [int64 count | 16-B pad | ids int32 x cap | rows x
+// row_bytes] (return messages use the same offsets, no ids). Only `count` rows move; the
+// grid is sized for the mailbox capacity and threads past the count exit, so no routing
+// value is ever read on the host and the whole exchange can be captured in a graph.
+__device__ __forceinline__ long ep_ids_off() { return 16; }
+__device__ __forceinline__ long ep_rows_off(int cap) {
+  return 16 + (((long)cap * 4 + 15) / 16) * 16;
+}
+
+__global__ void __launch_bounds__(256) ep_put_kernel(uint8_t* __restrict__ mbox, int cap,
+                                                     const int* __restrict__ count,
+                                                     const uint4* __restrict__ x, int row16,
+                                                     const int* __restrict__ ids) {
+  const int n = min(*count, cap);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *reinterpret_cast<long long*>(mbox) = n;
+  int* mid = reinterpret_cast<int*>(mbox + ep_ids_off());
+  uint4* mrow = reinterpret_cast<uint4*>(mbox + ep_rows_off(cap));
+  const long stride = (long)gridDim.x * blockDim.x;
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (ids != nullptr)
+    for (long i = tid; i < n; i += stride) mid[i] = ids[i];
+  const long total = (long)n * row16;
+  for (long i = tid; i < total; i += stride) mrow[i] = x[i];
+}
+
+__global__ void __launch_bounds__(256) ep_get_kernel(const uint8_t* __restrict__ mbox, int cap,
+                                                     uint4* __restrict__ x, int row16,
+                                                     int* __restrict__ ids, int fill,
+                                                     int* __restrict__ count_out) {
+  const int n = (int)min(*reinterpret_cast<const long long*>(mbox), (long long)cap);
+  const int* mid = reinterpret_cast<const int*>(mbox + ep_ids_off());
+  const uint4* mrow = reinterpret_cast<const uint4*>(mbox + ep_rows_off(cap));
+  const long stride = (long)gridDim.x * blockDim.x;
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (count_out != nullptr && tid == 0) *count_out = n;
+  if (ids != nullptr)
+    for (long i = tid; i < fill; i += stride) ids[i] = i < n ? mid[i] : -1;
+  const long total = (long)n * row16;
+  for (long i = tid; i < total; i += stride) x[i] = mrow[i];
+}
+
+// the rank's own bucket: send region -> receive region (ids -1 past the count)
+__global__ void __launch_bounds__(256) ep_local_kernel(const int* __restrict__ count,
+                                                       const uint4* __restrict__ xs, int row16,
+                                                       const int* __restrict__ ids_s,
+                                                       uint4* __restrict__ xd,
+                                                       int* __restrict__ ids_d, int fill,
+                                                       int* __restrict__ count_out) {
+  const int n = *count;
+  const long stride = (long)gridDim.x * blockDim.x;
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (count_out != nullptr && tid == 0) *count_out = n;
+  if (ids_d != nullptr)
+    for (long i = tid; i < fill; i += stride) ids_d[i] = i < n ? ids_s[i] : -1;
+  const long total = (long)n * row16;
+  for (long i = tid; i < total; i += stride) xd[i] = xs[i];
+}
+
 // Semaphore waits / signals as kernels, used while a stream is being captured into a
 // hipGraph (stream write/wait-value operations captured into a graph were measured to lose
 // their ordering against the copy kernels on replay: profiles/r3/ipc_probe_*.jsonl, check
@@ -402,6 +461,135 @@ int dli_ipc_exchange(void* h, void* stream, int n_send, void* const* send_ptrs,
     e->recvs++;
   }
   return r;
+}
+
+// Expert-parallel dispatch (ret = 0) or return (ret = 1) over the mailboxes, enqueued on
+// `stream`. Rows are row_bytes long (a multiple of 16).
+//   dispatch: the rows for peer p are send_x + send_base[p] rows (count on the device at
+//     send_cnt[p], global expert ids at send_e + send_base[p]); the rows from source q land
+//     in recv_x + recv_base[q] rows (region capacity recv_cap[q]; ids -> recv_e +
+//     recv_base[q], -1 past the count; count -> recv_cnt[q] on the device).
+//   return: the roles swap: the recv_cnt[q] result rows at recv_x + recv_base[q] go back to
+//     q, and peer p's results for my rows land at send_x + send_base[p] (no ids).
+// cap_rows[p] / in_cap_rows[q]: capacity in rows of the mailbox of edge me -> p / q -> me
+// (sized by the caller with dli_ipc_ep_bytes).
+int dli_ipc_ep(void* h, void* stream, int ret, int row_bytes, void* send_x, int* send_e,
+               const int* send_base, int* send_cnt, void* recv_x, int* recv_e,
+               const int* recv_base, const int* recv_cap, int* recv_cnt, const int* cap_rows,
+               const int* in_cap_rows) {
+  auto* e = E(h);
+  auto s = (hipStream_t)stream;
+  const int W = e->world, me = e->rank;
+  const int row16 = row_bytes / 16;
+  if (row_bytes % 16) return -1006;
+  auto ep_bytes = [&](long cap) { return 16 + (cap * 4 + 15) / 16 * 16 + cap * row_bytes; };
+  for (int p = 0; p < W; ++p) {
+    if (p == me) continue;
+    const Edge& g = e->edge[p];
+    if (g.peer_mailbox == nullptr || g.my_mailbox == nullptr) return -1003;
+    if (ep_bytes(cap_rows[p]) > g.out_bytes || ep_bytes(in_cap_rows[p]) > g.in_bytes)
+      return -1003;
+  }
+  bool kern = e->sync_mode == 1;
+  if (!kern) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive)
+      kern = true;
+  }
+  auto wait = [&](uint64_t* w) -> int {
+    if (kern) {
+      ipc_wait_kernel<<<1, 64, 0, s>>>(w, e->err_word, e->wait_budget);
+      return herr(hipGetLastError());
+    }
+    int r = herr(hipStreamWaitValue64(s, w, 1, hipStreamWaitValueEq));
+    return r ? r : herr(hipStreamWriteValue64(s, w, 0, 0));
+  };
+  auto signal = [&](uint64_t* w) -> int {
+    if (kern) {
+      ipc_signal_kernel<<<1, 64, 0, s>>>(w);
+      return herr(hipGetLastError());
+    }
+    return herr(hipStreamWriteValue64(s, w, 1, 0));
+  };
+  auto blocks = [&](long rows) {
+    long b = (rows * row16 + 4 * 256 - 1) / (4 * 256);
+    return (unsigned)(b < 1 ? 1 : (b > 2048 ? 2048 : b));
+  };
+  auto* sx = reinterpret_cast<uint8_t*>(send_x);
+  auto* rx = reinterpret_cast<uint8_t*>(recv_x);
+  const long rb = row_bytes;
+  int r = 0;
+  if (!ret) {
+    for (int p = 0; p < W && r == 0; ++p) {
+      if (p == me) continue;
+      const Edge& g = e->edge[p];
+      r = wait(g.my_free);
+      if (r) break;
+      ep_put_kernel<<<blocks(cap_rows[p]), 256, 0, s>>>(
+          g.peer_mailbox, cap_rows[p], send_cnt + p,
+          reinterpret_cast<const uint4*>(sx + (long)send_base[p] * rb), row16,
+          send_e + send_base[p]);
+      r = herr(hipGetLastError());
+      if (!r) r = signal(g.peer_ready);
+      e->sends++;
+    }
+    if (r == 0) {
+      ep_local_kernel<<<blocks(recv_cap[me]), 256, 0, s>>>(
+          send_cnt + me, reinterpret_cast<const uint4*>(sx + (long)send_base[me] * rb), row16,
+          send_e + send_base[me], reinterpret_cast<uint4*>(rx + (long)recv_base[me] * rb),
+          recv_e + recv_base[me], recv_cap[me], recv_cnt + me);
+      r = herr(hipGetLastError());
+    }
+    for (int q = 0; q < W && r == 0; ++q) {
+      if (q == me) continue;
+      const Edge& g = e->edge[q];
+      r = wait(g.my_ready);
+      if (r) break;
+      ep_get_kernel<<<blocks(recv_cap[q]), 256, 0, s>>>(
+          g.my_mailbox, in_cap_rows[q], reinterpret_cast<uint4*>(rx + (long)recv_base[q] * rb),
+          row16, recv_e + recv_base[q], recv_cap[q], recv_cnt + q);
+      r = herr(hipGetLastError());
+      if (!r) r = signal(g.peer_free);
+      e->recvs++;
+    }
+    return r;
+  }
+  for (int q = 0; q < W && r == 0; ++q) {
+    if (q == me) continue;
+    const Edge& g = e->edge[q];
+    r = wait(g.my_free);
+    if (r) break;
+    ep_put_kernel<<<blocks(recv_cap[q]), 256, 0, s>>>(
+        g.peer_mailbox, cap_rows[q], recv_cnt + q,
+        reinterpret_cast<const uint4*>(rx + (long)recv_base[q] * rb), row16, nullptr);
+    r = herr(hipGetLastError());
+    if (!r) r = signal(g.peer_ready);
+    e->sends++;
+  }
+  if (r == 0) {
+    ep_local_kernel<<<blocks(recv_cap[me]), 256, 0, s>>>(
+        recv_cnt + me, reinterpret_cast<const uint4*>(rx + (long)recv_base[me] * rb), row16,
+        nullptr, reinterpret_cast<uint4*>(sx + (long)send_base[me] * rb), nullptr, 0, nullptr);
+    r = herr(hipGetLastError());
+  }
+  for (int p = 0; p < W && r == 0; ++p) {
+    if (p == me) continue;
+    const Edge& g = e->edge[p];
+    r = wait(g.my_ready);
+    if (r) break;
+    ep_get_kernel<<<blocks(in_cap_rows[p]), 256, 0, s>>>(
+        g.my_mailbox, in_cap_rows[p], reinterpret_cast<uint4*>(sx + (long)send_base[p] * rb),
+        row16, nullptr, 0, nullptr);
+    r = herr(hipGetLastError());
+    if (!r) r = signal(g.peer_free);
+    e->recvs++;
+  }
+  return r;
+}
+
+// Mailbox bytes an expert-parallel edge of `cap_rows` rows needs.
+long long dli_ipc_ep_bytes(int cap_rows, int row_bytes) {
+  return 16 + ((long long)cap_rows * 4 + 15) / 16 * 16 + (long long)cap_rows * row_bytes;
 }
 
 // Host flag mode: 1 when a message from `peer` sits in my mailbox, not yet taken by my queue

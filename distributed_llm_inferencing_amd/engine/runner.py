@@ -46,6 +46,7 @@ class StageRunner:
         # the bucket's input rows into hidden_in before the layers, post(b, out) sends the
         # output after them, so a stage's decode tick is one H2D + one graph launch
         self.piped = None
+        self.force_eager = False        # lockstep users (EP): run this step's decode eagerly
         self.replays = 0
         self.uploads = 0
         self._pool = None
@@ -282,7 +283,8 @@ class StageRunner:
         ``feed``: the in-flight step's token output, read where ``meta.feed_src`` says."""
         if meta.feed_src is not None and feed is None:
             raise ValueError("step has lookahead rows but no in-flight output to feed them")
-        if meta.kind == DECODE and self.use_graphs and meta.num_seqs <= self.max_batch:
+        if (meta.kind == DECODE and self.use_graphs and meta.num_seqs <= self.max_batch
+                and not self.force_eager):
             S = meta.num_seqs
             b = self._bucket(S)
             if b not in self.graphs:

@@ -485,10 +485,11 @@ def moe_mlp(x, w_gu, w_down, topk_w, topk_ids, expert_offset: int = 0):
     return out
 
 
-def ep_pack(x, topk_ids, e_per: int, base, send_rows: int):
+def ep_pack(x, topk_ids, e_per: int, base, send_rows: int, counts: bool = False):
     """Expert-parallel dispatch: (token, pick) rows into per-destination-rank buckets
     starting at ``base[dest]`` (int32 [N] on the device). Returns (send_x [send_rows, D],
-    send_e int32 [send_rows] global expert id or -1, pos int32 [T, k] row of each pick)."""
+    send_e int32 [send_rows] global expert id or -1, pos int32 [T, k] row of each pick)
+    and, with ``counts``, the rows per destination (int32 [N] on the device)."""
     T, D = x.shape
     k = topk_ids.shape[1]
     dev = x.device
@@ -508,10 +509,15 @@ def ep_pack(x, topk_ids, e_per: int, base, send_rows: int):
                 pos[t, j] = p
                 send_e[p] = ids[t][j]
                 send_x[p] = x[t]
+        if counts:
+            return send_x, send_e, pos, torch.tensor(fill, dtype=torch.int32)
         return send_x, send_e, pos
     fill = torch.zeros(base.shape[0], dtype=torch.int32, device=dev)
-    _native_call("dli_ep_pack", _p(send_x), _p(send_e), _p(pos), _p(fill), _p(base), _p(x),
-                 _p(topk_ids), T, k, D, e_per, _st())
+    if T > 0:
+        _native_call("dli_ep_pack", _p(send_x), _p(send_e), _p(pos), _p(fill), _p(base), _p(x),
+                     _p(topk_ids), T, k, D, e_per, _st())
+    if counts:
+        return send_x, send_e, pos, fill
     return send_x, send_e, pos
 
 

@@ -45,7 +45,17 @@ EP_BOUND_MAX_TOKENS = int(os.environ.get("DLI_EP_BOUND_MAX_TOKENS", "1024"))
 
 
 class ExpertParallelMoE:
-    """Installed as ``TransformerLM.moe_fn`` on every rank."""
+    """Installed as ``TransformerLM.moe_fn`` on every rank.
+
+    Two data planes. ``torch``: three ``all_to_all_single`` per layer over fixed-capacity
+    buckets (below). ``ipc`` (``DLI_EP_COMM=ipc``): the mailbox transport
+    (``csrc/runtime/ipc.cpp`` ``dli_ipc_ep``; on CPU its host model in ``fifo.py``). The
+    per-destination row counts produced by ``ep_pack`` stay on the device and travel in each
+    message's header; the copy kernels move exactly the routed rows (no padding on the
+    wire) into the peer's mailbox, and the peer's expert rows come back the same way. No
+    host value is needed per layer, so the decode forward (attention + every MoE exchange)
+    is captured in one hipGraph per batch bucket; the only host sync per step is the
+    lockstep exchange."""
 
     def __init__(self, num_experts: int, top_k: int, group=None):
         self.group = group
@@ -62,9 +72,98 @@ class ExpertParallelMoE:
         self.host_reads = 0                            # routing-dependent host syncs
         self.peer_tokens: Optional[List[int]] = None   # T of every rank for this step
         self._bases = {}
+        self.ep = None                 # mailbox endpoint (setup_ipc)
+        self.static = False            # capturing / replaying graphs: fixed region sizes
+        self.graph_tokens = 0          # largest decode batch per rank (graph regions)
+        self.rows_sent = 0             # rows this rank sent to other ranks (dispatch)
+        self.rows_routed = 0           # routed (token, pick) rows produced on this rank
 
     def expert_range(self):
         return (self.e0, self.e0 + self.e_per)
+
+    def setup_ipc(self, device, dim: int, dtype, max_tokens: int, graph_tokens: int) -> None:
+        """Mailboxes for every ordered pair of ranks, each holding one layer's worth of rows
+        from a step of up to ``max_tokens`` tokens (``min(k, E/N)`` rows per token)."""
+        from .fifo import ShmMailboxTransport
+        N, me = self.world, self.rank
+        self.row_bytes = dim * torch.empty(0, dtype=dtype).element_size()
+        self.cap = max_tokens * self.per_token
+        self.graph_tokens = graph_tokens
+        dev = torch.device(device)
+        if dev.type == "cuda":
+            from ..runtime import IpcEndpoint
+            eb = IpcEndpoint.ep_bytes(self.cap, self.row_bytes)
+        else:
+            eb = 8 + 8 + self.cap * 4 + self.cap * self.row_bytes + 64
+        cap = [[0 if s == d else eb for d in range(N)] for s in range(N)]
+        box = [f"/dli_ep_{os.environ.get('MASTER_PORT', '0')}_{os.getpid()}"
+               if me == 0 else None]
+        dist.broadcast_object_list(box, src=0, group=self.group)
+        if dev.type == "cuda":
+            from ..runtime import IpcEndpoint
+            ep = IpcEndpoint(N, me, cap)
+            hs = [None] * N
+            dist.all_gather_object(hs, ep.handles(), group=self.group)
+            dist.barrier(group=self.group)
+            ep.connect(hs)
+        else:
+            ep = ShmMailboxTransport(N, me, cap, box[0])
+            dist.barrier(group=self.group)
+            ep.connect()
+        dist.barrier(group=self.group)
+        self.ep = ep
+        self.caps = [self.cap] * N
+
+    def close(self) -> None:
+        if self.ep is not None:
+            self.ep.close()
+            self.ep = None
+
+    def _call_ipc(self, h, topk_w, topk_ids, lp) -> torch.Tensor:
+        T, D = h.shape
+        dev = h.device
+        N, me, pt = self.world, self.rank, self.per_token
+        C = T * pt                                   # my rows for one destination, at most
+        send_base = [p * C for p in range(N)]
+        key = (C, str(dev))
+        base = self._bases.get(key)
+        if base is None:
+            base = torch.tensor(send_base, dtype=torch.int32, device=dev)
+            self._bases[key] = base
+        if self.static:          # a captured graph: regions sized for any decode batch
+            rcap = [self.graph_tokens * pt] * N
+        else:
+            rcap = [t * pt for t in self.peer_tokens]
+        recv_base = [0] * N
+        for q in range(1, N):
+            recv_base[q] = recv_base[q - 1] + rcap[q - 1]
+        R = sum(rcap)
+        send_x, send_e, pos, cnt = ops.ep_pack(h, topk_ids, self.e_per, base, N * C,
+                                               counts=True)
+        if send_x.shape[0] == 0:                     # an idle rank still joins
+            send_x = h.new_zeros(1, D)
+            send_e = torch.full((1,), -1, dtype=torch.int32, device=dev)
+        recv_x = h.new_empty(max(R, 1), D)
+        recv_e = torch.empty(max(R, 1), dtype=torch.int32, device=dev)
+        recv_cnt = torch.zeros(N, dtype=torch.int32, device=dev)
+        st = torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else 0
+        self.ep.ep(st, False, self.row_bytes, send_x, send_e, send_base, cnt, recv_x, recv_e,
+                   recv_base, rcap, recv_cnt, self.caps, self.caps)
+        if R > 0:
+            y = ops.moe_mlp(recv_x[:R], lp["w_gu"], lp["w_down"],
+                            torch.ones(R, 1, dtype=torch.float32, device=dev),
+                            recv_e[:R].view(R, 1), self.e0)
+        else:
+            y = recv_x
+        self.ep.ep(st, True, self.row_bytes, send_x, send_e, send_base, cnt, y, None,
+                   recv_base, rcap, recv_cnt, self.caps, self.caps)
+        self.exchanges += 1
+        self.rows_routed += T * self.k
+        if dev.type != "cuda":           # host model: counts are readable for the tests
+            self.rows_sent += int(cnt.sum()) - int(cnt[me])
+        if T == 0:
+            return h.new_zeros(0, D)
+        return ops.moe_combine(send_x, topk_w, pos)
 
     def begin_step(self, peer_tokens: List[int]) -> None:
         """Every rank's token count for the forward about to run (same list everywhere)."""
@@ -90,6 +189,8 @@ class ExpertParallelMoE:
         else:
             topk_w = torch.zeros(0, k, dtype=torch.float32, device=dev)
             topk_ids = torch.zeros(0, k, dtype=torch.int32, device=dev)
+        if self.ep is not None:
+            return self._call_ipc(h, topk_w, topk_ids, lp)
         bound = max(self.peer_tokens) <= EP_BOUND_MAX_TOKENS
         if bound:
             # fixed-capacity buckets: C_p = T_p * min(k, E/N) rows from rank p to each rank
@@ -149,33 +250,61 @@ class ExpertParallelEngine:
 
     def __init__(self, model: str, device, max_batch: int = 256, max_model_len: int = 2048,
                  seed: int = 0, num_blocks: Optional[int] = None, dtype=torch.bfloat16,
-                 max_prefill_tokens: int = 16384, lookahead: Optional[bool] = None):
+                 max_prefill_tokens: int = 16384, lookahead: Optional[bool] = None,
+                 comm: Optional[str] = None, model_dir: Optional[str] = None):
         from .transport import init_distributed
         dev = torch.device(device)
         self.rank, self.world = init_distributed(device=dev if dev.type == "cuda" else None)
-        cfg = get_config(model)
+        cfg = get_config(model) if model_dir is None else _dir_config(model_dir, model)
         if not cfg.is_moe:
             raise ValueError(f"{model} has no experts")
         self.cfg = cfg
+        self.comm = comm or os.environ.get("DLI_EP_COMM", "torch")
         self.moe = ExpertParallelMoE(cfg.num_experts, cfg.top_k_experts)
         er = self.moe.expert_range()
-        shapes = W.stage_param_shapes(cfg, 0, cfg.num_layers, True, True)
-        params = {}
-        # generate full tensors per name (deterministic) and keep only the local experts
-        for name, shape in shapes.items():
-            t = W.random_init({name: shape}, dev, dtype, seed)[name]
-            params[name] = W.slice_experts(name, t, er)
-            del t
+        if model_dir is not None:
+            params = load_ep_params(model_dir, cfg, er, dev, dtype)
+        else:
+            shapes = W.stage_param_shapes(cfg, 0, cfg.num_layers, True, True)
+            params = {}
+            # generate full tensors per name (deterministic) and keep only the local experts
+            for name, shape in shapes.items():
+                t = W.random_init({name: shape}, dev, dtype, seed)[name]
+                params[name] = W.slice_experts(name, t, er)
+                del t
         lm = TransformerLM(cfg, params, device=dev, expert_range=er)
         lm.moe_fn = self.moe
+        ipc = self.comm == "ipc"
+        if ipc:
+            self.moe.setup_ipc(dev, cfg.hidden_size, dtype,
+                               max(max_prefill_tokens, max_batch), max_batch)
+        # with the mailbox data plane the decode forward is captured (graphs); the torch
+        # data plane needs host-side split sizes per layer and runs eagerly
+        graphs = ipc and dev.type == "cuda" and os.environ.get("DLI_NO_GRAPHS", "0") != "1"
         self.engine = LLMEngine(cfg, device=str(dev), dtype=dtype, max_batch=max_batch,
                                 max_model_len=max_model_len, num_blocks=num_blocks,
-                                use_graphs=False, lm=lm,
+                                use_graphs=graphs, lm=lm,
                                 max_prefill_tokens=max_prefill_tokens, lookahead=lookahead,
                                 mixed_steps=False)
+        self.max_batch = max_batch
         self.device = dev
         self.steps = 0
+        self.graph_steps = 0
         self.lockstep_syncs = 0
+
+    def warmup(self):
+        """Capture the decode graphs (every rank, same bucket order: the warm-up forwards
+        inside each capture exchange with the peers)."""
+        run = self.engine.runner
+        if not run.use_graphs:
+            return
+        self.moe.static = True
+        try:
+            for b in run.buckets:
+                self.moe.begin_step([b] * self.world)
+                run.capture([b])
+        finally:
+            self.moe.static = False
 
     def _exchange(self, work: bool, tokens: int) -> List[List[int]]:
         """The per-step lockstep exchange: (has work, tokens of the next forward) of every
@@ -204,11 +333,19 @@ class ExpertParallelEngine:
         info = self._exchange(work, 0 if meta is None else meta.num_tokens)
         if not any(w for w, _ in info):
             return eng.finish_step(None), False
-        self.moe.begin_step([t for _, t in info])
+        toks = [t for _, t in info]
+        self.moe.begin_step(toks)
+        # a captured decode graph sizes its receive regions for decode batches: when any
+        # rank's step is larger (a prefill), every rank runs this step eagerly
+        run = eng.runner
+        run.force_eager = max(toks) > self.max_batch
+        replayed = run.replays
         if meta is None:
             self._idle_forward()
         self.steps += 1
-        return eng.finish_step(meta), True
+        out = eng.finish_step(meta)
+        self.graph_steps += run.replays - replayed
+        return out, True
 
     def run_until_idle(self):
         outs = []
@@ -225,6 +362,53 @@ class ExpertParallelEngine:
         return [done[r] for r in rids]
 
 
+def _dir_config(model_dir: str, name: str):
+    """Config of an exported model directory (ours or a HF checkpoint)."""
+    import json
+    from pathlib import Path
+    from ..models.configs import ModelConfig
+    from ..models.hf import config_from_hf, is_hf_dir
+    d = Path(model_dir)
+    if is_hf_dir(d):
+        return config_from_hf(json.loads((d / "config.json").read_text()), name)
+    for c in [d / "config.json"] + sorted(d.glob("shard_*/config.json")):
+        if c.exists():
+            return ModelConfig.from_dict(json.loads(c.read_text()))
+    raise FileNotFoundError(f"{model_dir}: no config.json")
+
+
+def load_ep_params(model_dir: str, cfg, expert_range, device, dtype):
+    """This rank's tensors from an exported model (``shard-model`` output: every
+    ``shard_<i>/model.safetensors``, or one ``model.safetensors``; or a HF checkpoint): all
+    attention / norm / embedding / head tensors, and of every expert tensor only the rows of
+    experts [e0, e1) — a contiguous byte range of the file (``SafetensorsFile.load_rows``), so
+    a rank never reads the other ranks' experts."""
+    from pathlib import Path
+    from ..models.hf import is_hf_dir, load_hf_dir
+    from ..runtime import SafetensorsFile
+    d = Path(model_dir)
+    e0, e1 = expert_range
+    if is_hf_dir(d):
+        _, full = load_hf_dir(d, "cpu", dtype)
+        return {k: W.slice_experts(k, v, expert_range).to(device) for k, v in full.items()}
+    files = sorted(d.glob("shard_*/model.safetensors")) or [d / "model.safetensors"]
+    out = {}
+    for f in files:
+        st = SafetensorsFile(str(f))
+        try:
+            names = st.keys()
+            experts = [n for n in names if n.endswith(".w_gu") or n.endswith(".w_down")]
+            rest = [n for n in names if n not in experts]
+            out.update(st.load(rest, device=device))
+            for n in experts:
+                out[n] = st.load_rows(n, e0, e1, device=device)
+        finally:
+            st.close()
+    if torch.device(device).type == "cuda":
+        torch.cuda.synchronize(device)
+    return {k: (v if v.dtype == dtype else v.to(dtype)) for k, v in out.items()}
+
+
 def bench_expert_parallel(args, world, rank, make_prompts):
     local = int(os.environ.get("LOCAL_RANK", rank))
     if os.environ.get("DLI_SAME_DEVICE", "0") == "1":
@@ -236,7 +420,9 @@ def bench_expert_parallel(args, world, rank, make_prompts):
         dev = torch.device("cpu")
     eng = ExpertParallelEngine(args.model, dev, max_batch=args.batch,
                                max_model_len=args.max_model_len,
-                               max_prefill_tokens=max(args.batch * args.prompt_len, 8192))
+                               max_prefill_tokens=max(args.batch * args.prompt_len, 8192),
+                               model_dir=getattr(args, "shard_dir", None))
+    eng.warmup()
     from ..engine.sequence import SamplingParams
     sp = SamplingParams(max_length=args.max_length, temperature=0.8, top_k=50, top_p=0.95,
                         ignore_eos=True)
@@ -269,9 +455,10 @@ def bench_expert_parallel(args, world, rank, make_prompts):
     gathered = [torch.zeros_like(lat_t) for _ in range(world)]
     dist.all_gather(gathered, lat_t)
     dist.barrier()
+    eng.moe.close()
     dist.destroy_process_group()
     if rank != 0:
         return None
     return {"tokens": int(tt.item()), "seconds": float(dt.item()),
             "latencies": torch.cat(gathered).tolist(), "global_batch": args.batch * world,
-            "parallelism": f"dp{world}-ep{world}"}
+            "parallelism": f"dp{world}-ep{world}" + ("-ipc" if eng.comm == "ipc" else "")}

@@ -151,6 +151,88 @@ class ShmMailboxTransport:
         self._flags(self.peers[peer])[(self.world + self.rank) * _LINE] = 1   # FREE
         self.recvs += 1
 
+    # ---- variable-length messages (expert-parallel rows: the count travels with them) ---
+    def send_raw(self, b: np.ndarray, peer: int) -> None:
+        b = np.ascontiguousarray(b).reshape(-1).view(np.uint8)
+        self.send(torch.from_numpy(b) if b.nbytes else torch.zeros(0, dtype=torch.uint8), peer)
+
+    def recv_raw(self, peer: int) -> np.ndarray:
+        """The message at the head of edge peer -> me, whatever its size."""
+        mine = self._flags(self.shm)
+        self._wait(mine, peer * _LINE, f"READY[{peer}->{self.rank}]")
+        off = self._off[peer]
+        n = int(np.ndarray((1,), np.int64, buffer=self.shm.buf, offset=off)[0])
+        out = np.ndarray((n,), np.uint8, buffer=self.shm.buf, offset=off + 8).copy()
+        self._flags(self.peers[peer])[(self.world + self.rank) * _LINE] = 1   # FREE
+        self.recvs += 1
+        return out
+
+    def ep(self, stream, ret: bool, row_bytes: int, send_x, send_e, send_base, send_cnt,
+           recv_x, recv_e, recv_base, recv_cap, recv_cnt, cap_rows, in_cap_rows) -> None:
+        """Host model of ``IpcEndpoint.ep`` (csrc/runtime/ipc.cpp ``dli_ipc_ep``): the same
+        message order and per-edge FIFO, counts read from the tensors."""
+        W, me = self.world, self.rank
+        sx = send_x.view(torch.uint8).view(-1, row_bytes)
+        rx = recv_x.view(torch.uint8).view(-1, row_bytes)
+
+        def msg(rows: torch.Tensor, ids: Optional[torch.Tensor]) -> np.ndarray:
+            n = np.array([rows.shape[0]], np.int64).view(np.uint8)
+            parts = [n]
+            if ids is not None:
+                parts.append(ids.contiguous().numpy().view(np.uint8))
+            parts.append(rows.contiguous().numpy().reshape(-1))
+            return np.concatenate(parts)
+
+        def unpack(b: np.ndarray, with_ids: bool):
+            n = int(b[:8].view(np.int64)[0])
+            o = 8
+            ids = None
+            if with_ids:
+                ids = torch.from_numpy(b[o:o + 4 * n].view(np.int32).copy())
+                o += 4 * n
+            rows = torch.from_numpy(b[o:o + n * row_bytes].copy()).view(n, row_bytes)
+            return n, ids, rows
+        if not ret:
+            for p in range(W):
+                if p == me:
+                    continue
+                c = int(send_cnt[p])
+                if c > cap_rows[p]:
+                    raise ValueError(f"expert bucket {me}->{p}: {c} rows > capacity {cap_rows[p]}")
+                b0 = int(send_base[p])
+                self.send_raw(msg(sx[b0:b0 + c], send_e[b0:b0 + c]), p)
+            c = int(send_cnt[me])
+            rb, sb = int(recv_base[me]), int(send_base[me])
+            rx[rb:rb + c] = sx[sb:sb + c]
+            recv_e[rb:rb + int(recv_cap[me])] = -1
+            recv_e[rb:rb + c] = send_e[sb:sb + c]
+            recv_cnt[me] = c
+            for q in range(W):
+                if q == me:
+                    continue
+                n, ids, rows = unpack(self.recv_raw(q), True)
+                rb = int(recv_base[q])
+                if n > int(recv_cap[q]):
+                    raise ValueError(f"expert rows {q}->{me}: {n} > region {recv_cap[q]}")
+                rx[rb:rb + n] = rows
+                recv_e[rb:rb + int(recv_cap[q])] = -1
+                recv_e[rb:rb + n] = ids
+                recv_cnt[q] = n
+            return
+        for q in range(W):
+            if q == me:
+                continue
+            c, rb = int(recv_cnt[q]), int(recv_base[q])
+            self.send_raw(msg(rx[rb:rb + c], None), q)
+        c, rb, sb = int(recv_cnt[me]), int(recv_base[me]), int(send_base[me])
+        sx[sb:sb + c] = rx[rb:rb + c]
+        for p in range(W):
+            if p == me:
+                continue
+            n, _, rows = unpack(self.recv_raw(p), False)
+            sb = int(send_base[p])
+            sx[sb:sb + n] = rows
+
     def exchange(self, sends: Sequence[Tuple[torch.Tensor, int]],
                  recvs: Sequence[Tuple[torch.Tensor, int]], stream=None) -> None:
         """Every send, then every receive, in issue order (the device queue's order)."""

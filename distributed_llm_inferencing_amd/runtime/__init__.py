@@ -87,6 +87,8 @@ _SIGS = {
     "dli_ipc_abort": ([_P, ctypes.c_double], _I),
     "dli_ipc_stats": ([_P, _P], None),
     "dli_ipc_error": ([_P], _I),
+    "dli_ipc_ep": ([_P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P], _I),
+    "dli_ipc_ep_bytes": ([_I, _I], _LL),
     "dli_ipc_host_flags": ([_P], _I),
     "dli_ipc_destroy": ([_P], None),
 }
@@ -580,6 +582,25 @@ class IpcEndpoint:
         r = lib().dli_ipc_abort(self._h, float(timeout_s))
         if r != 0:
             raise RuntimeError(f"IPC abort failed ({r})")
+
+    @staticmethod
+    def ep_bytes(cap_rows: int, row_bytes: int) -> int:
+        return int(lib().dli_ipc_ep_bytes(int(cap_rows), int(row_bytes)))
+
+    def ep(self, stream: int, ret: bool, row_bytes: int, send_x, send_e, send_base, send_cnt,
+           recv_x, recv_e, recv_base, recv_cap, recv_cnt, cap_rows, in_cap_rows) -> None:
+        """Expert-parallel dispatch (``ret`` False) or return over the mailboxes (see
+        ``dli_ipc_ep``): row counts stay on the device (``send_cnt`` / ``recv_cnt`` int32
+        tensors), only the routed rows move."""
+        W = self.world
+        ia = lambda v: (ctypes.c_int * W)(*[int(x) for x in v])  # noqa: E731
+        r = lib().dli_ipc_ep(self._h, ctypes.c_void_p(stream), int(bool(ret)), int(row_bytes),
+                             send_x.data_ptr(), send_e.data_ptr() if send_e is not None else None,
+                             ia(send_base), send_cnt.data_ptr(), recv_x.data_ptr(),
+                             recv_e.data_ptr() if recv_e is not None else None, ia(recv_base),
+                             ia(recv_cap), recv_cnt.data_ptr(), ia(cap_rows), ia(in_cap_rows))
+        if r != 0:
+            raise RuntimeError(f"IPC expert exchange failed ({r})")
 
     def error(self) -> bool:
         """A captured wait ran out of its budget (DLI_IPC_WAIT_S): a peer stopped."""

@@ -15,15 +15,19 @@ ap = argparse.ArgumentParser()
 ap.add_argument("dir")
 ap.add_argument("top", nargs="?", type=int, default=25)
 ap.add_argument("--tail-ms", type=float, default=None)
+ap.add_argument("--merge", action="store_true",
+                help="merge every kernel_trace.csv under the directory (all ranks' processes)")
 ap.add_argument("--gaps", type=int, default=0,
                 help="also list the N longest GPU-idle gaps (kernel before -> kernel after)")
 a = ap.parse_args()
 d = Path(a.dir)
-tr = list(d.glob("*kernel_trace.csv"))
+tr = sorted(d.rglob("*kernel_trace.csv"))
 ev = []
 if tr:
+    # every process's trace (a same-GPU multi-rank rehearsal writes one per rank): the
+    # union is what the one GPU did
     ev = sorted((int(x["Start_Timestamp"]), int(x["End_Timestamp"]), x["Kernel_Name"])
-                for x in csv.DictReader(open(tr[0])))
+                for f in (tr if a.merge else tr[:1]) for x in csv.DictReader(open(f)))
 if a.tail_ms is not None and ev:
     t_end = ev[-1][1]
     ev = [e for e in ev if e[0] >= t_end - a.tail_ms * 1e6]
@@ -34,7 +38,7 @@ if a.tail_ms is not None and ev:
     rows = [{"Name": n, "TotalDurationNs": v[0], "Calls": v[1], "AverageNs": v[0] / v[1]}
             for n, v in agg.items()]
 else:
-    stats = next(d.glob("*kernel_stats.csv"))
+    stats = next(d.rglob("*kernel_stats.csv"))
     rows = list(csv.DictReader(open(stats)))
 tot = sum(float(r["TotalDurationNs"]) for r in rows)
 print(f"{'ms':>9} {'%':>5} {'calls':>7} {'avg_us':>8}  kernel")

@@ -166,3 +166,49 @@ def test_pipeline_over_fifo_mailboxes_matches_single_stage(world, vp, mixed, chu
     if mixed == "1":
         assert res[4] > 0                     # mixed steps crossed the ring
     assert res[5]["sends"] > 0 and res[5]["recvs"] > 0
+
+
+# ------------------------------------------------------------------------------ experts
+def _ep_worker(rank, world, port, q, model, shard_dir):
+    _env(rank, world, port, DLI_EP_COMM="ipc")
+    import torch.distributed as dist
+    from distributed_llm_inferencing_amd.parallel.expert import ExpertParallelEngine
+    eng = ExpertParallelEngine(model, "cpu", max_batch=8, max_model_len=64, num_blocks=64,
+                               dtype=torch.float32, model_dir=shard_dir)
+    assert eng.moe.ep is not None
+    mine = PROMPTS[rank::world] if rank == 0 else PROMPTS[rank::world][:1]
+    sp = SamplingParams(max_length=18, do_sample=False, ignore_eos=True)
+    out = [o.all_ids for o in eng.generate(mine, sp)]
+    q.put((rank, mine, out, eng.moe.rows_sent, eng.moe.rows_routed, eng.moe.exchanges,
+           eng.lockstep_syncs, eng.steps, eng.engine.lookahead))
+    dist.barrier()
+    eng.moe.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("model,world,from_shards", [("mixtral-tiny", 2, False),
+                                                     ("mixtral-tiny", 4, True),
+                                                     ("mixtral-tiny8e", 8, False)])
+def test_expert_parallel_over_fifo_mailboxes_matches_dense(tmp_path, model, world, from_shards):
+    """DP attention + EP experts with the mailbox all-to-all (counts on the device, only
+    routed rows on the wire) == one process with all experts, token for token; ranks serve
+    different, unequal request sets (idle forwards join every exchange); one lockstep sync
+    per step; with ``from_shards`` every rank reads only its experts' rows of the exported
+    files."""
+    from distributed_llm_inferencing_amd.models import get_config
+    shard_dir = None
+    if from_shards:
+        from distributed_llm_inferencing_amd.shard.writer import export_shards
+        paths = export_shards(model, 2, str(tmp_path / "sh"), dtype=torch.float32,
+                              log=lambda *a: None)
+        shard_dir = str(paths[0].parent)
+    res = _spawn(_ep_worker, world, model, shard_dir, n_results=world)
+    eng = LLMEngine(model, device="cpu", dtype=torch.float32, max_batch=8, max_model_len=64,
+                    num_blocks=64)
+    sp = SamplingParams(max_length=18, do_sample=False, ignore_eos=True)
+    L = get_config(model).num_layers
+    for rank, mine, out, sent, routed, exch, syncs, steps, la in res:
+        assert out == [o.all_ids for o in eng.generate(mine, sp)], rank
+        assert exch == steps * L and la
+        assert syncs == steps + 1                    # the one lockstep exchange per step
+        assert sent <= routed                        # no padding rows cross ranks

@@ -67,7 +67,7 @@ def _run(target, world, *args):
     for p in procs:
         p.start()
     try:
-        n = world if (target is _ep_worker or "ipc" in args) else 1
+        n = world if (target in (_ep_worker, _ep_ipc_worker) or "ipc" in args) else 1
         res = [q.get(timeout=240) for _ in range(n)]
     finally:
         for p in procs:
@@ -153,5 +153,40 @@ def test_expert_parallel_two_ranks_on_gpu_match_dense(gpu):
         for rank, mine, out, reads, syncs, steps, la in res:
             assert out == [o.all_ids for o in eng.generate(mine, GREEDY)], rank
             assert reads == 0 and syncs == steps + 1 and la
+    finally:
+        del os.environ["DLI_GEMM_AUTOTUNE"]
+
+
+def _ep_ipc_worker(rank, world, port, q):
+    _env(rank, world, port, DLI_EP_COMM="ipc")
+    import torch.distributed as dist
+    from distributed_llm_inferencing_amd.parallel.expert import ExpertParallelEngine
+    eng = ExpertParallelEngine("mixtral-tiny", "cuda", max_batch=8, max_model_len=64,
+                               num_blocks=64)
+    eng.warmup()                      # every decode bucket captured, exchanges included
+    mine = PROMPTS[rank::world]
+    out = [o.all_ids for o in eng.generate(mine, GREEDY)]
+    q.put((rank, mine, out, eng.graph_steps, eng.lockstep_syncs, eng.steps,
+           eng.engine.runner.uploads, eng.engine.lookahead))
+    dist.barrier()
+    eng.moe.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 4])
+def test_expert_parallel_over_ipc_graphs_on_gpu(gpu, world):
+    """Experts over N ranks on one GPU through the IPC mailboxes: counts stay on the device,
+    the decode forward (attention + every MoE dispatch / return) is one graph replay, one
+    lockstep sync per step; tokens identical to one process holding every expert."""
+    res = _run(_ep_ipc_worker, world)
+    os.environ["DLI_GEMM_AUTOTUNE"] = "0"
+    try:
+        eng = LLMEngine("mixtral-tiny", device="cuda", max_batch=8, max_model_len=64,
+                        num_blocks=64)
+        for rank, mine, out, graph_steps, syncs, steps, uploads, la in res:
+            assert out == [o.all_ids for o in eng.generate(mine, GREEDY)], rank
+            assert syncs == steps + 1 and la
+            assert graph_steps > 0 and uploads == graph_steps   # one H2D + one replay
     finally:
         del os.environ["DLI_GEMM_AUTOTUNE"]
