@@ -991,6 +991,162 @@ static int launch_8p224(const void* A, int lda, const void* W, int ldw, void* C,
   DLI_RETURN_LAUNCH();
 }
 
+// ---------------------------------------------------------------------------------------
+// Skinny GEMM for M <= 4 rows (batch-1 / tiny-batch decode: SURVEY.md §7.4 "the decode
+// skinny GEMM must approach the HBM roofline"): every weight byte is used M times, so the
+// kernel is a weight stream, not an MFMA tile. A workgroup (4 waves) owns R = 4 * RW output
+// rows of W over one K slice; in a wave, lane l covers the 8 K-elements [8 (l + 64 s),
+// +8) of step s for its RW rows: RW 16-B nontemporal weight loads per step (the weights are
+// read exactly once, MI355X_MICROARCH.md 'nt-weights'), two steps in flight, bf16 pairs
+// accumulated by v_dot2c_f32_bf16 against x (M rows, L1/L2-resident). Lane partial sums
+// are reduced across the wave with shuffles and staged in LDS; the epilogue then writes
+// bf16 / fp32 / SiLU(gate)*up (the 16-row interleaved gate/up weight: a workgroup's 32 rows
+// are 16 gate + 16 up features) or fp32 split-K slabs for the fused reduces. No MFMA, no
+// LDS tiles, no padding rows: bytes moved = weights + M * K * 2 + outputs.
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
+
+// bf16 pairs by __builtin_shufflevector: a __builtin_bit_cast of one element of a uint
+// ext-vector was compiled (ROCm 7.2 clang) into the FIRST element for every lane pair
+__device__ __forceinline__ float dot8_acc(const bf16x8v w, const bf16x8v x, float acc) {
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(w, w, 0, 1),
+                                        __builtin_shufflevector(x, x, 0, 1), acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(w, w, 2, 3),
+                                        __builtin_shufflevector(x, x, 2, 3), acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(w, w, 4, 5),
+                                        __builtin_shufflevector(x, x, 4, 5), acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(w, w, 6, 7),
+                                        __builtin_shufflevector(x, x, 6, 7), acc, false);
+  return acc;
+}
+
+template <int MB, int RW, int EPI>
+__global__ void __launch_bounds__(256) gemv_kernel(
+    const u16* __restrict__ A, int lda, const u16* __restrict__ W, int ldw,
+    void* __restrict__ C, int ldc, int M, int N, int K, int k_split_len,
+    const u16* __restrict__ bias, float* __restrict__ ws) {
+  constexpr int R = 4 * RW;
+  __shared__ float res[MB][R];
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int n_base = blockIdx.x * R;
+  const int ks = blockIdx.y;
+  const int kb = ks * k_split_len;
+  const int klen = min(k_split_len, K - kb);
+  const int nchunk = klen >> 3;                     // 8-element chunks of the K slice
+  const int r0 = n_base + wid * RW;                 // this wave's first row
+  const bf16x8v* wrow[RW];
+#pragma unroll
+  for (int r = 0; r < RW; ++r) {
+    const int n = min(r0 + r, N - 1);
+    wrow[r] = reinterpret_cast<const bf16x8v*>(W + (long)n * ldw + kb);
+  }
+  const bf16x8v* xrow[MB];
+#pragma unroll
+  for (int m = 0; m < MB; ++m)
+    xrow[m] = reinterpret_cast<const bf16x8v*>(A + (long)min(m, M - 1) * lda + kb);
+  float acc[MB][RW];
+#pragma unroll
+  for (int m = 0; m < MB; ++m)
+#pragma unroll
+    for (int r = 0; r < RW; ++r) acc[m][r] = 0.f;
+  int c = lane;
+  // two 64-chunk steps per iteration: 2 * RW weight loads in flight per lane
+  for (; c + 64 < nchunk; c += 128) {
+    bf16x8v w0[RW], w1[RW];
+#pragma unroll
+    for (int r = 0; r < RW; ++r) {
+      w0[r] = __builtin_nontemporal_load(wrow[r] + c);
+      w1[r] = __builtin_nontemporal_load(wrow[r] + c + 64);
+    }
+#pragma unroll
+    for (int m = 0; m < MB; ++m) {
+      const bf16x8v x0 = xrow[m][c], x1 = xrow[m][c + 64];
+#pragma unroll
+      for (int r = 0; r < RW; ++r) acc[m][r] = dot8_acc(w1[r], x1, dot8_acc(w0[r], x0, acc[m][r]));
+    }
+  }
+  for (; c < nchunk; c += 64) {
+    bf16x8v w0[RW];
+#pragma unroll
+    for (int r = 0; r < RW; ++r) w0[r] = __builtin_nontemporal_load(wrow[r] + c);
+#pragma unroll
+    for (int m = 0; m < MB; ++m) {
+      const bf16x8v x0 = xrow[m][c];
+#pragma unroll
+      for (int r = 0; r < RW; ++r) acc[m][r] = dot8_acc(w0[r], x0, acc[m][r]);
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < MB; ++m)
+#pragma unroll
+    for (int r = 0; r < RW; ++r) {
+      const float v = wave_sum(acc[m][r]);
+      if (lane == 0) res[m][wid * RW + r] = v;
+    }
+  __syncthreads();
+  // epilogue: one thread per (row m, output column)
+  if (ws != nullptr && gridDim.y > 1) {             // fp32 partial slab of this K slice
+    for (int t = threadIdx.x; t < MB * R; t += 256) {
+      const int m = t / R, j = t % R, n = n_base + j;
+      if (m < M && n < N) ws[((long)ks * M + m) * N + n] = res[m][j];
+    }
+    return;
+  }
+  if (EPI == EPI_SILU) {                            // R = 32: rows 0-15 gate, 16-31 up
+    for (int t = threadIdx.x; t < MB * 16; t += 256) {
+      const int m = t / 16, j = t % 16;
+      const int f = (n_base >> 5) * 16 + j;
+      if (m < M && n_base + j < N)
+        ((u16*)C)[(long)m * ldc + f] = f2bf(silu_f(res[m][j]) * res[m][j + 16]);
+    }
+    return;
+  }
+  for (int t = threadIdx.x; t < MB * R; t += 256) {
+    const int m = t / R, j = t % R, n = n_base + j;
+    if (m < M && n < N) store_pair_or_one<EPI>(C, ldc, m, n, res[m][j], bias);
+  }
+}
+
+template <int MB, int RW, int EPI>
+static int launch_gemv(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M,
+                       int N, int K, int splits, const void* bias, void* ws, hipStream_t st) {
+  constexpr int R = 4 * RW;
+  if (M > MB || (EPI == EPI_SILU && (R != 32 || N % 32)) || K % 8 || lda % 8 || ldw % 8)
+    return (int)hipErrorInvalidValue;
+  int ksl = K / splits;
+  ksl = (ksl / 8) * 8;
+  if (ksl * splits != K) return (int)hipErrorInvalidValue;
+  dim3 grid((N + R - 1) / R, splits);
+  gemv_kernel<MB, RW, EPI><<<grid, 256, 0, st>>>((const u16*)A, lda, (const u16*)W, ldw, C, ldc,
+                                                 M, N, K, ksl, (const u16*)bias,
+                                                 splits > 1 ? (float*)ws : nullptr);
+  if (splits > 1 && C != nullptr) {
+    const int outN = (EPI == EPI_SILU) ? N / 2 : N;
+    const long total = (long)M * outN;
+    splitk_reduce_kernel<EPI><<<(int)((total + 255) / 256), 256, 0, st>>>(
+        C, ldc, (const float*)ws, M, N, splits, (const u16*)bias);
+  }
+  DLI_RETURN_LAUNCH();
+}
+
+template <int EPI>
+static int dispatch_gemv(int tile_cfg, const void* A, int lda, const void* W, int ldw, void* C,
+                         int ldc, int M, int N, int K, int splits, const void* bias, void* ws,
+                         hipStream_t st) {
+  // 30: 16 rows per workgroup, 31: 32 rows (the SiLU gate/up pairing needs 32)
+  const bool r32 = tile_cfg == 31;
+  if (M <= 1)
+    return r32 ? launch_gemv<1, 8, EPI>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st)
+               : launch_gemv<1, 4, EPI>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st);
+  if (M <= 2)
+    return r32 ? launch_gemv<2, 8, EPI>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st)
+               : launch_gemv<2, 4, EPI>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st);
+  if (M <= 4)
+    return r32 ? launch_gemv<4, 8, EPI>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st)
+               : launch_gemv<4, 4, EPI>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st);
+  return (int)hipErrorInvalidValue;
+}
+
 template <int EPI>
 static int dispatch_tile(int tile_cfg, const void* A, int lda, const void* W, int ldw, void* C,
                          int ldc, int M, int N, int K, int splits, const void* bias, void* ws,
@@ -1019,6 +1175,10 @@ static int dispatch_tile(int tile_cfg, const void* A, int lda, const void* W, in
     DLI_CFG8(23, 128, 192, 3, 2, 4) DLI_CFG8(24, 128, 192, 2, 2, 4) DLI_CFG8(25, 256, 192, 2, 4, 2)
     // 256x224 ping-pong (gemm8p224_kernel): N = 28672 gate/up at M = 512 is 256 tiles
     case 26: return launch_8p224<EPI>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
+    // skinny weight-streaming GEMM for M <= 4 (no grouped mode)
+    case 30: case 31:
+      if (go != nullptr) return (int)hipErrorInvalidValue;
+      return dispatch_gemv<EPI>(tile_cfg, A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st);
 #undef DLI_CFG8
 #undef DLI_CFG
     default: return (int)hipErrorInvalidValue;
@@ -1030,14 +1190,15 @@ static int dispatch_tile(int tile_cfg, const void* A, int lda, const void* W, in
 // stages, 12 = 160x128 (MoE experts of ~130-190 rows in one pass); 13-17 = 8-wave tiles
 // 256x256, 256x128, 128x256 (2 stages) and 256x128, 128x256 (3 stages); 18/19 = 128x96 and
 // 20/21 = 128x64 with 2/3 stages; 22 = 256x256 8-phase ping-pong; 23/24 = 128x192 (3/2
-// stages), 25 = 256x192, 8 waves; 26 = 256x224 ping-pong. ws: fp32 [splits, M, N] when
-// splits>1.
+// stages), 25 = 256x192, 8 waves; 26 = 256x224 ping-pong; 30 / 31 = the M <= 4 weight
+// stream (16 / 32 rows per workgroup). ws: fp32 [splits, M, N] when splits>1.
 // group_off (nullable): int[groups+1] row offsets; M is then the max rows of any group.
 extern "C" int dli_gemm(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M,
                         int N, int K, int epi, int tile_cfg, int splits, const void* bias,
                         void* ws, const int* group_off, int groups, hipStream_t st) {
   if (M <= 0 || N <= 0) return 0;
-  if (K % BK || lda % 8 || ldw % 8 || splits < 1) return (int)hipErrorInvalidValue;
+  if ((tile_cfg < 30 && K % BK) || lda % 8 || ldw % 8 || splits < 1)
+    return (int)hipErrorInvalidValue;
   if (epi == EPI_SILU && N % 32) return (int)hipErrorInvalidValue;
   if (splits > 1 && ws == nullptr) return (int)hipErrorInvalidValue;
   if (groups < 1) groups = 1;

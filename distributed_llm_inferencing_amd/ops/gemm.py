@@ -41,6 +41,10 @@ TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256), 4: (256, 128),
          26: (256, 224),
          # 22 with the round-1 schedule (a vmcnt wait every phase), for A/B runs only
          27: (256, 256)}
+# weight-streaming skinny GEMM (gemm.hip gemv_kernel) for M <= GEMV_MAX_M rows: 16 / 32 output
+# rows per workgroup (31 for the SiLU*up gate/up pairing); not an MFMA tile, so kept apart
+GEMV_TILES = {30: 16, 31: 32}
+GEMV_MAX_M = 4
 TILE_WAVES = {13: (2, 4), 14: (4, 2), 15: (2, 4), 16: (4, 2), 17: (2, 4),
               22: (2, 4), 23: (2, 4), 24: (2, 4), 25: (4, 2),
               26: (4, 2), 27: (2, 4)}
@@ -49,6 +53,8 @@ TILE_WAVES = {13: (2, 4), 14: (4, 2), 15: (2, 4), 16: (4, 2), 17: (2, 4),
 def tile_ok(tile: int, epi: str) -> bool:
     """The SiLU*up epilogue pairs 16-column gate/up blocks inside a wave's column range,
     which must therefore be a multiple of 32."""
+    if tile in GEMV_TILES:
+        return epi != "silu_mul" or tile == 31
     if epi != "silu_mul":
         return True
     if tile == 26:              # the straddling gate/up pair meets through LDS
@@ -110,6 +116,18 @@ def _heuristic(M: int, N: int, K: int, epi: str) -> GemmPlan:
                    and K // (splits * 2) >= 1024 and splits < 4):
                 splits *= 2
         return GemmPlan("dli", 22, splits)
+    if M <= GEMV_MAX_M:
+        # batch-1 / tiny batches: stream the weights (gemv_kernel) with enough workgroups
+        # (>= 512, two per CU) to keep ~64 KB of loads in flight per CU
+        tile = 31 if epi == "silu_mul" else 30
+        wgs = -(-N // GEMV_TILES[tile])
+        splits = 1
+        while (wgs * splits < 512 and K % (64 * splits * 2) == 0
+               and K // (splits * 2) >= 1024 and splits < 8):
+            splits *= 2
+        if epi == "splitk" and splits == 1 and K % 128 == 0:
+            splits = 2
+        return GemmPlan("dli", tile, splits)
     if M <= 128:
         tile = 0 if N <= 8192 else 1
     elif M <= 256:
@@ -314,6 +332,13 @@ def candidate_plans(M: int, N: int, K: int, epi: str):
             if splits > 1 and tiles * splits > 4 * NUM_CUS:
                 continue
             out.append(GemmPlan("dli", tile, splits))
+    if M <= GEMV_MAX_M:
+        for tile in GEMV_TILES:
+            if tile in excl or not tile_ok(tile, epi):
+                continue
+            for splits in (1, 2, 4, 8):
+                if K % (64 * splits) == 0 and K // splits >= 512:
+                    out.append(GemmPlan("dli", tile, splits))
     # hipBLASLt (+ our epilogue pass for silu_mul) competes for decode-sized GEMMs only when
     # DLI_GEMM_DECODE_BLAS=1: measured in-situ at M = 512 our kernels (8-wave 256x256 gate/up
     # with fused SiLU, 3-stage 128-row tiles) run the decode layer as fast as the library mix

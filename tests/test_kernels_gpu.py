@@ -95,6 +95,45 @@ def test_gemm_256x224_pingpong(gpu, M, N, K, epi):
         close(out, ref, rtol=2e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("M", [1, 2, 3, 4])
+@pytest.mark.parametrize("N,K,epi", [(6144, 4096, "none"), (4096, 14336, "none"),
+                                     (28672, 4096, "silu_mul"), (50257, 768, "f32"),
+                                     (2304, 768, "bias")])
+def test_gemv_skinny(gpu, M, N, K, epi):
+    """The M <= 4 weight-streaming GEMM (tiles 30 / 31) against the fp32 reference: every
+    epilogue, split-K 1/2/4 (reduce kernel), a K (768) that is not a multiple of the
+    512-element wave step, and a final partial row block (N = 50257)."""
+    torch.manual_seed(7)
+    x, w, b = rnd(M, K, dev=gpu), rnd(N, K, dev=gpu, scale=0.05), rnd(N, dev=gpu)
+    if epi == "silu_mul":
+        ref = R.silu_mul(R.linear(x, w).float().to(BF))
+    elif epi == "f32":
+        ref = R.linear(x, w, out_dtype=torch.float32)
+    elif epi == "bias":
+        ref = R.linear(x, w, b)
+    else:
+        ref = R.linear(x, w, out_dtype=torch.float32)
+    for tile in G.GEMV_TILES:
+        if not G.tile_ok(tile, epi):
+            continue
+        for splits in (1, 2, 4):
+            if K % (64 * splits):
+                continue
+            out = ops._gemm_native(x, w, epi, bias=b if epi == "bias" else None,
+                                   plan=G.GemmPlan("dli", tile, splits))
+            close(out, ref, rtol=2e-2, atol=2e-2)
+    if epi == "none" and K % 128 == 0:       # split-K slabs into the fused add + RMSNorm
+        r0, nw = rnd(M, N, dev=gpu), rnd(N, dev=gpu)
+        ref_out, ref_res = R.fused_add_rmsnorm(R.linear(x, w), r0, nw, 1e-5)
+        for splits in (2, 4):
+            G.set_plan(M, N, K, "splitk", G.GemmPlan("dli", 30, splits))
+            res = r0.clone()
+            out = ops.linear_add_rmsnorm(x, w, res, nw, 1e-5)
+            close(out, ref_out, rtol=2e-2, atol=3e-2)
+            close(res, ref_res, rtol=1e-2, atol=2e-2)
+        G.clear_plans()
+
+
 def test_gemm_asymmetric_identity(gpu):
     """A = I with asymmetric B catches a transposed C write (cdna_hip_programming.md §3)."""
     n = 128
