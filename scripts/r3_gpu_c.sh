@@ -5,7 +5,7 @@ mkdir -p gpurun_out/r3c
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 O=gpurun_out/r3c
 run() { local name=$1 t=$2; shift 2; echo "=== $name $(date +%T)"; timeout -k 10 $t "$@" > $O/$name.log 2>&1; local rc=$?; echo "rc[$name]=$rc"; tail -3 $O/$name.log; return $rc; }
-run gputests 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread &&
+run gputests 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread ; 
 run bench1 600 python bench.py --steps 3 --warmup 1 &&
 run bench_b1 600 python bench.py --steps 16 --warmup 2 --batch 1 &&
 DLI_DIST_BACKEND=gloo DLI_SAME_DEVICE=1 DLI_PP_COMM=ipc run pp2_ipc 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29633 bench.py --gpus 2 --steps 2 --warmup 1 --batch 512 &&

@@ -49,6 +49,7 @@ def _pp_worker(rank, world, port, q, vp, comm="torch"):
         q.put(res)
     else:
         eng.serve()
+    if rank != 0 and comm == "ipc":
         from distributed_llm_inferencing_amd.engine.batch import DECODE, PREFILL
         run = eng.stage.runner
         q.put(("stage", rank, run.piped is not None, run.replays, run.uploads,
