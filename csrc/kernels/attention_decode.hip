@@ -31,13 +31,14 @@ typedef short s16x8 __attribute__((ext_vector_type(8)));
 
 // The tile loop shared by the plain and the fused kernel: one wave = one (sequence, kv head,
 // split) item with its Q^T fragments already in registers.
+// The tile loop over tokens [s_begin, s_end): leaves the unnormalised O rows in o_acc, the
+// running max of head `col` in m_run and this lane's partial denominator in l_part.
 template <int HD>
-__device__ __forceinline__ void decode_attn_core(
-    const bf16x8 (&qf)[HD / 32], u16* vt, int lane, int b, int kvh, int split, int G, int ctx,
-    int s_begin, int s_end, u16* __restrict__ out, const u16* __restrict__ k_cache,
-    const u16* __restrict__ v_cache, const int* __restrict__ block_tables, int max_blocks,
-    int hq, int hkv, int block_size, float scale_log2, int num_splits,
-    float* __restrict__ ws_o, float* __restrict__ ws_ml) {
+__device__ __forceinline__ void decode_attn_loop(
+    const bf16x8 (&qf)[HD / 32], u16* vt, int lane, int b, int kvh, int s_begin, int s_end,
+    const u16* __restrict__ k_cache, const u16* __restrict__ v_cache,
+    const int* __restrict__ block_tables, int max_blocks, int hkv, int block_size,
+    float scale_log2, f32x4 (&o_acc)[HD / 16], float& m_run, float& l_part) {
   constexpr int DB = HD / 16;     // 16-wide output column blocks (= V pieces per lane)
   constexpr int KK = HD / 32;
   constexpr int VROW = HD + 16;   // padded LDS row of the V tile, in u16
@@ -50,9 +51,8 @@ __device__ __forceinline__ void decode_attn_core(
   int win = s_begin / block_size;
   int bt_lane = bt[min(win + lane, last_blk)];
   const long kv_head_stride = (long)block_size * HD;           // elements per (blk, head)
-  float m_run = -INFINITY;          // running max for head `col` (replicated over groups)
-  float l_part = 0.f;               // this lane's partial denominator for head `col`
-  f32x4 o_acc[DB];
+  m_run = -INFINITY;                // running max for head `col` (replicated over groups)
+  l_part = 0.f;                     // this lane's partial denominator for head `col`
 #pragma unroll
   for (int i = 0; i < DB; ++i) o_acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -150,6 +150,21 @@ __device__ __forceinline__ void decode_attn_core(
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before next overwrite
   }
+}
+
+template <int HD>
+__device__ __forceinline__ void decode_attn_core(
+    const bf16x8 (&qf)[HD / 32], u16* vt, int lane, int b, int kvh, int split, int G, int ctx,
+    int s_begin, int s_end, u16* __restrict__ out, const u16* __restrict__ k_cache,
+    const u16* __restrict__ v_cache, const int* __restrict__ block_tables, int max_blocks,
+    int hq, int hkv, int block_size, float scale_log2, int num_splits,
+    float* __restrict__ ws_o, float* __restrict__ ws_ml) {
+  constexpr int DB = HD / 16;
+  const int col = lane & 15, grp = lane >> 4;
+  f32x4 o_acc[DB];
+  float m_run, l_part;
+  decode_attn_loop<HD>(qf, vt, lane, b, kvh, s_begin, s_end, k_cache, v_cache, block_tables,
+                       max_blocks, hkv, block_size, scale_log2, o_acc, m_run, l_part);
   // ---- finalize: denominator of head `col`, then rows 4grp + r of O
   float l_tot = l_part + __shfl_xor(l_part, 16, 64);
   l_tot += __shfl_xor(l_tot, 32, 64);
@@ -221,6 +236,96 @@ __global__ void __launch_bounds__(256, MINW) decode_attn_kernel(
                        num_splits, ws_o, ws_ml);
 }
 
+// One (sequence, kv head) item per workgroup of WPI waves: wave wv walks the wv-th of WPI
+// equal slices of the context's 32-token tiles, then the partial (m, l, O) merge through
+// LDS (each wave's V-tile rows are reused for its O partial) and the workgroup writes the
+// GQA group's output rows. Small batches: with one item per wave most of the chip idles and
+// each wave pays one HBM round trip per tile of the whole context.
+template <int WPI>
+__device__ __forceinline__ void decode_attn_wg(
+    const bf16x8 (&qf)[4], u16 (*vtile_all)[DEC_TILE * 144], float (*ml_all)[16][2], int wv,
+    int lane, int b, int kvh, int G, int ctx, u16* __restrict__ out,
+    const u16* __restrict__ k_cache, const u16* __restrict__ v_cache,
+    const int* __restrict__ block_tables, int max_blocks, int hq, int hkv, int block_size,
+    float scale_log2) {
+  constexpr int HD = 128, DB = HD / 16;
+  static_assert(16 * HD * 4 <= DEC_TILE * 144 * 2, "O partials fit a wave's V tile");
+  const int col = lane & 15, grp = lane >> 4;
+  const int tiles = (ctx + DEC_TILE - 1) / DEC_TILE;
+  const int per = (tiles + WPI - 1) / WPI;
+  const int s_begin = min(ctx, wv * per * DEC_TILE);
+  const int s_end = min(ctx, s_begin + per * DEC_TILE);
+  f32x4 o_acc[DB];
+  float m_run, l_part;
+  decode_attn_loop<HD>(qf, vtile_all[wv], lane, b, kvh, s_begin, s_end, k_cache, v_cache,
+                       block_tables, max_blocks, hkv, block_size, scale_log2, o_acc, m_run,
+                       l_part);
+  float l_tot = l_part + __shfl_xor(l_part, 16, 64);
+  l_tot += __shfl_xor(l_tot, 32, 64);
+  float* po = reinterpret_cast<float*>(vtile_all[wv]);
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int i = 0; i < DB; ++i) po[(4 * grp + r) * HD + 16 * i + col] = o_acc[i][r];
+  if (grp == 0) {
+    ml_all[wv][col][0] = m_run;
+    ml_all[wv][col][1] = l_tot;
+  }
+  __syncthreads();
+  // merge: thread t -> head t / 16, dims 8 (t % 16) .. +7
+  const int h = threadIdx.x >> 4, d0 = (threadIdx.x & 15) * 8;
+  if (h >= G) return;
+  float M = -INFINITY;
+#pragma unroll
+  for (int w = 0; w < WPI; ++w) M = fmaxf(M, ml_all[w][h][0]);
+  float den = 0.f, acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int w = 0; w < WPI; ++w) {
+    const float mw = ml_all[w][h][0];
+    const float e = mw == -INFINITY ? 0.f : exp2f(mw - M);
+    den += e * ml_all[w][h][1];
+    const float4* o4 = reinterpret_cast<const float4*>(
+        reinterpret_cast<const float*>(vtile_all[w]) + h * HD + d0);
+    const float4 a = o4[0], c = o4[1];
+    acc[0] += e * a.x; acc[1] += e * a.y; acc[2] += e * a.z; acc[3] += e * a.w;
+    acc[4] += e * c.x; acc[5] += e * c.y; acc[6] += e * c.z; acc[7] += e * c.w;
+  }
+  const float inv = den > 0.f ? 1.f / den : 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] *= inv;
+  store8(out + ((long)b * hq + kvh * G + h) * HD + d0, acc);
+}
+
+// Small-batch form of decode_attn_kernel (head dim 128, one KV split): a workgroup per item.
+__global__ void __launch_bounds__(256) decode_attn_wg_kernel(
+    u16* __restrict__ out, const u16* __restrict__ q, int q_stride,
+    const u16* __restrict__ k_cache, const u16* __restrict__ v_cache,
+    const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ context_lens,
+    int B, int hq, int hkv, int block_size, float scale_log2) {
+  constexpr int HD = 128, KK = HD / 32, VROW = HD + 16;
+  __shared__ __attribute__((aligned(16))) u16 vtile_all[DEC_WAVES][DEC_TILE * VROW];
+  __shared__ float ml_all[DEC_WAVES][16][2];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int item = blockIdx.x;
+  const int kvh = item % hkv, b = item / hkv;
+  const int col = lane & 15, grp = lane >> 4;
+  const int G = hq / hkv;
+  bf16x8 qf[KK];
+  {
+    const bool valid = col < G;
+    const u16* qp = q + (long)b * q_stride + (long)(kvh * G + (valid ? col : 0)) * HD;
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      uint4 v = valid ? *reinterpret_cast<const uint4*>(qp + kk * 32 + grp * 8)
+                      : make_uint4(0, 0, 0, 0);
+      qf[kk] = *reinterpret_cast<bf16x8*>(&v);
+    }
+  }
+  decode_attn_wg<DEC_WAVES>(qf, vtile_all, ml_all, wv, lane, b, kvh, G, context_lens[b], out,
+                            k_cache, v_cache, block_tables, max_blocks, hq, hkv, block_size,
+                            scale_log2);
+}
+
 // Fused variant for the decode graph (one KV split per item): the QKV GEMM's split-K fp32
 // slabs go straight into the attention wave instead of through dli_splitk_rope_cache.
 // Prologue of item (sequence b, kv head h): lane l sums the slabs of this token's k and v
@@ -229,19 +334,29 @@ __global__ void __launch_bounds__(256, MINW) decode_attn_kernel(
 // the GQA group, dims 32kk + 8grp .. +7 and their RoPE partners 64 apart, which the same
 // lane holds) from the slabs. Numerics equal the unfused kernels: sum -> bf16 -> rotate ->
 // bf16. The q rows never go to memory, and one kernel per layer and its slab pass are gone.
-template <int SPL>
+//
+// WPI = 1: one wave per (sequence, kv head) item, 4 items per workgroup (large batches).
+// WPI = DEC_WAVES: one workgroup per item for small batches, where 4 items per workgroup
+// leave most of the chip idle and each wave walks the whole context serially (one HBM round
+// trip per 32-token tile): wave 0 writes the new k/v row, every wave builds the Q fragments,
+// wave w takes the w-th quarter of the context's tiles, and the four partial (m, l, O) merge
+// through LDS (the V-tile rows are reused for the O partials).
+template <int SPL, int WPI>
 __global__ void __launch_bounds__(256, 4) decode_attn_fused_kernel(
     u16* __restrict__ out, const float* __restrict__ ws, int N,
     const int* __restrict__ positions, const int* __restrict__ slot_mapping,
     const float* __restrict__ cos_sin, u16* __restrict__ k_cache, u16* __restrict__ v_cache,
     const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ context_lens,
     int B, int hq, int hkv, int block_size, float scale_log2) {
-  constexpr int HD = 128, HALF = 64, KK = HD / 32, VROW = HD + 16;
+  constexpr int HD = 128, HALF = 64, KK = HD / 32, VROW = HD + 16, DB = HD / 16;
+  static_assert(WPI == 1 || WPI == DEC_WAVES, "one item per wave or per workgroup");
   __shared__ __attribute__((aligned(16))) u16 vtile_all[DEC_WAVES][DEC_TILE * VROW];
-  u16* vt = vtile_all[threadIdx.x >> 6];
+  __shared__ float ml_all[WPI > 1 ? WPI : 1][16][2];
+  const int wv = threadIdx.x >> 6;
+  u16* vt = vtile_all[wv];
   const int lane = threadIdx.x & 63;
-  const int item = blockIdx.x * DEC_WAVES + (threadIdx.x >> 6);
-  if (item >= B * hkv) return;                                 // wave-uniform exit
+  const int item = WPI > 1 ? (int)blockIdx.x : (int)blockIdx.x * DEC_WAVES + wv;
+  if (item >= B * hkv) return;                                 // wave-uniform exit (WPI 1)
   const int kvh = item % hkv, b = item / hkv;
   const int col = lane & 15, grp = lane >> 4;
   const int G = hq / hkv;
@@ -251,7 +366,7 @@ __global__ void __launch_bounds__(256, 4) decode_attn_fused_kernel(
   const long splitstride = (long)B * N;
   // ---- this token's k (rotated) and v -> paged cache (lane: dims lane, lane + 64)
   const int slot = slot_mapping[b];
-  if (slot >= 0) {
+  if (slot >= 0 && (WPI == 1 || wv == 0)) {
     const float* kp = ws + rowoff + (long)(hq + kvh) * HD;
     const float* vp = ws + rowoff + (long)(hq + hkv + kvh) * HD;
     float k1 = 0.f, k2 = 0.f, v1 = 0.f, v2 = 0.f;
@@ -308,9 +423,15 @@ __global__ void __launch_bounds__(256, 4) decode_attn_fused_kernel(
       qf[kk] = *reinterpret_cast<bf16x8*>(&z);
     }
   }
-  decode_attn_core<HD>(qf, vt, lane, b, kvh, 0, G, ctx, 0, ctx, out, k_cache, v_cache,
-                       block_tables, max_blocks, hq, hkv, block_size, scale_log2, 1, nullptr,
-                       nullptr);
+  if constexpr (WPI == 1) {
+    decode_attn_core<HD>(qf, vt, lane, b, kvh, 0, G, ctx, 0, ctx, out, k_cache, v_cache,
+                         block_tables, max_blocks, hq, hkv, block_size, scale_log2, 1, nullptr,
+                         nullptr);
+  } else {
+    __syncthreads();                       // wave 0's cache row visible to the other waves
+    decode_attn_wg<WPI>(qf, vtile_all, ml_all, wv, lane, b, kvh, G, ctx, out, k_cache, v_cache,
+                        block_tables, max_blocks, hq, hkv, block_size, scale_log2);
+  }
 }
 
 // Software-pipelined variant: a wave walks a list of work units (item = (sequence, kv head,
@@ -602,6 +723,14 @@ extern "C" int dli_decode_get_pipe() {
   return g_decode_pipe;
 }
 
+// a workgroup per (sequence, kv head) item while the items alone would leave most CUs idle
+// (<= 256 items: B <= 32 at 8 kv heads); DLI_DECODE_WPI=1 / 4 forces either form
+static bool wg_form(long items) {
+  const char* e = getenv("DLI_DECODE_WPI");
+  const int v = e ? atoi(e) : 0;
+  return v == DEC_WAVES || (v != 1 && items <= 256);
+}
+
 extern "C" int dli_decode_attention(void* out, const void* q, int q_stride, const void* k_cache,
                                     const void* v_cache, const int* block_tables, int max_blocks,
                                     const int* context_lens, int B, int hq, int hkv, int hd,
@@ -635,6 +764,10 @@ extern "C" int dli_decode_attention(void* out, const void* q, int q_stride, cons
         (u16*)out, (const u16*)q, q_stride, (const u16*)k_cache, (const u16*)v_cache,
         block_tables, max_blocks, context_lens, B, hq, hkv, block_size, scale_log2, num_splits,
         split_tokens, ws_o, ws_ml);
+  } else if (hd == 128 && num_splits == 1 && wg_form(items)) {
+    decode_attn_wg_kernel<<<(int)items, 64 * DEC_WAVES, 0, st>>>(
+        (u16*)out, (const u16*)q, q_stride, (const u16*)k_cache, (const u16*)v_cache,
+        block_tables, max_blocks, context_lens, B, hq, hkv, block_size, scale_log2);
   } else {
   dim3 grid((int)((items + DEC_WAVES - 1) / DEC_WAVES));
   if (hd == 128)
@@ -672,11 +805,17 @@ extern "C" int dli_decode_attention_fused(void* out, const float* ws, int splits
     return (int)hipErrorInvalidValue;
   const int N = (hq + 2 * hkv) * hd;
   const float scale_log2 = scale * 1.4426950408889634f;
-  dim3 grid((int)(((long)B * hkv + DEC_WAVES - 1) / DEC_WAVES));
-#define DLI_DAF(S) decode_attn_fused_kernel<S><<<grid, 64 * DEC_WAVES, 0, st>>>(                \
+  const long items = (long)B * hkv;
+  const bool per_wg = wg_form(items);
+  dim3 grid((int)(per_wg ? items : (items + DEC_WAVES - 1) / DEC_WAVES));
+#define DLI_DAF(S, W) decode_attn_fused_kernel<S, W><<<grid, 64 * DEC_WAVES, 0, st>>>(          \
       (u16*)out, ws, N, positions, slot_mapping, cos_sin, (u16*)k_cache, (u16*)v_cache,      \
       block_tables, max_blocks, context_lens, B, hq, hkv, block_size, scale_log2)
-  if (splits == 2) DLI_DAF(2); else DLI_DAF(4);
+  if (per_wg) {
+    if (splits == 2) DLI_DAF(2, DEC_WAVES); else DLI_DAF(4, DEC_WAVES);
+  } else {
+    if (splits == 2) DLI_DAF(2, 1); else DLI_DAF(4, 1);
+  }
 #undef DLI_DAF
   DLI_RETURN_LAUNCH();
 }

@@ -119,3 +119,31 @@ extern "C" int dli_feed_ids(int* ids, const int* src, const int* feed, int n, in
   feed_ids_kernel<<<(n + 255) / 256, 256, 0, st>>>(ids, src, feed, n, n_feed);
   DLI_RETURN_LAUNCH();
 }
+
+// Read `bytes` of device memory and discard it: pulls a weight matrix into the memory-side
+// Infinity Cache (256 MB) ahead of the GEMM that streams it, from a side stream while the
+// main stream runs latency-bound work (decode attention, norms). 4 x 16 B in flight per lane;
+// the xor keeps the loads alive (the guarded store never happens for real data patterns).
+__global__ void __launch_bounds__(256) prefetch_kernel(const uint4* __restrict__ p, long n16,
+                                                       unsigned* __restrict__ sink) {
+  unsigned acc = 0;
+  const long stride = (long)gridDim.x * 256;
+  long i = (long)blockIdx.x * 256 + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    const uint4 a = p[i], b = p[i + stride], c = p[i + 2 * stride], d = p[i + 3 * stride];
+    acc ^= a.x ^ b.y ^ c.z ^ d.w;
+  }
+  for (; i < n16; i += stride) acc ^= p[i].x;
+  if (acc == 0x9e3779b9u) sink[threadIdx.x] = acc;
+}
+
+extern "C" int dli_prefetch(const void* p, long bytes, int max_wgs, void* sink, hipStream_t st) {
+  const long n16 = bytes / 16;
+  if (n16 <= 0) return 0;
+  if (((uintptr_t)p & 15) || sink == nullptr) return (int)hipErrorInvalidValue;
+  long wgs = (n16 + 1023) / 1024;
+  if (max_wgs <= 0) max_wgs = 256;
+  if (wgs > max_wgs) wgs = max_wgs;
+  prefetch_kernel<<<(int)wgs, 256, 0, st>>>((const uint4*)p, n16, (unsigned*)sink);
+  DLI_RETURN_LAUNCH();
+}

@@ -1020,7 +1020,7 @@ __device__ __forceinline__ float dot8_acc(const bf16x8v w, const bf16x8v x, floa
   return acc;
 }
 
-template <int MB, int RW, int EPI>
+template <int MB, int RW, int EPI, int UNROLL>
 __global__ void __launch_bounds__(256) gemv_kernel(
     const u16* __restrict__ A, int lda, const u16* __restrict__ W, int ldw,
     void* __restrict__ C, int ldc, int M, int N, int K, int k_split_len,
@@ -1050,19 +1050,23 @@ __global__ void __launch_bounds__(256) gemv_kernel(
 #pragma unroll
     for (int r = 0; r < RW; ++r) acc[m][r] = 0.f;
   int c = lane;
-  // two 64-chunk steps per iteration: 2 * RW weight loads in flight per lane
-  for (; c + 64 < nchunk; c += 128) {
-    bf16x8v w0[RW], w1[RW];
+  // UNROLL 64-chunk steps per iteration: UNROLL * RW weight loads in flight per lane (the
+  // short projections of a batch-1 layer run only a few iterations, so depth, not
+  // occupancy, hides the HBM latency)
+  for (; c + 64 * (UNROLL - 1) < nchunk; c += 64 * UNROLL) {
+    bf16x8v w[UNROLL][RW];
 #pragma unroll
-    for (int r = 0; r < RW; ++r) {
-      w0[r] = __builtin_nontemporal_load(wrow[r] + c);
-      w1[r] = __builtin_nontemporal_load(wrow[r] + c + 64);
-    }
+    for (int u = 0; u < UNROLL; ++u)
+#pragma unroll
+      for (int r = 0; r < RW; ++r) w[u][r] = __builtin_nontemporal_load(wrow[r] + c + 64 * u);
 #pragma unroll
     for (int m = 0; m < MB; ++m) {
-      const bf16x8v x0 = xrow[m][c], x1 = xrow[m][c + 64];
 #pragma unroll
-      for (int r = 0; r < RW; ++r) acc[m][r] = dot8_acc(w1[r], x1, dot8_acc(w0[r], x0, acc[m][r]));
+      for (int u = 0; u < UNROLL; ++u) {
+        const bf16x8v xv = xrow[m][c + 64 * u];
+#pragma unroll
+        for (int r = 0; r < RW; ++r) acc[m][r] = dot8_acc(w[u][r], xv, acc[m][r]);
+      }
     }
   }
   for (; c < nchunk; c += 64) {
@@ -1107,7 +1111,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(
   }
 }
 
-template <int MB, int RW, int EPI>
+template <int MB, int RW, int EPI, int UNROLL = 2>
 static int launch_gemv(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M,
                        int N, int K, int splits, const void* bias, void* ws, hipStream_t st) {
   constexpr int R = 4 * RW;
@@ -1117,7 +1121,7 @@ static int launch_gemv(const void* A, int lda, const void* W, int ldw, void* C, 
   ksl = (ksl / 8) * 8;
   if (ksl * splits != K) return (int)hipErrorInvalidValue;
   dim3 grid((N + R - 1) / R, splits);
-  gemv_kernel<MB, RW, EPI><<<grid, 256, 0, st>>>((const u16*)A, lda, (const u16*)W, ldw, C, ldc,
+  gemv_kernel<MB, RW, EPI, UNROLL><<<grid, 256, 0, st>>>((const u16*)A, lda, (const u16*)W, ldw, C, ldc,
                                                  M, N, K, ksl, (const u16*)bias,
                                                  splits > 1 ? (float*)ws : nullptr);
   if (splits > 1 && C != nullptr) {
@@ -1133,8 +1137,12 @@ template <int EPI>
 static int dispatch_gemv(int tile_cfg, const void* A, int lda, const void* W, int ldw, void* C,
                          int ldc, int M, int N, int K, int splits, const void* bias, void* ws,
                          hipStream_t st) {
-  // 30: 16 rows per workgroup, 31: 32 rows (the SiLU gate/up pairing needs 32)
+  // 30: 16 rows per workgroup, 31: 32 rows (the SiLU gate/up pairing needs 32), 32: 16 rows
+  // with 4 K-steps in flight per lane (M = 1)
   const bool r32 = tile_cfg == 31;
+  if (tile_cfg == 32)
+    return M <= 1 ? launch_gemv<1, 4, EPI, 4>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st)
+                  : (int)hipErrorInvalidValue;
   if (M <= 1)
     return r32 ? launch_gemv<1, 8, EPI>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st)
                : launch_gemv<1, 4, EPI>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st);
@@ -1176,7 +1184,7 @@ static int dispatch_tile(int tile_cfg, const void* A, int lda, const void* W, in
     // 256x224 ping-pong (gemm8p224_kernel): N = 28672 gate/up at M = 512 is 256 tiles
     case 26: return launch_8p224<EPI>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
     // skinny weight-streaming GEMM for M <= 4 (no grouped mode)
-    case 30: case 31:
+    case 30: case 31: case 32:
       if (go != nullptr) return (int)hipErrorInvalidValue;
       return dispatch_gemv<EPI>(tile_cfg, A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st);
 #undef DLI_CFG8

@@ -261,6 +261,22 @@ def feed_ids(ids, src, feed):
     return ids
 
 
+_sinks: dict = {}
+
+
+def prefetch(t: torch.Tensor, max_wgs: int = 256, nbytes: Optional[int] = None) -> None:
+    """Read ``t`` (its first ``nbytes``) on the current stream and discard it: the weight
+    lands in the Infinity Cache for the GEMM that streams it next (see
+    ``TransformerLM._llama_layers``). No-op off the GPU."""
+    if not _use_native(t):
+        return
+    sink = _sinks.get(t.device)
+    if sink is None:
+        sink = _sinks[t.device] = torch.empty(256, dtype=torch.int32, device=t.device)
+    n = t.numel() * t.element_size() if nbytes is None else int(nbytes)
+    _native_call("dli_prefetch", _p(t), n, int(max_wgs), _p(sink), _st())
+
+
 def silu_mul(gu):
     if not _use_native(gu):
         return R.silu_mul(gu)
@@ -357,7 +373,12 @@ def decode_num_splits(B: int, hkv: int, max_context: int) -> int:
     resident waves for long contexts, keeping >= 128 tokens per split."""
     items = B * hkv
     splits = 1
-    while items * splits < 2048 and max_context // (splits * 2) >= 128 and splits < 64:
+    # tiny batches (batch-1 latency): >= 512 tokens per split, so graphs captured for a
+    # 512-token table take the single-pass kernel with the fused QKV reduce / RoPE / cache
+    # prologue (the 4-split form cost rope + attention + merge = 23 us per layer at B = 1,
+    # profiles/r3/prof_b1_summary.txt)
+    min_tok = 512 if B <= 4 else 128
+    while items * splits < 2048 and max_context // (splits * 2) >= min_tok and splits < 64:
         splits *= 2
     return splits
 
@@ -543,10 +564,37 @@ def native_library_path():
     return N.loaded_path()
 
 
-def benchmark(fn, iters: int = 20, warmup: int = 3) -> float:
-    """Median milliseconds of fn() on the current stream (GPU) or wall clock (CPU)."""
+def benchmark(fn, iters: int = 20, warmup: int = 3, graph: bool = False) -> float:
+    """Median milliseconds of fn() on the current stream (GPU) or wall clock (CPU).
+    ``graph=True`` captures fn() in a HIP graph and times replays: the GPU time of a
+    launch-bound sequence as a decode graph runs it. Timed eagerly, a batch-1 GEMM (~15 us)
+    plus its consumer kernel cost less GPU time than the host spends launching them, so the
+    autotuner compared host launch overheads and picked plans at random (two runs of the
+    same bench took different decode paths)."""
     for _ in range(warmup):
         fn()
+    if graph and torch.cuda.is_available():
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            with torch.cuda.graph(g, stream=side):
+                fn()
+        torch.cuda.current_stream().wait_stream(side)
+        g.replay()
+        torch.cuda.synchronize()
+        times = []
+        for _ in range(iters):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            g.replay()
+            e.record()
+            e.synchronize()
+            times.append(s.elapsed_time(e))
+        del g
+        times.sort()
+        return times[len(times) // 2]
     if torch.cuda.is_available():
         torch.cuda.synchronize()
         times = []

@@ -38,6 +38,7 @@ _SIGS = {
     "dli_silu_mul": [P, P, I, I, P],
     "dli_bias_act": [P, P, I, I, I, P],
     "dli_feed_ids": [P, P, P, I, I, P],
+    "dli_prefetch": [P, L, I, P, P],
     "dli_decode_attention": [P, P, I, P, P, P, I, P, I, I, I, I, I, F, I, I, P, P],
     "dli_decode_attention_workspace_bytes": [I, I, I, I],
     "dli_prefill_attention": [P, I, P, I, P, I, I, I, I, I, F, P],

@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import os
 import threading
+import time
 from dataclasses import dataclass
 
 import numpy as np
@@ -43,7 +44,7 @@ TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256), 4: (256, 128),
          27: (256, 256)}
 # weight-streaming skinny GEMM (gemm.hip gemv_kernel) for M <= GEMV_MAX_M rows: 16 / 32 output
 # rows per workgroup (31 for the SiLU*up gate/up pairing); not an MFMA tile, so kept apart
-GEMV_TILES = {30: 16, 31: 32}
+GEMV_TILES = {30: 16, 31: 32, 32: 16}      # 32: 4 K-steps in flight per lane, M = 1
 GEMV_MAX_M = 4
 TILE_WAVES = {13: (2, 4), 14: (4, 2), 15: (2, 4), 16: (4, 2), 17: (2, 4),
               22: (2, 4), 23: (2, 4), 24: (2, 4), 25: (4, 2),
@@ -202,7 +203,7 @@ def autotune_grouped(rows: int, w: torch.Tensor, epi: str, iters: int = 5, log=N
         try:
             ms = ops.benchmark(lambda p=p: ops._gemm_native(
                 x, w, epi, plan=p, groups=E, group_off=off, rows_per_group=rows),
-                iters=iters, warmup=1)
+                iters=iters, warmup=1, graph=_GRAPH_TUNE)
         except Exception:  # noqa: BLE001
             continue
         if best is None or ms < best[1]:
@@ -277,6 +278,7 @@ def autotune(shapes, weights: dict, device, iters: int = 6, log=None,
             res = torch.zeros(M, N, dtype=w0.dtype, device=device)
             nw = torch.ones(N, dtype=w0.dtype, device=device)
         best = None
+        t_shape = time.perf_counter()
         for p in candidate_plans(M, N, K, epi):
             if p.backend == "hipblaslt" and epi not in ("none", "splitk", "silu_mul", "f32"):
                 continue
@@ -288,7 +290,7 @@ def autotune(shapes, weights: dict, device, iters: int = 6, log=None,
                     else:
                         ops._gemm_native(x, w, epi, plan=p)
             try:
-                ms = ops.benchmark(run, iters=iters, warmup=1) / len(ws_)
+                ms = ops.benchmark(run, iters=iters, warmup=1, graph=_GRAPH_TUNE) / len(ws_)
             except Exception:  # noqa: BLE001 — an invalid candidate is skipped
                 continue
             if best is None or ms < best[1]:
@@ -302,11 +304,14 @@ def autotune(shapes, weights: dict, device, iters: int = 6, log=None,
                 _tuned.add((_bucket(M), N, K, "none"))
             out[(M, N, K, epi)] = best
             if log:
-                log(f"[gemm autotune] M={M} N={N} K={K} {epi}: {best[0]} {best[1]*1e3:.1f} us")
+                log(f"[gemm autotune] M={M} N={N} K={K} {epi}: {best[0]} {best[1]*1e3:.1f} us "
+                    f"({time.perf_counter() - t_shape:.1f} s)")
     return out
 
 
 _tuned: set = set()
+# candidates timed as graph replays (ops.benchmark graph=True); DLI_GEMM_TUNE_GRAPH=0: eager
+_GRAPH_TUNE = os.environ.get("DLI_GEMM_TUNE_GRAPH", "1") == "1"
 
 
 def candidate_plans(M: int, N: int, K: int, epi: str):
@@ -334,7 +339,7 @@ def candidate_plans(M: int, N: int, K: int, epi: str):
             out.append(GemmPlan("dli", tile, splits))
     if M <= GEMV_MAX_M:
         for tile in GEMV_TILES:
-            if tile in excl or not tile_ok(tile, epi):
+            if tile in excl or not tile_ok(tile, epi) or (tile == 32 and M > 1):
                 continue
             for splits in (1, 2, 4, 8):
                 if K % (64 * splits) == 0 and K // splits >= 512:

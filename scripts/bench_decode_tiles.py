@@ -57,7 +57,7 @@ def main():
                              "error": str(e)[:80]})
                 continue
             rows.append({"shape": name, "M": a.m, "slab_store": a.slab_store, "tile": p.tile,
-                         "bm_bn": G.TILES[p.tile],
+                         "bm_bn": G.TILES.get(p.tile, ("gemv", G.GEMV_TILES.get(p.tile))),
                          "splits": p.splits, "us": round(ms * 1e3, 2),
                          "tflops": round(2 * a.m * N * K / (ms * 1e-3) / 1e12, 1)})
         for r in sorted(rows, key=lambda r: r.get("us", 1e9))[:a.top or None]:
