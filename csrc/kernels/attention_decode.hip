@@ -21,6 +21,7 @@
 // [nblk,Hkv,bs,hd] (token-major: the per-step cache write is a contiguous row),
 // block_tables [B, max_blocks], out [B, Hq, hd].
 #include "common.h"
+#include <limits.h>
 #include <stdlib.h>
 
 #define DEC_WAVES 4
@@ -33,12 +34,31 @@ typedef short s16x8 __attribute__((ext_vector_type(8)));
 // split) item with its Q^T fragments already in registers.
 // The tile loop over tokens [s_begin, s_end): leaves the unnormalised O rows in o_acc, the
 // running max of head `col` in m_run and this lane's partial denominator in l_part.
+// The first 64-block window of the block-table row of tokens [s_begin, s_end), one block id
+// per lane (decode_attn_loop's bt_lane0): loaded by the caller so that the load can be
+// issued ahead of the prologue's cache write and its fence.
+__device__ __forceinline__ int decode_bt_window(const int* __restrict__ block_tables,
+                                                int max_blocks, int b, int s_begin, int s_end,
+                                                int block_size, int lane) {
+  const int last_blk = max(s_end - 1, 0) / block_size;
+  return block_tables[(long)b * max_blocks + min(s_begin / block_size + lane, last_blk)];
+}
+
+// [s_begin, s_end) of wave wv when WPI waves split a context of ctx tokens by whole tiles
+template <int WPI>
+__device__ __forceinline__ void decode_wg_range(int ctx, int wv, int& s_begin, int& s_end) {
+  const int tiles = (ctx + DEC_TILE - 1) / DEC_TILE;
+  const int per = (tiles + WPI - 1) / WPI;
+  s_begin = min(ctx, wv * per * DEC_TILE);
+  s_end = min(ctx, s_begin + per * DEC_TILE);
+}
+
 template <int HD>
 __device__ __forceinline__ void decode_attn_loop(
     const bf16x8 (&qf)[HD / 32], u16* vt, int lane, int b, int kvh, int s_begin, int s_end,
     const u16* __restrict__ k_cache, const u16* __restrict__ v_cache,
     const int* __restrict__ block_tables, int max_blocks, int hkv, int block_size,
-    float scale_log2, f32x4 (&o_acc)[HD / 16], float& m_run, float& l_part) {
+    float scale_log2, int bt_lane0, f32x4 (&o_acc)[HD / 16], float& m_run, float& l_part) {
   constexpr int DB = HD / 16;     // 16-wide output column blocks (= V pieces per lane)
   constexpr int KK = HD / 32;
   constexpr int VROW = HD + 16;   // padded LDS row of the V tile, in u16
@@ -49,7 +69,7 @@ __device__ __forceinline__ void decode_attn_loop(
   // lane shuffle): the per-tile K/V loads no longer wait on a dependent block-table load
   const int last_blk = max(s_end - 1, 0) / block_size;
   int win = s_begin / block_size;
-  int bt_lane = bt[min(win + lane, last_blk)];
+  int bt_lane = bt_lane0;
   const long kv_head_stride = (long)block_size * HD;           // elements per (blk, head)
   m_run = -INFINITY;                // running max for head `col` (replicated over groups)
   l_part = 0.f;                     // this lane's partial denominator for head `col`
@@ -158,13 +178,15 @@ __device__ __forceinline__ void decode_attn_core(
     int s_begin, int s_end, u16* __restrict__ out, const u16* __restrict__ k_cache,
     const u16* __restrict__ v_cache, const int* __restrict__ block_tables, int max_blocks,
     int hq, int hkv, int block_size, float scale_log2, int num_splits,
-    float* __restrict__ ws_o, float* __restrict__ ws_ml) {
+    float* __restrict__ ws_o, float* __restrict__ ws_ml, int bt_lane0 = INT_MIN) {
   constexpr int DB = HD / 16;
   const int col = lane & 15, grp = lane >> 4;
   f32x4 o_acc[DB];
   float m_run, l_part;
+  if (bt_lane0 == INT_MIN)
+    bt_lane0 = decode_bt_window(block_tables, max_blocks, b, s_begin, s_end, block_size, lane);
   decode_attn_loop<HD>(qf, vt, lane, b, kvh, s_begin, s_end, k_cache, v_cache, block_tables,
-                       max_blocks, hkv, block_size, scale_log2, o_acc, m_run, l_part);
+                       max_blocks, hkv, block_size, scale_log2, bt_lane0, o_acc, m_run, l_part);
   // ---- finalize: denominator of head `col`, then rows 4grp + r of O
   float l_tot = l_part + __shfl_xor(l_part, 16, 64);
   l_tot += __shfl_xor(l_tot, 32, 64);
@@ -244,22 +266,18 @@ __global__ void __launch_bounds__(256, MINW) decode_attn_kernel(
 template <int WPI>
 __device__ __forceinline__ void decode_attn_wg(
     const bf16x8 (&qf)[4], u16 (*vtile_all)[DEC_TILE * 144], float (*ml_all)[16][2], int wv,
-    int lane, int b, int kvh, int G, int ctx, u16* __restrict__ out,
-    const u16* __restrict__ k_cache, const u16* __restrict__ v_cache,
+    int lane, int b, int kvh, int G, int s_begin, int s_end, int bt_lane0,
+    u16* __restrict__ out, const u16* __restrict__ k_cache, const u16* __restrict__ v_cache,
     const int* __restrict__ block_tables, int max_blocks, int hq, int hkv, int block_size,
     float scale_log2) {
   constexpr int HD = 128, DB = HD / 16;
   static_assert(16 * HD * 4 <= DEC_TILE * 144 * 2, "O partials fit a wave's V tile");
   const int col = lane & 15, grp = lane >> 4;
-  const int tiles = (ctx + DEC_TILE - 1) / DEC_TILE;
-  const int per = (tiles + WPI - 1) / WPI;
-  const int s_begin = min(ctx, wv * per * DEC_TILE);
-  const int s_end = min(ctx, s_begin + per * DEC_TILE);
   f32x4 o_acc[DB];
   float m_run, l_part;
   decode_attn_loop<HD>(qf, vtile_all[wv], lane, b, kvh, s_begin, s_end, k_cache, v_cache,
-                       block_tables, max_blocks, hkv, block_size, scale_log2, o_acc, m_run,
-                       l_part);
+                       block_tables, max_blocks, hkv, block_size, scale_log2, bt_lane0, o_acc,
+                       m_run, l_part);
   float l_tot = l_part + __shfl_xor(l_part, 16, 64);
   l_tot += __shfl_xor(l_tot, 32, 64);
   float* po = reinterpret_cast<float*>(vtile_all[wv]);
@@ -321,9 +339,12 @@ __global__ void __launch_bounds__(256) decode_attn_wg_kernel(
       qf[kk] = *reinterpret_cast<bf16x8*>(&v);
     }
   }
-  decode_attn_wg<DEC_WAVES>(qf, vtile_all, ml_all, wv, lane, b, kvh, G, context_lens[b], out,
-                            k_cache, v_cache, block_tables, max_blocks, hq, hkv, block_size,
-                            scale_log2);
+  int s_begin, s_end;
+  decode_wg_range<DEC_WAVES>(context_lens[b], wv, s_begin, s_end);
+  const int bt0 = decode_bt_window(block_tables, max_blocks, b, s_begin, s_end, block_size, lane);
+  decode_attn_wg<DEC_WAVES>(qf, vtile_all, ml_all, wv, lane, b, kvh, G, s_begin, s_end, bt0,
+                            out, k_cache, v_cache, block_tables, max_blocks, hq, hkv,
+                            block_size, scale_log2);
 }
 
 // Fused variant for the decode graph (one KV split per item): the QKV GEMM's split-K fp32
@@ -343,12 +364,16 @@ __global__ void __launch_bounds__(256) decode_attn_wg_kernel(
 // through LDS (the V-tile rows are reused for the O partials).
 template <int SPL, int WPI>
 __global__ void __launch_bounds__(256, 4) decode_attn_fused_kernel(
-    u16* __restrict__ out, const float* __restrict__ ws, int N,
+    u16* __restrict__ out, const void* __restrict__ src, int N,
     const int* __restrict__ positions, const int* __restrict__ slot_mapping,
     const float* __restrict__ cos_sin, u16* __restrict__ k_cache, u16* __restrict__ v_cache,
     const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ context_lens,
     int B, int hq, int hkv, int block_size, float scale_log2) {
   constexpr int HD = 128, HALF = 64, KK = HD / 32, VROW = HD + 16, DB = HD / 16;
+  // SPL > 0: src = the QKV GEMM's fp32 split-K slabs [SPL, B, N]; SPL == 0: the bf16 QKV rows
+  // [B, N] of an unsplit GEMM (the same prologue minus the slab sum)
+  const float* ws = static_cast<const float*>(src);
+  const u16* qkv = static_cast<const u16*>(src);
   static_assert(WPI == 1 || WPI == DEC_WAVES, "one item per wave or per workgroup");
   __shared__ __attribute__((aligned(16))) u16 vtile_all[DEC_WAVES][DEC_TILE * VROW];
   __shared__ float ml_all[WPI > 1 ? WPI : 1][16][2];
@@ -364,33 +389,9 @@ __global__ void __launch_bounds__(256, 4) decode_attn_fused_kernel(
   const float* cs = cos_sin + (long)positions[b] * HD;
   const long rowoff = (long)b * N;
   const long splitstride = (long)B * N;
-  // ---- this token's k (rotated) and v -> paged cache (lane: dims lane, lane + 64)
-  const int slot = slot_mapping[b];
-  if (slot >= 0 && (WPI == 1 || wv == 0)) {
-    const float* kp = ws + rowoff + (long)(hq + kvh) * HD;
-    const float* vp = ws + rowoff + (long)(hq + hkv + kvh) * HD;
-    float k1 = 0.f, k2 = 0.f, v1 = 0.f, v2 = 0.f;
-#pragma unroll
-    for (int s = 0; s < SPL; ++s) {
-      k1 += kp[s * splitstride + lane];
-      k2 += kp[s * splitstride + HALF + lane];
-      v1 += vp[s * splitstride + lane];
-      v2 += vp[s * splitstride + HALF + lane];
-    }
-    k1 = bf2f(f2bf(k1)); k2 = bf2f(f2bf(k2));
-    const float co = cs[lane], si = cs[HALF + lane];
-    const int blk = slot / block_size, off = slot - blk * block_size;
-    const long dst = (((long)blk * hkv + kvh) * block_size + off) * HD;
-    k_cache[dst + lane] = f2bf(k1 * co - k2 * si);
-    k_cache[dst + HALF + lane] = f2bf(k2 * co + k1 * si);
-    v_cache[dst + lane] = f2bf(v1);
-    v_cache[dst + HALF + lane] = f2bf(v2);
-  }
-  // the tile loop below reads this row back (other lanes of this wave): order the stores
-  // before those loads
-  __threadfence_block();
-  // ---- Q^T fragments: head col of the group, dims 32kk + 8grp .. +7 (kk < 2: first half,
-  // its RoPE partner is fragment kk + 2 of the same lane)
+  // ---- Q^T fragments (first: their slab loads do not wait on the cache write below): head
+  // col of the group, dims 32kk + 8grp .. +7 (kk < 2: first half, its RoPE partner is
+  // fragment kk + 2 of the same lane)
   bf16x8 qf[KK];
   if (col < G) {
     const float* qp = ws + rowoff + (long)(kvh * G + col) * HD;
@@ -398,6 +399,11 @@ __global__ void __launch_bounds__(256, 4) decode_attn_fused_kernel(
     for (int kp2 = 0; kp2 < KK / 2; ++kp2) {
       const int d1 = 32 * kp2 + 8 * grp;
       float x1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, x2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      if constexpr (SPL == 0) {
+        const u16* qr = qkv + rowoff + (long)(kvh * G + col) * HD;
+        load8(qr + d1, x1);
+        load8(qr + HALF + d1, x2);
+      }
 #pragma unroll
       for (int s = 0; s < SPL; ++s) {
         const float4* a = reinterpret_cast<const float4*>(qp + s * splitstride + d1);
@@ -423,14 +429,52 @@ __global__ void __launch_bounds__(256, 4) decode_attn_fused_kernel(
       qf[kk] = *reinterpret_cast<bf16x8*>(&z);
     }
   }
+  // the block-table window too: every load the tile loop's first tile waits on except the
+  // new cache row is issued before the fence below
+  int s_begin = 0, s_end = ctx;
+  if constexpr (WPI > 1) decode_wg_range<WPI>(ctx, wv, s_begin, s_end);
+  const int bt0 = decode_bt_window(block_tables, max_blocks, b, s_begin, s_end, block_size, lane);
+  // ---- this token's k (rotated) and v -> paged cache (lane: dims lane, lane + 64)
+  const int slot = slot_mapping[b];
+  if (slot >= 0 && (WPI == 1 || wv == 0)) {
+    const float* kp = ws + rowoff + (long)(hq + kvh) * HD;
+    const float* vp = ws + rowoff + (long)(hq + hkv + kvh) * HD;
+    float k1 = 0.f, k2 = 0.f, v1 = 0.f, v2 = 0.f;
+    if constexpr (SPL > 0) {
+#pragma unroll
+      for (int s = 0; s < SPL; ++s) {
+        k1 += kp[s * splitstride + lane];
+        k2 += kp[s * splitstride + HALF + lane];
+        v1 += vp[s * splitstride + lane];
+        v2 += vp[s * splitstride + HALF + lane];
+      }
+    } else {
+      const u16* kr = qkv + rowoff + (long)(hq + kvh) * HD;
+      const u16* vr = qkv + rowoff + (long)(hq + hkv + kvh) * HD;
+      k1 = bf2f(kr[lane]); k2 = bf2f(kr[HALF + lane]);
+      v1 = bf2f(vr[lane]); v2 = bf2f(vr[HALF + lane]);
+    }
+    k1 = bf2f(f2bf(k1)); k2 = bf2f(f2bf(k2));
+    const float co = cs[lane], si = cs[HALF + lane];
+    const int blk = slot / block_size, off = slot - blk * block_size;
+    const long dst = (((long)blk * hkv + kvh) * block_size + off) * HD;
+    k_cache[dst + lane] = f2bf(k1 * co - k2 * si);
+    k_cache[dst + HALF + lane] = f2bf(k2 * co + k1 * si);
+    v_cache[dst + lane] = f2bf(v1);
+    v_cache[dst + HALF + lane] = f2bf(v2);
+  }
+  // the tile loop below reads this row back (other lanes of this wave): order the stores
+  // before those loads
+  __threadfence_block();
   if constexpr (WPI == 1) {
     decode_attn_core<HD>(qf, vt, lane, b, kvh, 0, G, ctx, 0, ctx, out, k_cache, v_cache,
                          block_tables, max_blocks, hq, hkv, block_size, scale_log2, 1, nullptr,
-                         nullptr);
+                         nullptr, bt0);
   } else {
     __syncthreads();                       // wave 0's cache row visible to the other waves
-    decode_attn_wg<WPI>(qf, vtile_all, ml_all, wv, lane, b, kvh, G, ctx, out, k_cache, v_cache,
-                        block_tables, max_blocks, hq, hkv, block_size, scale_log2);
+    decode_attn_wg<WPI>(qf, vtile_all, ml_all, wv, lane, b, kvh, G, s_begin, s_end, bt0, out,
+                        k_cache, v_cache, block_tables, max_blocks, hq, hkv, block_size,
+                        scale_log2);
   }
 }
 
@@ -793,15 +837,17 @@ extern "C" int dli_decode_attention(void* out, const void* q, int q_stride, cons
 }
 
 // Fused split-K QKV reduce + RoPE + KV-cache write + decode attention (one KV split, head
-// dim 128, RoPE models): ws = the QKV GEMM's fp32 slabs [splits, B, (hq + 2 hkv) * 128].
-extern "C" int dli_decode_attention_fused(void* out, const float* ws, int splits,
+// dim 128, RoPE models): ws = the QKV GEMM's fp32 slabs [splits, B, (hq + 2 hkv) * 128], or
+// with splits == 0 the bf16 QKV rows [B, (hq + 2 hkv) * 128] of an unsplit GEMM.
+extern "C" int dli_decode_attention_fused(void* out, const void* ws, int splits,
                                           const int* positions, const int* slot_mapping,
                                           const float* cos_sin, void* k_cache, void* v_cache,
                                           const int* block_tables, int max_blocks,
                                           const int* context_lens, int B, int hq, int hkv,
                                           int hd, int block_size, float scale, hipStream_t st) {
   if (B <= 0) return 0;
-  if (hd != 128 || hq % hkv || hq / hkv > 16 || block_size % 16 || (splits != 2 && splits != 4))
+  if (hd != 128 || hq % hkv || hq / hkv > 16 || block_size % 16 ||
+      (splits != 0 && splits != 2 && splits != 4))
     return (int)hipErrorInvalidValue;
   const int N = (hq + 2 * hkv) * hd;
   const float scale_log2 = scale * 1.4426950408889634f;
@@ -812,9 +858,13 @@ extern "C" int dli_decode_attention_fused(void* out, const float* ws, int splits
       (u16*)out, ws, N, positions, slot_mapping, cos_sin, (u16*)k_cache, (u16*)v_cache,      \
       block_tables, max_blocks, context_lens, B, hq, hkv, block_size, scale_log2)
   if (per_wg) {
-    if (splits == 2) DLI_DAF(2, DEC_WAVES); else DLI_DAF(4, DEC_WAVES);
+    if (splits == 0) DLI_DAF(0, DEC_WAVES);
+    else if (splits == 2) DLI_DAF(2, DEC_WAVES);
+    else DLI_DAF(4, DEC_WAVES);
   } else {
-    if (splits == 2) DLI_DAF(2, 1); else DLI_DAF(4, 1);
+    if (splits == 0) DLI_DAF(0, 1);
+    else if (splits == 2) DLI_DAF(2, 1);
+    else DLI_DAF(4, 1);
   }
 #undef DLI_DAF
   DLI_RETURN_LAUNCH();

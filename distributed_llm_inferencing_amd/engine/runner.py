@@ -212,7 +212,9 @@ class StageRunner:
                and m.layers[0]["w_gu"].dim() == 3)
         for b in (buckets or self.buckets):
             shapes, weights = self.gemm_shapes(b)
-            G.autotune(shapes, weights, self.device, log=log)
+            c = m.cfg
+            qkv = ((c.num_heads, c.num_kv_heads, c.head_dim) if c.arch != "gpt2" else None)
+            G.autotune(shapes, weights, self.device, log=log, qkv_heads=qkv)
             if moe:      # grouped expert GEMMs: rows = b tokens x top-k (uniform routing)
                 lp = m.layers[0]
                 rows = b * m.cfg.top_k_experts

@@ -195,11 +195,15 @@ def linear_add_rmsnorm(x, w, residual, norm_w, eps, plan: Optional[G.GemmPlan] =
 
 
 def linear_rope_cache(x, w, positions, slot_mapping, cos_sin, k_cache, v_cache, hq, hkv, hd,
-                      use_rope: bool = True):
-    """qkv = x @ w.T with RoPE applied in place to q,k and k,v written to the paged cache."""
-    p = _splitk_plan(x, w)
+                      use_rope: bool = True, plan: Optional[G.GemmPlan] = None):
+    """qkv = x @ w.T with RoPE applied in place to q,k and k,v written to the paged cache.
+    ``plan`` forces the GEMM plan (the autotuner times QKV candidates with this consumer)."""
+    if plan is None:
+        p = _splitk_plan(x, w)
+    else:
+        p = plan if (plan.backend == "dli" and plan.splits > 1) else None
     if p is None:
-        qkv = linear(x, w)
+        qkv = linear(x, w) if plan is None else _gemm_native(x, w, "none", plan=plan)
         rope_and_cache(qkv, positions, slot_mapping, cos_sin, k_cache, v_cache, hq, hkv, hd,
                        use_rope)
         return qkv
@@ -218,17 +222,18 @@ def linear_rope_cache(x, w, positions, slot_mapping, cos_sin, k_cache, v_cache, 
 
 def linear_rope_attention(x, w, positions, slot_mapping, cos_sin, k_cache, v_cache,
                           block_tables, context_lens, max_context: int, hq, hkv, hd, scale):
-    """Decode step, one fused pass after the QKV GEMM: the split-K slabs are reduced, q and k
-    rotated, k/v written to the paged cache and attention computed by ONE kernel per layer
-    (``dli_decode_attention_fused``) instead of ``linear_rope_cache`` + ``decode_attention``.
-    Returns the attention output [B, hq*hd], or None where the fused kernel does not apply
-    (the caller then runs the two-kernel path): unsplit QKV plans, KV-split attention (short
-    batches / long contexts: its merge workspace is the GEMM's slab workspace), the
+    """Decode step, one fused pass after the QKV GEMM: the split-K slabs (or, for an unsplit
+    plan, the bf16 QKV rows) are reduced, q and k rotated, k/v written to the paged cache and
+    attention computed by ONE kernel per layer (``dli_decode_attention_fused``) instead of
+    ``linear_rope_cache`` + ``decode_attention``. Returns the attention output [B, hq*hd], or
+    None where the fused kernel does not apply (the caller then runs the two-kernel path):
+    split counts other than 2 / 4, KV-split attention (long contexts at small batch), the
     pipelined long-context kernel, head dim != 128. ``DLI_FUSED_ROPE_ATTN=0`` turns it off."""
-    if os.environ.get("DLI_FUSED_ROPE_ATTN", "1") != "1" or hd != 128 or k_cache is None:
+    if (os.environ.get("DLI_FUSED_ROPE_ATTN", "1") != "1" or hd != 128 or k_cache is None
+            or not _use_native(x)):
         return None
     p = _splitk_plan(x, w)
-    if p is None or p.splits not in (2, 4):
+    if p is not None and p.splits not in (2, 4):
         return None
     B, K = x.shape
     if decode_num_splits(B, hkv, max_context) != 1:
@@ -237,11 +242,14 @@ def linear_rope_attention(x, w, positions, slot_mapping, cos_sin, k_cache, v_cac
     if mode == 1 or (mode == 2 and -(-max_context // 32) * 32 >= 768):
         return None                       # dli_decode_attention picks the pipelined kernel
     Nn = w.shape[0]
-    ws = G.workspace(x.device, p.splits * B * Nn * 4)
-    _native_call("dli_gemm", _p(x), x.stride(0), _p(w), w.stride(-2), None, Nn, B, Nn, K,
-                 0, p.tile, p.splits, None, _p(ws), None, 1, _st())
+    if p is None:                         # unsplit plan: the prologue reads the bf16 rows
+        src, splits = linear(x, w), 0
+    else:
+        src, splits = G.workspace(x.device, p.splits * B * Nn * 4), p.splits
+        _native_call("dli_gemm", _p(x), x.stride(0), _p(w), w.stride(-2), None, Nn, B, Nn, K,
+                     0, p.tile, p.splits, None, _p(src), None, 1, _st())
     out = torch.empty(B, hq * hd, dtype=x.dtype, device=x.device)
-    _native_call("dli_decode_attention_fused", _p(out), _p(ws), p.splits, _p(positions),
+    _native_call("dli_decode_attention_fused", _p(out), _p(src), splits, _p(positions),
                  _p(slot_mapping), _p(cos_sin), _p(k_cache), _p(v_cache), _p(block_tables),
                  block_tables.stride(0), _p(context_lens), B, hq, hkv, hd, k_cache.shape[2],
                  scale, _st())

@@ -250,7 +250,7 @@ def clear_plans() -> None:
 
 
 def autotune(shapes, weights: dict, device, iters: int = 6, log=None,
-             cold_bytes: int = 1 << 30) -> dict:
+             cold_bytes: int = 1 << 30, qkv_heads=None) -> dict:
     """Measure every candidate plan for each (M, N, K, epi) and pin the fastest
     ("measure, don't guess"). ``weights[(N, K)]`` is a real [N, K] weight of that shape.
 
@@ -259,6 +259,10 @@ def autotune(shapes, weights: dict, device, iters: int = 6, log=None,
     picked plans that ran 12 % slower in the model), and split-K plans pay their slab
     reduction (a "splitk" GEMM feeds a fused reduce that reads every slab). A non-split
     winner for a "splitk" shape also becomes that shape's plain plan (unfused path).
+    ``qkv_heads`` = (hq, hkv, hd): the "splitk" shape with N = (hq + 2 hkv) hd is the fused
+    QKV projection, whose consumer is the decode attention prologue (slab sum or bf16 read,
+    RoPE, KV write), so its candidates are timed with the RoPE + cache-write kernel of the
+    same input (``ops.linear_rope_cache``) instead of the add + RMSNorm one.
     Returns {shape: (plan, ms)}."""
     from .. import ops  # local import: ops imports this module
     out = {}
@@ -270,13 +274,22 @@ def autotune(shapes, weights: dict, device, iters: int = 6, log=None,
         n_copies = max(2, min(16, -(-cold_bytes // (w0.numel() * w0.element_size()))))
         ws_ = [w0] + [w0.clone() for _ in range(n_copies - 1)]
         x = (torch.randn(M, K, device=device) * 0.5).to(w0.dtype)
+        is_qkv = (epi == "splitk" and qkv_heads is not None
+                  and N == (qkv_heads[0] + 2 * qkv_heads[1]) * qkv_heads[2])
         if epi == "splitk":
             # a "splitk" GEMM is timed WITH its consumer: split plans reduce their slabs in a
             # fused add+RMSNorm, unsplit plans write bf16 and run the separate add+RMSNorm
-            # pass (for QKV the real consumers are the RoPE/cache kernels of the same bytes
-            # pattern); timing the unsplit GEMM alone hid that pass and biased the choice
+            # pass; timing the unsplit GEMM alone hid that pass and biased the choice
             res = torch.zeros(M, N, dtype=w0.dtype, device=device)
             nw = torch.ones(N, dtype=w0.dtype, device=device)
+        if is_qkv:
+            from . import reference as R
+            hq, hkv, hd = qkv_heads
+            pos = torch.zeros(M, dtype=torch.int32, device=device)
+            slots = torch.arange(M, dtype=torch.int32, device=device)
+            kc = torch.empty(-(-M // 16), hkv, 16, hd, dtype=w0.dtype, device=device)
+            vc = torch.empty_like(kc)
+            cs = R.rope_cos_sin(16, hd, 10000.0, device=device)
         best = None
         t_shape = time.perf_counter()
         for p in candidate_plans(M, N, K, epi):
@@ -285,7 +298,10 @@ def autotune(shapes, weights: dict, device, iters: int = 6, log=None,
 
             def run(p=p):
                 for w in ws_:
-                    if epi == "splitk":
+                    if is_qkv:
+                        ops.linear_rope_cache(x, w, pos, slots, cs, kc, vc, hq, hkv, hd,
+                                              plan=p)
+                    elif epi == "splitk":
                         ops.linear_add_rmsnorm(x, w, res, nw, 1e-5, plan=p)
                     else:
                         ops._gemm_native(x, w, epi, plan=p)

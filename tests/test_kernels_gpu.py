@@ -299,12 +299,13 @@ def test_decode_attention_paged(gpu, hq, hkv, hd, bs, lens):
 
 
 @pytest.mark.parametrize("wpi", ["1", "4"])
-@pytest.mark.parametrize("splits", [2, 4])
+@pytest.mark.parametrize("splits", [1, 2, 4])
 @pytest.mark.parametrize("hq,hkv", [(32, 8), (8, 1)])
 def test_fused_rope_attention(gpu, monkeypatch, hq, hkv, splits, wpi):
     """dli_decode_attention_fused (split-K QKV reduce + RoPE + KV write + attention in one
     kernel) == linear_rope_cache + decode_attention: the same cache bytes, the same output,
-    and the output matches the fp32 reference. wpi 1 = a wave per (sequence, kv head), 4 = a
+    and the output matches the fp32 reference. splits 1: an unsplit QKV plan (the prologue
+    reads the bf16 QKV rows). wpi 1 = a wave per (sequence, kv head), 4 = a
     workgroup per item with the context split over its waves and merged in LDS."""
     monkeypatch.setenv("DLI_DECODE_WPI", wpi)
     hd, bs = 128, 16
