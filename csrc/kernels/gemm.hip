@@ -1020,16 +1020,14 @@ __device__ __forceinline__ float dot8_acc(const bf16x8v w, const bf16x8v x, floa
   return acc;
 }
 
-template <int MB, int RW, int EPI, int UNROLL>
-__global__ void __launch_bounds__(256) gemv_kernel(
-    const u16* __restrict__ A, int lda, const u16* __restrict__ W, int ldw,
-    void* __restrict__ C, int ldc, int M, int N, int K, int k_split_len,
-    const u16* __restrict__ bias, float* __restrict__ ws) {
-  constexpr int R = 4 * RW;
-  __shared__ float res[MB][R];
+// The weight stream of one workgroup: res[m][j] = sum over this K slice of
+// A[m, :] . W[n_base + j, :] (j < R = 4 RW), reduced across the wave and staged in LDS.
+template <int MB, int RW, int UNROLL>
+__device__ __forceinline__ void gemv_core(const u16* __restrict__ A, int lda,
+                                          const u16* __restrict__ W, int ldw, int M, int N,
+                                          int K, int k_split_len, int n_base, int ks,
+                                          float (&res)[MB][4 * RW]) {
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int n_base = blockIdx.x * R;
-  const int ks = blockIdx.y;
   const int kb = ks * k_split_len;
   const int klen = min(k_split_len, K - kb);
   const int nchunk = klen >> 3;                     // 8-element chunks of the K slice
@@ -1087,6 +1085,18 @@ __global__ void __launch_bounds__(256) gemv_kernel(
       const float v = wave_sum(acc[m][r]);
       if (lane == 0) res[m][wid * RW + r] = v;
     }
+}
+
+template <int MB, int RW, int EPI, int UNROLL>
+__global__ void __launch_bounds__(256) gemv_kernel(
+    const u16* __restrict__ A, int lda, const u16* __restrict__ W, int ldw,
+    void* __restrict__ C, int ldc, int M, int N, int K, int k_split_len,
+    const u16* __restrict__ bias, float* __restrict__ ws) {
+  constexpr int R = 4 * RW;
+  __shared__ float res[MB][R];
+  const int n_base = blockIdx.x * R;
+  const int ks = blockIdx.y;
+  gemv_core<MB, RW, UNROLL>(A, lda, W, ldw, M, N, K, k_split_len, n_base, ks, res);
   __syncthreads();
   // epilogue: one thread per (row m, output column)
   if (ws != nullptr && gridDim.y > 1) {             // fp32 partial slab of this K slice
