@@ -872,6 +872,228 @@ __global__ void __launch_bounds__(512) gemm8p224_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// 256x128 ping-pong GEMM: the 8-phase schedule of gemm8p224_kernel for 128-column N-tiles.
+// Where 256-column tiles leave most of the chip idle or need deep K splits: the Mixtral
+// grouped down projection (N = 4096, one 256-row tile per expert: 8 x 16 = 128 workgroups of
+// 256x256 / 152 of 256x224, here 8 x 32 = 256), and the dense N = 4096 projections at
+// M = 512 (64 tiles: split-K 4 fills 256 CUs with half the fp32 slab bytes of 32 tiles x 8).
+//
+// Waves: group g = wid >> 2 = the tile's 128-row half (one wave of each group per SIMD,
+// group 1 one barrier behind); wave (wm, wn) = (w4 >> 1, w4 & 1) of a group owns rows
+// 128 g + 64 wm .. +63 and columns 64 wn .. +63: 4 x 4 MFMA blocks.
+//   phase | reads                              | MFMAs             | DMA for T+2
+//   0     | A rows +0..31 (both kk), B +0..31  | rows 0-31, cols 0-31   | -
+//   1     | B +32..63                          | rows 0-31, cols 32-63  | A h0
+//   2     | A rows +32..63                     | rows 32-63, cols 32-63 | B
+//   3     | -                                  | rows 32-63, cols 0-31  | A h1, then a counted
+//                                                                         wait for T+1's DMAs
+// (A h0 = rows r % 64 < 32, h1 the rest; B = all 128 rows, last read in phase 1.) LDS:
+// 2 x (A 256 x 64 + B 128 x 64) bf16 = 96 KiB. SiLU pairs (2p, 2p+1) stay inside a wave.
+template <int EPI>
+__global__ void __launch_bounds__(512) gemm8p128_kernel(
+    const u16* __restrict__ A, int lda, const u16* __restrict__ W, int ldw,
+    void* __restrict__ C, int ldc, int M, int N, int K, int k_split_len,
+    const u16* __restrict__ bias, float* __restrict__ ws, const int* __restrict__ group_off) {
+  constexpr int BM = 256, BN = 128;
+  constexpr int A_BYTES = BM * BK * 2, BUF = A_BYTES + BN * BK * 2;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  int row0 = 0, Mg = M;
+  const u16* Wg = W;
+  if (group_off != nullptr) {
+    row0 = group_off[blockIdx.z];
+    Mg = group_off[blockIdx.z + 1] - row0;
+    Wg = W + (long)blockIdx.z * N * ldw;
+  }
+  const int tiles_m = (M + BM - 1) / BM;
+  const int tiles_n = (N + BN - 1) / BN;
+  int tile, ks;
+  split_tile(tiles_m * tiles_n, group_off != nullptr, tile, ks);
+  constexpr int GM = 4;                            // grouped tile order (see gemm8p_kernel)
+  const int per_group = GM * tiles_n;
+  const int first_m = (tile / per_group) * GM;
+  const int gsz = min(tiles_m - first_m, GM);
+  const int in_g = tile % per_group;
+  const int tm = first_m + in_g % gsz, tn = in_g / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+  if (m0 >= Mg) return;
+  const int kb = ks * k_split_len;
+  const int nk = min(k_split_len, K - kb) / BK;
+  const u16* Ab = A + (long)row0 * lda;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = wid >> 2, w4 = wid & 3, wm = w4 >> 1, wn = w4 & 1;
+
+  // ---- LDS-DMA pieces (8 rows x 128 B; lane L lands at row L/8, physical chunk L%8, so it
+  // loads logical chunk (L%8) ^ ((r >> 1) & 7)). 16 pieces per region, wave wid takes pieces
+  // wid and wid + 8: A h0 piece q -> rows 64 (q >> 2) + 8 (q & 3), A h1 -> the same + 32,
+  // B piece q -> rows 8 q.
+  auto piece_row = [](int region, int q) {
+    switch (region) {
+      case 0: return 64 * (q >> 2) + 8 * (q & 3);
+      case 1: return 64 * (q >> 2) + 8 * (q & 3) + 32;
+      default: return 8 * q;
+    }
+  };
+  int src[3][2], dst[3][2];                        // [region: A h0, A h1, B][piece]
+#pragma unroll
+  for (int rg = 0; rg < 3; ++rg)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int rb = piece_row(rg, wid + 8 * i);
+      const int r = rb + (lane >> 3);
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      if (rg < 2) src[rg][i] = min(m0 + r, Mg - 1) * lda + kb + c * 8;
+      else src[rg][i] = min(n0 + r, N - 1) * ldw + kb + c * 8;
+      dst[rg][i] = (rg < 2 ? 0 : A_BYTES) + rb * 128;
+    }
+  auto dma = [&](auto RG, int kt) {
+    constexpr int rg = decltype(RG)::value;
+    const u16* base = rg < 2 ? Ab : Wg;
+    char* lds = smem + (kt & 1) * BUF;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((gbl_void*)(base + src[rg][i] + kt * BK),
+                                       (lds_void*)(lds + dst[rg][i]), 16, 0, 0);
+  };
+  auto dma_all = [&](int kt) {
+    dma(std::integral_constant<int, 0>{}, kt); dma(std::integral_constant<int, 1>{}, kt);
+    dma(std::integral_constant<int, 2>{}, kt);
+  };
+
+  const int fr = lane & 15, fq = lane >> 4;
+  auto read_frag = [&](const char* part, int row, int kk) -> bf16x8 {
+    const int c = kk * 4 + fq;
+    return *reinterpret_cast<const bf16x8*>(part + row * 128 + ((c ^ ((row >> 1) & 7)) << 4));
+  };
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // ---- prologue: K-tiles 0 and 1 whole
+  if (nk > 0) dma_all(0);
+  if (nk > 1) { dma_all(1); wait_vmcnt<6>(); }
+  else wait_vmcnt<0>();
+  __syncthreads();
+  if (g == 1) {                                    // stagger: group 1 runs one segment behind
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_setprio(1);                 // static priority for the younger half
+  }
+  auto barrier = [&]() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
+  };
+  const int arow = 128 * g + 64 * wm + fr, brow = 64 * wn + fr;
+  bf16x8 a0[2][2], a1[2][2], b0[2][2], b1[2][2];
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* abuf = smem + (kt & 1) * BUF;
+    const char* bbuf = abuf + A_BYTES;
+    auto phase = [&](auto P) {
+      constexpr int p = decltype(P)::value;
+      if (p == 0) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) a0[i][kk] = read_frag(abuf, arow + 16 * i, kk);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) b0[j][kk] = read_frag(bbuf, brow + 16 * j, kk);
+      } else if (p == 1) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) b1[j][kk] = read_frag(bbuf, brow + 32 + 16 * j, kk);
+        if (kt + 2 < nk) dma(std::integral_constant<int, 0>{}, kt + 2);
+      } else if (p == 2) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) a1[i][kk] = read_frag(abuf, arow + 32 + 16 * i, kk);
+        if (kt + 2 < nk) dma(std::integral_constant<int, 2>{}, kt + 2);
+      } else {
+        if (kt + 2 < nk) { dma(std::integral_constant<int, 1>{}, kt + 2); wait_vmcnt<6>(); }
+        else wait_vmcnt<0>();
+      }
+      __builtin_amdgcn_s_waitcnt(0xC07F);          // lgkmcnt(0): this segment's reads done
+      barrier();
+      const bf16x8 (&af)[2][2] = (p < 2) ? a0 : a1;
+      const bf16x8 (&bf)[2][2] = (p == 0 || p == 3) ? b0 : b1;
+      constexpr int I0 = (p < 2) ? 0 : 2, J0 = (p == 0 || p == 3) ? 0 : 2;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[I0 + i][J0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                af[i][kk], bf[j][kk], acc[I0 + i][J0 + j], 0, 0, 0);
+      barrier();
+    };
+    phase(std::integral_constant<int, 0>{});
+    phase(std::integral_constant<int, 1>{});
+    phase(std::integral_constant<int, 2>{});
+    phase(std::integral_constant<int, 3>{});
+  }
+  if (g == 0) __builtin_amdgcn_s_barrier();       // balance group 1's stagger barrier
+
+  // ---- epilogue: acc[i][j][r] = C[m0 + 128 g + 64 wm + 16 i + 4 fq + r][n0 + 64 wn + 16 j + fr]
+  const int wr0 = m0 + 128 * g + 64 * wm, wc0 = n0 + 64 * wn;
+  if (gridDim.y > 1) {
+    float* slab = ws + (long)ks * M * N;
+    const int sm = g_slab_store;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wr0 + 16 * i + 4 * fq + r;
+        if (row >= Mg) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int col = wc0 + 16 * j + fr;
+          if (col < N) slab_store(slab + (long)(row0 + row) * N + col, acc[i][j][r], sm);
+        }
+      }
+    return;
+  }
+  if (EPI == EPI_SILU) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wr0 + 16 * i + 4 * fq + r;
+        if (row >= Mg) continue;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int gcol = wc0 + 32 * q;
+          if (gcol < N)
+            ((u16*)C)[(long)(row0 + row) * ldc + (gcol >> 5) * 16 + fr] =
+                f2bf(silu_f(acc[i][2 * q][r]) * acc[i][2 * q + 1][r]);
+        }
+      }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = wr0 + 16 * i + 4 * fq + r;
+      if (row >= Mg) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = wc0 + 16 * j + fr;
+        if (col < N) store_pair_or_one<EPI>(C, ldc, row0 + row, col, acc[i][j][r], bias);
+      }
+    }
+}
+
 // split-K reduction + epilogue: one thread per output element group of 4 columns
 template <int EPI>
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(void* __restrict__ C, int ldc,
@@ -980,6 +1202,35 @@ static int launch_8p224(const void* A, int lda, const void* W, int ldw, void* C,
   }
   dim3 grid(tiles, splits, groups);
   gemm8p224_kernel<EPI><<<grid, 512, lds, st>>>((const u16*)A, lda, (const u16*)W, ldw, C, ldc,
+                                                M, N, K, ksl, (const u16*)bias, (float*)ws,
+                                                group_off);
+  if (splits > 1 && C != nullptr) {
+    const int outN = (EPI == EPI_SILU) ? N / 2 : N;
+    const long total = (long)M * outN;
+    splitk_reduce_kernel<EPI><<<(int)((total + 255) / 256), 256, 0, st>>>(
+        C, ldc, (const float*)ws, M, N, splits, (const u16*)bias);
+  }
+  DLI_RETURN_LAUNCH();
+}
+
+template <int EPI>
+static int launch_8p128(const void* A, int lda, const void* W, int ldw, void* C, int ldc,
+                        int M, int N, int K, int splits, const void* bias, void* ws,
+                        const int* group_off, int groups, hipStream_t st) {
+  if (EPI == EPI_SILU && N % 32) return (int)hipErrorInvalidValue;
+  const int tiles = ((M + 255) / 256) * ((N + 127) / 128);
+  int ksl = K / splits;
+  ksl = (ksl / BK) * BK;
+  if (ksl * splits != K) return (int)hipErrorInvalidValue;
+  constexpr size_t lds = 2 * (size_t)(256 + 128) * BK * 2;
+  static bool attr_done = false;
+  if (!attr_done) {
+    hipFuncSetAttribute((const void*)gemm8p128_kernel<EPI>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_done = true;
+  }
+  dim3 grid(tiles, splits, groups);
+  gemm8p128_kernel<EPI><<<grid, 512, lds, st>>>((const u16*)A, lda, (const u16*)W, ldw, C, ldc,
                                                 M, N, K, ksl, (const u16*)bias, (float*)ws,
                                                 group_off);
   if (splits > 1 && C != nullptr) {
@@ -1193,6 +1444,9 @@ static int dispatch_tile(int tile_cfg, const void* A, int lda, const void* W, in
     DLI_CFG8(23, 128, 192, 3, 2, 4) DLI_CFG8(24, 128, 192, 2, 2, 4) DLI_CFG8(25, 256, 192, 2, 4, 2)
     // 256x224 ping-pong (gemm8p224_kernel): N = 28672 gate/up at M = 512 is 256 tiles
     case 26: return launch_8p224<EPI>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
+    // 256x128 ping-pong (gemm8p128_kernel): Mixtral grouped down (8 x 32 tiles), N = 4096 at
+    // M = 512 (64 tiles x split 4)
+    case 28: return launch_8p128<EPI>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
     // skinny weight-streaming GEMM for M <= 4 (no grouped mode)
     case 30: case 31: case 32:
       if (go != nullptr) return (int)hipErrorInvalidValue;

@@ -41,14 +41,17 @@ TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256), 4: (256, 128),
          # 256x224 ping-pong: N = 28672 (Llama-3 gate/up) at M = 512 = 256 tiles on 256 CUs
          26: (256, 224),
          # 22 with the round-1 schedule (a vmcnt wait every phase), for A/B runs only
-         27: (256, 256)}
+         27: (256, 256),
+         # 256x128 ping-pong: Mixtral grouped down (N = 4096: 32 column tiles per expert),
+         # N = 4096 at M = 512 with split-K 4
+         28: (256, 128)}
 # weight-streaming skinny GEMM (gemm.hip gemv_kernel) for M <= GEMV_MAX_M rows: 16 / 32 output
 # rows per workgroup (31 for the SiLU*up gate/up pairing); not an MFMA tile, so kept apart
 GEMV_TILES = {30: 16, 31: 32, 32: 16}      # 32: 4 K-steps in flight per lane, M = 1
 GEMV_MAX_M = 4
 TILE_WAVES = {13: (2, 4), 14: (4, 2), 15: (2, 4), 16: (4, 2), 17: (2, 4),
               22: (2, 4), 23: (2, 4), 24: (2, 4), 25: (4, 2),
-              26: (4, 2), 27: (2, 4)}
+              26: (4, 2), 27: (2, 4), 28: (4, 2)}
 
 
 def tile_ok(tile: int, epi: str) -> bool:

@@ -80,19 +80,22 @@ def test_gemm_bf16_all_tiles(gpu, M, N, K):
             close(out, ref, rtol=1e-2, atol=1e-2)
 
 
+@pytest.mark.parametrize("tile", [26, 28])
 @pytest.mark.parametrize("M,N,K,epi", [(512, 28672, 4096, "silu_mul"), (500, 2240, 14336, "none"),
-                                       (1000, 7168, 1024, "f32")])
-def test_gemm_256x224_pingpong(gpu, M, N, K, epi):
-    """Tile 26 (256x224 ping-pong) at the Llama-3 gate/up decode shape and with long K /
-    partial M tiles, against the fp32 reference."""
+                                       (1000, 7168, 1024, "f32"), (512, 4096, 14336, "none")])
+def test_gemm_256x224_pingpong(gpu, M, N, K, epi, tile):
+    """Tiles 26 (256x224 ping-pong) and 28 (256x128 ping-pong) at the Llama-3 gate/up and
+    down decode shapes and with long K / partial M tiles, against the fp32 reference."""
     torch.manual_seed(5)
     x, w = rnd(M, K, dev=gpu), rnd(N, K, dev=gpu, scale=0.05)
     if epi == "silu_mul":
         ref = R.silu_mul(R.linear(x, w).float().to(BF))
     else:
         ref = R.linear(x, w, out_dtype=torch.float32)
-    for splits in (1, 2):
-        out = ops._gemm_native(x, w, epi, plan=G.GemmPlan("dli", 26, splits))
+    for splits in (1, 2, 4):
+        if K % (64 * splits):
+            continue
+        out = ops._gemm_native(x, w, epi, plan=G.GemmPlan("dli", tile, splits))
         close(out, ref, rtol=2e-2, atol=2e-2)
 
 
