@@ -69,6 +69,95 @@ __device__ __forceinline__ void slab_store(float* p, float v, int mode) {
   }
 }
 
+// ---- transposed accumulators. Every MFMA kernel in this file passes the W fragment as MFMA
+// operand A and the activation fragment as operand B, i.e. it computes C^T = W . A^T. A
+// 16x16 output block then lands as: lane (fq = lane / 16, fr = lane % 16) holds
+// C[16 i + fr][16 j + 4 fq + r] for r = 0..3 — four CONSECUTIVE columns of one row — so an
+// epilogue writes one 16-B (fp32 slab / logits) or 8-B (bf16) vector per block instead of
+// four 4-B / 2-B scalars. The epilogue store tail of a short-K split GEMM is issue-bound
+// (cdna_hip_programming.md T21: halving the store instructions at equal bytes halved it);
+// the fragments read from LDS, the MFMA count and the slab layout are unchanged.
+__device__ __forceinline__ void slab_store4(float* p, f32x4 v, int mode) {
+  if (mode == 1) {
+    __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
+  } else if (mode == 2) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+  } else if (mode == 3) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+  } else {
+    *reinterpret_cast<f32x4*>(p) = v;
+  }
+}
+
+// one split-K partial quad: p = &slab[row][col]; vec = (N % 4 == 0), so col + 3 < N
+__device__ __forceinline__ void slab_quad(float* p, f32x4 v, int mode, bool vec, int left) {
+  if (vec) {
+    slab_store4(p, v, mode);
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (r < left) slab_store(p + r, v[r], mode);
+  }
+}
+
+// four consecutive output columns [col, col + 4) of one row; vec = (N % 4 == 0 && ldc % 4
+// == 0): one 16-B (fp32) / 8-B (bf16) store, else per-column stores for the row's tail
+template <int EPI>
+__device__ __forceinline__ void store_quad(void* C, int ldc, int row, int col, int N, f32x4 v,
+                                           const u16* bias, bool vec) {
+  if (!vec) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (col + r < N) store_pair_or_one<EPI>(C, ldc, row, col + r, v[r], bias);
+    return;
+  }
+  if (EPI == EPI_F32) {
+    *reinterpret_cast<f32x4*>((float*)C + (long)row * ldc + col) = v;
+    return;
+  }
+  float o[4] = {v[0], v[1], v[2], v[3]};
+  if (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
+    const uint2 b = *reinterpret_cast<const uint2*>(bias + col);
+    o[0] += __uint_as_float(b.x << 16); o[1] += __uint_as_float(b.x & 0xffff0000u);
+    o[2] += __uint_as_float(b.y << 16); o[3] += __uint_as_float(b.y & 0xffff0000u);
+  }
+  if (EPI == EPI_BIAS_GELU) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] = gelu_f(o[r]);
+  }
+  uint2 pk;
+  pk.x = pack2bf(o[0], o[1]);
+  pk.y = pack2bf(o[2], o[3]);
+  *reinterpret_cast<uint2*>((u16*)C + (long)row * ldc + col) = pk;
+}
+
+// the vector epilogue needs every row start and column quad aligned: N and ldc multiples
+// of 4, C (and the bias) 16-B (fp32) / 8-B (bf16) aligned (C may be a column view)
+template <int EPI>
+__device__ __forceinline__ bool out_vec(const void* C, int ldc, int N, const u16* bias) {
+  const uintptr_t mis = ((uintptr_t)C | (uintptr_t)bias) & (EPI == EPI_F32 ? 15 : 7);
+  return ((N | ldc) & 3) == 0 && mis == 0;
+}
+
+// SiLU(gate) * up of one gate block g and its up block u (same lane, same row): the four
+// features [f, f + 4) of the 16-row-interleaved gate/up layout
+__device__ __forceinline__ void store_silu_quad(void* C, int ldc, int row, int f, f32x4 g,
+                                                f32x4 u, bool vec) {
+  float o[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) o[r] = silu_f(g[r]) * u[r];
+  u16* p = (u16*)C + (long)row * ldc + f;
+  if (vec) {
+    uint2 pk;
+    pk.x = pack2bf(o[0], o[1]);
+    pk.y = pack2bf(o[2], o[3]);
+    *reinterpret_cast<uint2*>(p) = pk;
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) p[r] = f2bf(o[r]);
+  }
+}
+
 // s_waitcnt vmcnt(N) with expcnt/lgkmcnt left at their maxima (gfx9 encoding)
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -197,7 +286,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NI; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
   };
 
@@ -234,57 +323,53 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(
     wait_vmcnt<0>();
   }
 
-  // ---- epilogue. acc[i][j][r] = C[m0 + wm*BM/2 + 16i + 4fq + r][n0 + wn*BN/2 + 16j + fr]
+  // ---- epilogue (transposed accumulators):
+  // acc[i][j][r] = C[m0 + wm*TM + 16i + fr][n0 + wn*TN + 16j + 4fq + r]
   const bool split = gridDim.y > 1;
   if (split) {
     float* slab = ws + (long)ks * M * N;
     const int sm = g_slab_store;
+    const bool vec = (N & 3) == 0;
 #pragma unroll
-    for (int i = 0; i < MI; ++i)
+    for (int i = 0; i < MI; ++i) {
+      const int row = m0 + wm * TM + 16 * i + fr;
+      if (row >= Mg) continue;
+      float* srow = slab + (long)(row0 + row) * N;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * TM + 16 * i + 4 * fq + r;
-        if (row >= Mg) continue;
-#pragma unroll
-        for (int j = 0; j < NI; ++j) {
-          const int col = n0 + wn * TN + 16 * j + fr;
-          if (col < N) slab_store(slab + (long)(row0 + row) * N + col, acc[i][j][r], sm);
-        }
+      for (int j = 0; j < NI; ++j) {
+        const int col = n0 + wn * TN + 16 * j + 4 * fq;
+        if (col < N) slab_quad(srow + col, acc[i][j], sm, vec, N - col);
       }
+    }
     return;
   }
+  const bool vec = out_vec<EPI>(C, ldc, N, bias);
   if (EPI == EPI_SILU) {
     // column blocks j (even) = gate, j+1 = up of the same 16 features
 #pragma unroll
-    for (int i = 0; i < MI; ++i)
+    for (int i = 0; i < MI; ++i) {
+      const int row = m0 + wm * TM + 16 * i + fr;
+      if (row >= Mg) continue;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * TM + 16 * i + 4 * fq + r;
-        if (row >= Mg) continue;
-#pragma unroll
-        for (int j = 0; j < NI; j += 2) {
-          const int gcol = n0 + wn * TN + 16 * j;       // first gate row of the pair
-          if (gcol < N) {
-            const int f = (gcol >> 5) * 16 + fr;
-            const float v = silu_f(acc[i][j][r]) * acc[i][j + 1][r];
-            ((u16*)C)[(long)(row0 + row) * ldc + f] = f2bf(v);
-          }
-        }
+      for (int j = 0; j < NI; j += 2) {
+        const int gcol = n0 + wn * TN + 16 * j;         // first gate row of the pair
+        if (gcol < N)
+          store_silu_quad(C, ldc, row0 + row, (gcol >> 5) * 16 + 4 * fq, acc[i][j],
+                          acc[i][j + 1], vec);
       }
+    }
     return;
   }
 #pragma unroll
-  for (int i = 0; i < MI; ++i)
+  for (int i = 0; i < MI; ++i) {
+    const int row = m0 + wm * TM + 16 * i + fr;
+    if (row >= Mg) continue;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = m0 + wm * TM + 16 * i + 4 * fq + r;
-      if (row >= Mg) continue;
-#pragma unroll
-      for (int j = 0; j < NI; ++j) {
-        const int col = n0 + wn * TN + 16 * j + fr;
-        if (col < N) store_pair_or_one<EPI>(C, ldc, row0 + row, col, acc[i][j][r], bias);
-      }
+    for (int j = 0; j < NI; ++j) {
+      const int col = n0 + wn * TN + 16 * j + 4 * fq;
+      if (col < N) store_quad<EPI>(C, ldc, row0 + row, col, N, acc[i][j], bias, vec);
     }
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -542,7 +627,7 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(
 #pragma unroll
           for (int j = 0; j < 2; ++j)
             acc[I0 + i][J0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                af[i][kk], bf[j][kk], acc[I0 + i][J0 + j], 0, 0, 0);
+                bf[j][kk], af[i][kk], acc[I0 + i][J0 + j], 0, 0, 0);
       if (!(VAR & 256)) __builtin_amdgcn_s_setprio(0);
       barrier();
     };
@@ -555,56 +640,52 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(
     __builtin_amdgcn_s_barrier();
   }
 
-  // ---- epilogue: acc[I][J][r] = C[m0 + 128g + 16I + 4fq + r][n0 + 64gw + 16J + fr]
+  // ---- epilogue (transposed accumulators):
+  // acc[I][J][r] = C[m0 + 128g + 16I + fr][n0 + 64gw + 16J + 4fq + r]
   const int wr0 = m0 + 128 * g, wc0 = n0 + 64 * gw;
   if (gridDim.y > 1) {
     float* slab = ws + (long)ks * M * N;
     const int sm = g_slab_store;
+    const bool vec = (N & 3) == 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = wr0 + 16 * i + 4 * fq + r;
-        if (row >= Mg) continue;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int col = wc0 + 16 * j + fr;
-          if (col < N) slab_store(slab + (long)(row0 + row) * N + col, acc[i][j][r], sm);
-        }
-      }
-    return;
-  }
-  if (EPI == EPI_SILU) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = wr0 + 16 * i + 4 * fq + r;
-        if (row >= Mg) continue;
-#pragma unroll
-        for (int j = 0; j < 4; j += 2) {
-          const int gcol = wc0 + 16 * j;
-          if (gcol < N) {
-            const int f = (gcol >> 5) * 16 + fr;
-            const float v = silu_f(acc[i][j][r]) * acc[i][j + 1][r];
-            ((u16*)C)[(long)(row0 + row) * ldc + f] = f2bf(v);
-          }
-        }
-      }
-    return;
-  }
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = wr0 + 16 * i + 4 * fq + r;
+    for (int i = 0; i < 8; ++i) {
+      const int row = wr0 + 16 * i + fr;
       if (row >= Mg) continue;
+      float* srow = slab + (long)(row0 + row) * N;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int col = wc0 + 16 * j + fr;
-        if (col < N) store_pair_or_one<EPI>(C, ldc, row0 + row, col, acc[i][j][r], bias);
+        const int col = wc0 + 16 * j + 4 * fq;
+        if (col < N) slab_quad(srow + col, acc[i][j], sm, vec, N - col);
       }
     }
+    return;
+  }
+  const bool vec = out_vec<EPI>(C, ldc, N, bias);
+  if (EPI == EPI_SILU) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = wr0 + 16 * i + fr;
+      if (row >= Mg) continue;
+#pragma unroll
+      for (int j = 0; j < 4; j += 2) {
+        const int gcol = wc0 + 16 * j;
+        if (gcol < N)
+          store_silu_quad(C, ldc, row0 + row, (gcol >> 5) * 16 + 4 * fq, acc[i][j],
+                          acc[i][j + 1], vec);
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = wr0 + 16 * i + fr;
+    if (row >= Mg) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = wc0 + 16 * j + 4 * fq;
+      if (col < N) store_quad<EPI>(C, ldc, row0 + row, col, N, acc[i][j], bias, vec);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -777,12 +858,12 @@ __global__ void __launch_bounds__(512) gemm8p224_kernel(
 #pragma unroll
             for (int j = 0; j < 4; ++j)
               acc[I0 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                  af[i][kk], b0[j][kk], acc[I0 + i][j], 0, 0, 0);
+                  b0[j][kk], af[i][kk], acc[I0 + i][j], 0, 0, 0);
           } else {
 #pragma unroll
             for (int j = 0; j < 3; ++j)
               acc[I0 + i][4 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                  af[i][kk], b1[j][kk], acc[I0 + i][4 + j], 0, 0, 0);
+                  b1[j][kk], af[i][kk], acc[I0 + i][4 + j], 0, 0, 0);
           }
         }
       barrier();
@@ -794,25 +875,27 @@ __global__ void __launch_bounds__(512) gemm8p224_kernel(
   }
   if (g == 0) __builtin_amdgcn_s_barrier();       // balance group 1's stagger barrier
 
-  // ---- epilogue: acc[i][j][r] = C[m0 + 128 g + 64 wm + 16 i + 4 fq + r][n0 + 112 wn + 16 j + fr]
+  // ---- epilogue (transposed accumulators):
+  // acc[i][j][r] = C[m0 + 128 g + 64 wm + 16 i + fr][n0 + 112 wn + 16 j + 4 fq + r]
   const int wr0 = m0 + 128 * g + 64 * wm, wc0 = n0 + 112 * wn;
   if (gridDim.y > 1) {
     float* slab = ws + (long)ks * M * N;
     const int sm = g_slab_store;
+    const bool vec = (N & 3) == 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i) {
+      const int row = wr0 + 16 * i + fr;
+      if (row >= Mg) continue;
+      float* srow = slab + (long)(row0 + row) * N;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = wr0 + 16 * i + 4 * fq + r;
-        if (row >= Mg) continue;
-#pragma unroll
-        for (int j = 0; j < 7; ++j) {
-          const int col = wc0 + 16 * j + fr;
-          if (col < N) slab_store(slab + (long)(row0 + row) * N + col, acc[i][j][r], sm);
-        }
+      for (int j = 0; j < 7; ++j) {
+        const int col = wc0 + 16 * j + 4 * fq;
+        if (col < N) slab_quad(srow + col, acc[i][j], sm, vec, N - col);
       }
+    }
     return;
   }
+  const bool vec = out_vec<EPI>(C, ldc, N, bias);
   if (EPI == EPI_SILU) {
     // block 6 of wave wn = 0 (gate) pairs with block 0 of wave wn = 1 (up): through LDS
     __syncthreads();                               // every wave is past its last LDS read
@@ -820,56 +903,50 @@ __global__ void __launch_bounds__(512) gemm8p224_kernel(
     if (wn == 1) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) xch[(16 * i + 4 * fq + r) * 16 + fr] = acc[i][0][r];
+        *reinterpret_cast<f32x4*>(xch + (16 * i + fr) * 16 + 4 * fq) = acc[i][0];
     }
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i) {
+      const int row = wr0 + 16 * i + fr;
+      if (row >= Mg) continue;
+      // own pairs: wave 0 blocks (0,1) (2,3) (4,5) + (6, partner's 0); wave 1 (1,2) (3,4)
+      // (5,6) (compile-time block indices in each branch: no runtime-indexed registers)
+      if (wn == 0) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = wr0 + 16 * i + 4 * fq + r;
-        if (row >= Mg) continue;
-        u16* crow = (u16*)C + (long)(row0 + row) * ldc;
-        // own pairs: wave 0 blocks (0,1) (2,3) (4,5) + (6, partner's 0); wave 1 (1,2) (3,4)
-        // (5,6) (compile-time block indices in each branch: no runtime-indexed registers)
-        if (wn == 0) {
+        for (int q = 0; q < 3; ++q) {
+          const int gcol = wc0 + 32 * q;
+          if (gcol < N)
+            store_silu_quad(C, ldc, row0 + row, (gcol >> 5) * 16 + 4 * fq, acc[i][2 * q],
+                            acc[i][2 * q + 1], vec);
+        }
+        const int gcol = wc0 + 16 * 6;
+        if (gcol < N) {
+          const f32x4 up = *reinterpret_cast<const f32x4*>(xch + (16 * i + fr) * 16 + 4 * fq);
+          store_silu_quad(C, ldc, row0 + row, (gcol >> 5) * 16 + 4 * fq, acc[i][6], up, vec);
+        }
+      } else {
 #pragma unroll
-          for (int q = 0; q < 3; ++q) {
-            const int gcol = wc0 + 32 * q;
-            if (gcol < N)
-              crow[(gcol >> 5) * 16 + fr] =
-                  f2bf(silu_f(acc[i][2 * q][r]) * acc[i][2 * q + 1][r]);
-          }
-          const int gcol = wc0 + 16 * 6;
-          if (gcol < N) {
-            const float up = xch[(16 * i + 4 * fq + r) * 16 + fr];
-            crow[(gcol >> 5) * 16 + fr] = f2bf(silu_f(acc[i][6][r]) * up);
-          }
-        } else {
-#pragma unroll
-          for (int q = 0; q < 3; ++q) {
-            const int gcol = wc0 + 16 + 32 * q;
-            if (gcol < N)
-              crow[(gcol >> 5) * 16 + fr] =
-                  f2bf(silu_f(acc[i][2 * q + 1][r]) * acc[i][2 * q + 2][r]);
-          }
+        for (int q = 0; q < 3; ++q) {
+          const int gcol = wc0 + 16 + 32 * q;
+          if (gcol < N)
+            store_silu_quad(C, ldc, row0 + row, (gcol >> 5) * 16 + 4 * fq, acc[i][2 * q + 1],
+                            acc[i][2 * q + 2], vec);
         }
       }
+    }
     return;
   }
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 4; ++i) {
+    const int row = wr0 + 16 * i + fr;
+    if (row >= Mg) continue;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = wr0 + 16 * i + 4 * fq + r;
-      if (row >= Mg) continue;
-#pragma unroll
-      for (int j = 0; j < 7; ++j) {
-        const int col = wc0 + 16 * j + fr;
-        if (col < N) store_pair_or_one<EPI>(C, ldc, row0 + row, col, acc[i][j][r], bias);
-      }
+    for (int j = 0; j < 7; ++j) {
+      const int col = wc0 + 16 * j + 4 * fq;
+      if (col < N) store_quad<EPI>(C, ldc, row0 + row, col, N, acc[i][j], bias, vec);
     }
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1034,7 +1111,7 @@ __global__ void __launch_bounds__(512) gemm8p128_kernel(
 #pragma unroll
           for (int j = 0; j < 2; ++j)
             acc[I0 + i][J0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                af[i][kk], bf[j][kk], acc[I0 + i][J0 + j], 0, 0, 0);
+                bf[j][kk], af[i][kk], acc[I0 + i][J0 + j], 0, 0, 0);
       barrier();
     };
     phase(std::integral_constant<int, 0>{});
@@ -1044,54 +1121,52 @@ __global__ void __launch_bounds__(512) gemm8p128_kernel(
   }
   if (g == 0) __builtin_amdgcn_s_barrier();       // balance group 1's stagger barrier
 
-  // ---- epilogue: acc[i][j][r] = C[m0 + 128 g + 64 wm + 16 i + 4 fq + r][n0 + 64 wn + 16 j + fr]
+  // ---- epilogue (transposed accumulators):
+  // acc[i][j][r] = C[m0 + 128 g + 64 wm + 16 i + fr][n0 + 64 wn + 16 j + 4 fq + r]
   const int wr0 = m0 + 128 * g + 64 * wm, wc0 = n0 + 64 * wn;
   if (gridDim.y > 1) {
     float* slab = ws + (long)ks * M * N;
     const int sm = g_slab_store;
+    const bool vec = (N & 3) == 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = wr0 + 16 * i + 4 * fq + r;
-        if (row >= Mg) continue;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int col = wc0 + 16 * j + fr;
-          if (col < N) slab_store(slab + (long)(row0 + row) * N + col, acc[i][j][r], sm);
-        }
-      }
-    return;
-  }
-  if (EPI == EPI_SILU) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = wr0 + 16 * i + 4 * fq + r;
-        if (row >= Mg) continue;
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const int gcol = wc0 + 32 * q;
-          if (gcol < N)
-            ((u16*)C)[(long)(row0 + row) * ldc + (gcol >> 5) * 16 + fr] =
-                f2bf(silu_f(acc[i][2 * q][r]) * acc[i][2 * q + 1][r]);
-        }
-      }
-    return;
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = wr0 + 16 * i + 4 * fq + r;
+    for (int i = 0; i < 4; ++i) {
+      const int row = wr0 + 16 * i + fr;
       if (row >= Mg) continue;
+      float* srow = slab + (long)(row0 + row) * N;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int col = wc0 + 16 * j + fr;
-        if (col < N) store_pair_or_one<EPI>(C, ldc, row0 + row, col, acc[i][j][r], bias);
+        const int col = wc0 + 16 * j + 4 * fq;
+        if (col < N) slab_quad(srow + col, acc[i][j], sm, vec, N - col);
       }
     }
+    return;
+  }
+  const bool vec = out_vec<EPI>(C, ldc, N, bias);
+  if (EPI == EPI_SILU) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = wr0 + 16 * i + fr;
+      if (row >= Mg) continue;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int gcol = wc0 + 32 * q;
+        if (gcol < N)
+          store_silu_quad(C, ldc, row0 + row, (gcol >> 5) * 16 + 4 * fq, acc[i][2 * q],
+                          acc[i][2 * q + 1], vec);
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = wr0 + 16 * i + fr;
+    if (row >= Mg) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = wc0 + 16 * j + 4 * fq;
+      if (col < N) store_quad<EPI>(C, ldc, row0 + row, col, N, acc[i][j], bias, vec);
+    }
+  }
 }
 
 // split-K reduction + epilogue: one thread per output element group of 4 columns

@@ -148,6 +148,37 @@ def test_gemm_asymmetric_identity(gpu):
         assert torch.equal(out, w.t().contiguous()), tile
 
 
+@pytest.mark.parametrize("epi", ["none", "f32", "silu_mul", "bias"])
+@pytest.mark.parametrize("col0", [3, 4])
+def test_gemm_strided_output_views(gpu, epi, col0):
+    """The epilogues write four consecutive columns per lane (transposed accumulators) as one
+    16-B / 8-B store when C, ldc and N allow it: a column view of a wider buffer at an aligned
+    offset (col0 = 4: vector stores with ldc != N) and at a misaligned one (col0 = 3: the
+    per-column fallback) must both match the fp32 reference and leave the rest untouched."""
+    torch.manual_seed(13)
+    M, N, K = 300, 1024, 512
+    x, w, b = rnd(M, K, dev=gpu), rnd(N, K, dev=gpu, scale=0.05), rnd(N, dev=gpu)
+    if epi == "silu_mul":
+        ref = R.silu_mul(R.linear(x, w).float().to(BF))
+    elif epi == "bias":
+        ref = R.linear(x, w, b)
+    else:
+        ref = R.linear(x, w, out_dtype=torch.float32)
+    out_n = ref.shape[1]
+    dt = torch.float32 if epi == "f32" else BF
+    for tile in (2, 7, 13, 22, 26, 28):
+        if not G.tile_ok(tile, epi):
+            continue
+        for splits in (1, 2):
+            big = torch.full((M, out_n + 8), -7.0, dtype=dt, device=gpu)
+            view = big[:, col0:col0 + out_n]
+            ops._gemm_native(x, w, epi, bias=b if epi == "bias" else None, out=view,
+                             plan=G.GemmPlan("dli", tile, splits))
+            close(view, ref, rtol=2e-2, atol=2e-2)
+            assert bool((big[:, :col0] == -7.0).all()), (tile, splits)
+            assert bool((big[:, col0 + out_n:] == -7.0).all()), (tile, splits)
+
+
 @pytest.mark.parametrize("epi", ["f32", "silu_mul", "bias_gelu", "bias"])
 @pytest.mark.parametrize("M,N,K", [(5, 512, 256), (128, 1024, 512), (260, 3072, 768)])
 def test_gemm_epilogues(gpu, epi, M, N, K):
