@@ -165,6 +165,18 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
+// s_waitcnt vmcnt(INSTR * ahead) for a wave-uniform ahead in [0, MAXA]: retire everything
+// but the `ahead` youngest tiles of INSTR LDS-DMA instructions each
+template <int INSTR, int MAXA>
+__device__ __forceinline__ void wait_ahead(int ahead) {
+  static_assert(MAXA <= 4 && INSTR * MAXA < 64, "vmcnt range");
+  if constexpr (MAXA >= 4) { if (ahead >= 4) { wait_vmcnt<INSTR * 4>(); return; } }
+  if constexpr (MAXA >= 3) { if (ahead == 3) { wait_vmcnt<INSTR * 3>(); return; } }
+  if constexpr (MAXA >= 2) { if (ahead == 2) { wait_vmcnt<INSTR * 2>(); return; } }
+  if constexpr (MAXA >= 1) { if (ahead == 1) { wait_vmcnt<INSTR>(); return; } }
+  wait_vmcnt<0>();
+}
+
 // Block -> (output tile, K split). Without split-K: the XCD remap over tiles (n-major order,
 // so an XCD's tiles share W panels). With split-K, (split, tile) is one split-major index
 // remapped over the whole grid, so an XCD's blocks work on ONE K slice: its L2 fetches that
@@ -303,22 +315,30 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(
       __syncthreads();
     }
   } else {
-    // 3 LDS buffers, one tile kept in flight ACROSS the barrier (cdna_hip_programming.md §5
-    // 'Pipelining across barriers'): counted vmcnt retires tile kt only, then a raw
-    // s_barrier (a __syncthreads() would emit vmcnt(0) and drain the DMA); the restaged
-    // buffer (kt+2)%3 was last read in iteration kt-1, which every wave has finished.
+    // NS >= 3 LDS buffers, NS - 2 tiles kept in flight ACROSS the barrier
+    // (cdna_hip_programming.md §5 'Pipelining across barriers'): a counted vmcnt retires
+    // tile kt only (the tiles issued after it stay in flight), then a raw s_barrier (a
+    // __syncthreads() would emit vmcnt(0) and drain the DMA); the restaged buffer
+    // (kt + NS - 1) % NS was last read in iteration kt - 1, which every wave has finished.
+    // Deeper rings (NS 4-6 on the 128x64 / 128x96 / 128x128 / 128x192 decode tiles) were
+    // measured and not kept: equal or slower at M = 512 (profiles/r3/deep_ring/).
     constexpr int INSTR = A_INSTR + W_INSTR;
-    if (nk > 0) stage(0, 0);
-    if (nk > 1) stage(1, 1);
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s)
+      if (s < nk) stage(s, s);
     int cur = 0;
     for (int kt = 0; kt < nk; ++kt) {
-      if (kt + 1 < nk) wait_vmcnt<INSTR>();
-      else wait_vmcnt<0>();
+      const int ahead = min(nk - 1 - kt, NS - 2);     // tiles issued after kt (uniform)
+      wait_ahead<INSTR, NS - 2>(ahead);
       __builtin_amdgcn_s_waitcnt(0xC07F);          // lgkmcnt(0)
       __builtin_amdgcn_s_barrier();
-      if (kt + 2 < nk) stage(cur == 0 ? 2 : cur - 1, kt + 2);
+      if (kt + NS - 1 < nk) {
+        int nb = cur + NS - 1;
+        if (nb >= NS) nb -= NS;
+        stage(nb, kt + NS - 1);
+      }
       compute(cur);
-      cur = (cur == 2) ? 0 : cur + 1;
+      cur = (cur + 1 == NS) ? 0 : cur + 1;
     }
     wait_vmcnt<0>();
   }

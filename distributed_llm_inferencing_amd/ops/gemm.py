@@ -340,8 +340,18 @@ def candidate_plans(M: int, N: int, K: int, epi: str):
     # autotune (98.8 vs ~106 us), but in the decode step it ran 97.9 vs 99.0 us per call and
     # the bench 0.3-0.7 % lower in three same-box A/B runs (profiles/r2_s2/README.md)
     # 27 is tile 22 with the round-1 wait schedule (A/B reference only)
-    excl = {int(t) for t in os.environ.get("DLI_GEMM_EXCLUDE", "26,27").split(",")
+    excl_env = os.environ.get("DLI_GEMM_EXCLUDE")
+    excl = {int(t) for t in (excl_env if excl_env is not None else "26,27").split(",")
             if t.strip()}
+    # ... except where 256x256 tiles take more than one wave of the chip and 256x224 tiles
+    # land on a whole number of waves (Llama-3-70B gate/up at M = 512: N = 57344 is 448
+    # 256x256 tiles = 1.75 waves, 512 256x224 tiles = 2 waves); an explicit
+    # DLI_GEMM_EXCLUDE keeps the list as given
+    if excl_env is None and 26 in excl:
+        t256 = -(-M // 256) * -(-N // 256)
+        t224 = -(-M // 256) * -(-N // 224)
+        if t256 > NUM_CUS and t224 % NUM_CUS == 0:
+            excl.discard(26)
     for tile, (bm, bn) in TILES.items():
         if not tile_ok(tile, epi) or tile in excl:
             continue
