@@ -239,6 +239,32 @@ class AsyncDispatcher(Dispatcher):
         t.start()
         self._threads.append(t)
 
+    def start_on_loop(self, loop) -> None:
+        """Run the dispatch loop as a task on ``loop`` (the ASGI server's own event loop)
+        instead of a thread of its own: the submit handler, the long polls and the worker
+        calls then share one thread, so a request never crosses threads on its hot path
+        (no self-pipe wake-ups, no GIL hand-offs; the inline store's lock is uncontended)."""
+        if getattr(self, "_task", None) is not None or self._threads:
+            return
+        import asyncio
+        self._loop = loop
+        self._wake = asyncio.Event()
+        self._task = loop.create_task(self._main())
+
+    def submit(self, request_id: int):
+        self.queue.put(request_id)
+        wake = getattr(self, "_wake", None)
+        if wake is not None:                 # on-loop mode: wake the dispatch loop now
+            import asyncio
+            try:
+                here = asyncio.get_running_loop()
+            except RuntimeError:
+                here = None
+            if here is self._loop:
+                wake.set()
+            else:
+                self._loop.call_soon_threadsafe(wake.set)
+
     def stop(self, timeout: float = 5.0):
         self._stop.set()
         for t in self._threads:
@@ -272,7 +298,25 @@ class AsyncDispatcher(Dispatcher):
                 while free < 256 and not sem.locked():     # claim every free slot (burst)
                     await sem.acquire()
                     free += 1
-                rids = await loop.run_in_executor(getter, self.queue.get_many, free, 0.2)
+                wake = getattr(self, "_wake", None)
+                if wake is not None and getattr(self.queue, "name", "") == "inproc":
+                    # on the server's loop: take what is queued without a thread hop; when
+                    # nothing is, sleep until a submit wakes us (or 0.2 s, for producers in
+                    # other processes: the sqlite / redis queues)
+                    rids = self.queue.get_many(free, 0.0)
+                    if not rids:
+                        wake.clear()
+                        rids = self.queue.get_many(free, 0.0)   # a submit raced the clear
+                    if not rids:
+                        for _ in range(free):
+                            sem.release()
+                        try:
+                            await asyncio.wait_for(wake.wait(), 0.2)
+                        except asyncio.TimeoutError:
+                            pass
+                        continue
+                else:
+                    rids = await loop.run_in_executor(getter, self.queue.get_many, free, 0.2)
                 for _ in range(free - len(rids)):
                     sem.release()
                 for rid in rids:
@@ -291,6 +335,8 @@ class AsyncDispatcher(Dispatcher):
         """A store call, awaited without blocking the event loop: run on the store's database
         thread itself when the store offers it (no thread hop), else on a small pool."""
         import asyncio
+        if getattr(self.store, "inline", False):
+            return fn(*args)                     # the caller's thread runs the statement
         submit = getattr(self.store, "submit", None)
         if submit is not None:
             return await asyncio.wrap_future(submit(lambda _c: fn(*args)))
@@ -307,10 +353,14 @@ class AsyncDispatcher(Dispatcher):
 
     async def process_async(self, rid: int) -> None:
         try:
-            req = await self._s(self.store.get_request, rid)
+            fields = getattr(self.store, "request_fields", None)
+            if fields is not None:
+                model, prompt = await self._s(fields, rid)
+            else:
+                req = await self._s(self.store.get_request, rid)
+                model, prompt = req["model_name"], req["prompt"]
         except KeyError:
             return
-        model, prompt = req["model_name"], req["prompt"]
         try:
             nodes, shard_map = await self._s(self._candidates, model)
             if not nodes:

@@ -58,7 +58,11 @@ class MasterState:
         if recovered:
             log.warning("re-queued %d requests orphaned in 'processing'", len(recovered))
         if start_background:
-            self.dispatcher.start()
+            # an ASGI front (serve-master --server uvicorn / aiohttp) runs the async
+            # dispatcher on its own event loop (control/asgi.py starts it there)
+            if not (os.environ.get("DLI_DISPATCH_ON_SERVER_LOOP", "0") == "1"
+                    and hasattr(self.dispatcher, "start_on_loop")):
+                self.dispatcher.start()
             self.health.start()
 
     def shutdown(self):
@@ -334,11 +338,21 @@ def main(argv=None):
     ap = argparse.ArgumentParser("dli serve-master")
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--port", type=int, default=8000)
-    ap.add_argument("--server", default="werkzeug", choices=["werkzeug", "uvicorn"],
+    ap.add_argument("--server", default="werkzeug", choices=["werkzeug", "uvicorn", "aiohttp"],
                     help="werkzeug: threaded WSGI server (a thread per connection); uvicorn: "
-                         "ASGI front (control/asgi.py: async status long polls) over the "
-                         "same Flask app")
+                         "ASGI front (control/asgi.py: async submit and status long polls) "
+                         "over the same Flask app; aiohttp: the same ASGI front on aiohttp's "
+                         "C HTTP parser (utils/aioserve.py)")
     a = ap.parse_args(argv)
+    if a.server in ("aiohttp", "uvicorn"):
+        os.environ.setdefault("DLI_DISPATCH_ON_SERVER_LOOP", "1")
+    if a.server == "aiohttp":
+        from .asgi import create_asgi_app
+        from ..utils.aioserve import run_asgi
+        from ..utils.log import setup_logging
+        setup_logging("master")
+        run_asgi(create_asgi_app(create_master_app()), host=a.host, port=a.port)
+        return
     if a.server == "uvicorn":
         # ASGI front: status long polls as coroutines, the Flask app behind a WSGI adapter
         import uvicorn

@@ -20,6 +20,7 @@ and ``recover()`` which re-queues requests orphaned in ``processing`` by a resta
 from __future__ import annotations
 
 import json
+import os
 import queue
 import sqlite3
 import threading
@@ -95,15 +96,25 @@ class _Exec:
 
 
 class Store:
-    """The connection is owned by ONE database thread; every other thread hands it a call
-    and sleeps until it is done. The thread runs the calls queued meanwhile in one
-    transaction (one commit per batch). With hundreds of dispatcher and HTTP threads a
-    shared lock around the connection convoyed on the GIL (the holder re-acquires it after
-    each sqlite call): the master topped out at ~140 requests/s; the single owner has no
-    lock to contend for and batches the commits."""
+    """Two access modes (``inline``, below). Inline (default): the caller runs its call
+    under one re-entrant lock; with the threaded WSGI server's hundreds of threads that lock
+    convoyed on the GIL (~140 requests/s), but the ASGI fronts run the hot path on ONE event
+    loop (plus the async dispatcher's), so the lock is almost never contended. Threaded
+    (``DLI_STORE_INLINE=0``): ONE database thread owns the connection; every other thread
+    hands it a call and sleeps until it is done, and the thread runs the calls queued
+    meanwhile in one transaction (one commit per batch) — the better mode for the
+    thread-per-request werkzeug server."""
 
-    def __init__(self, path: str = ":memory:"):
+    def __init__(self, path: str = ":memory:", inline: Optional[bool] = None):
         self.path = path
+        # inline mode (DLI_STORE_INLINE=1, default): calls run on the CALLER's thread under one
+        # re-entrant lock, one commit per outermost call. The asyncio hot path (ASGI submit,
+        # async dispatcher) then never hands a statement to another thread: with the
+        # database thread, every sqlite3 call released the GIL and waited for it to come back
+        # from the busy event loop (~0.5 ms wall per statement, cProfile of the master at
+        # ~400 requests/s, scripts/bench_control_plane.py), which serialised the dispatcher.
+        self.inline = (os.environ.get("DLI_STORE_INLINE", "1") == "1"
+                       if inline is None else bool(inline))
         self._waiters: Dict[int, threading.Event] = {}   # long polls, by request id
         self._awaiters: Dict[int, list] = {}             # asyncio long polls: [(loop, fut)]
         self._wlock = threading.Lock()
@@ -111,17 +122,28 @@ class Store:
         # the copy cannot go stale even when other processes share the database): status
         # reads of finished requests skip the database
         self._final_rows: Dict[int, Dict[str, Any]] = {}
+        # rows of requests THIS process created and has not seen finish: the dispatcher
+        # reads their (immutable) model / prompt and a long poll its first answer from here
+        # instead of a SELECT each (other processes sharing the database are still seen:
+        # a long poll re-reads the row every 2 s)
+        self._live_rows: Dict[int, Dict[str, Any]] = {}
+        self._returning = sqlite3.sqlite_version_info >= (3, 35, 0)
         self.topology_version = 0
         self._q: "queue.SimpleQueue[_Call]" = queue.SimpleQueue()
         self._conn_obj: Optional[sqlite3.Connection] = None
-        ready = threading.Event()
-        self._t = threading.Thread(target=self._run, args=(ready,), name="dli-store", daemon=True)
-        self._t.start()
-        ready.wait()
+        if self.inline:
+            self._ilock = threading.RLock()
+            self._depth = 0
+            self._conn_obj = self._connect()
+        else:
+            ready = threading.Event()
+            self._t = threading.Thread(target=self._run, args=(ready,), name="dli-store",
+                                       daemon=True)
+            self._t.start()
+            ready.wait()
         self._call(lambda c: c.executescript(_SCHEMA))
 
-    # ------------------------------------------------------------------ the db thread
-    def _run(self, ready: threading.Event):
+    def _connect(self) -> sqlite3.Connection:
         # File databases run in WAL mode with synchronous=NORMAL (a commit appends to the
         # WAL without an fsync); other processes (a second master worker, the sqlite queue)
         # share the file safely.
@@ -131,6 +153,11 @@ class Store:
         if self.path != ":memory:":
             c.execute("PRAGMA journal_mode = WAL")
             c.execute("PRAGMA synchronous = NORMAL")
+        return c
+
+    # ------------------------------------------------------------------ the db thread
+    def _run(self, ready: threading.Event):
+        c = self._connect()
         self._conn_obj = c
         self._tid = threading.get_ident()
         ready.set()
@@ -160,6 +187,20 @@ class Store:
                 call.ev.set()
 
     def _call(self, fn):
+        if self.inline:
+            with self._ilock:
+                self._depth += 1
+                try:
+                    r = fn(self._conn_obj)
+                    if self._depth == 1:
+                        self._conn_obj.commit()
+                    return r
+                except BaseException:
+                    if self._depth == 1:
+                        self._conn_obj.rollback()
+                    raise
+                finally:
+                    self._depth -= 1
         if threading.get_ident() == getattr(self, "_tid", None):
             return fn(self._conn_obj)                     # nested call on the db thread
         call = _Call(fn)
@@ -174,6 +215,12 @@ class Store:
         await it with ``asyncio.wrap_future`` instead of blocking a thread)."""
         import concurrent.futures
         fut: concurrent.futures.Future = concurrent.futures.Future()
+        if self.inline:                        # run now, on this thread: a done future
+            try:
+                fut.set_result(self._call(fn))
+            except BaseException as e:  # noqa: BLE001 — delivered through the future
+                fut.set_exception(e)
+            return fut
         self._q.put(_Call(fn, fut))
         return fut
 
@@ -274,9 +321,26 @@ class Store:
 
     # ------------------------------------------------------------------ requests
     def create_request(self, model_name: str, prompt: str) -> int:
+        t = now_iso()
         cur = self._exec("INSERT INTO inference_request (model_name, prompt, status, created_at)"
-                         " VALUES (?,?, 'pending', ?)", (model_name, prompt, now_iso()))
-        return int(cur.lastrowid)
+                         " VALUES (?,?, 'pending', ?)", (model_name, prompt, t))
+        rid = int(cur.lastrowid)
+        if len(self._live_rows) > 200_000:            # bounded: drop the oldest half
+            for k in sorted(self._live_rows)[:100_000]:
+                self._live_rows.pop(k, None)
+        self._live_rows[rid] = {"id": rid, "model_name": model_name, "prompt": prompt,
+                                "result": None, "error": None, "status": "pending",
+                                "created_at": t, "completed_at": None, "started_at": None,
+                                "node_id": None, "attempts": 0, "execution_time": None}
+        return rid
+
+    def request_fields(self, rid: int):
+        """(model_name, prompt) of a request: immutable, so served from this process's own
+        rows when it created the request."""
+        r = self._live_rows.get(rid) or self._final_rows.get(rid)
+        if r is None:
+            r = self.get_request(rid)
+        return r["model_name"], r["prompt"]
 
     def get_request(self, rid: int) -> Dict[str, Any]:
         r = self._final_rows.get(rid)
@@ -296,29 +360,36 @@ class Store:
         self._final_rows[int(row["id"])] = dict(row)
 
     def mark_processing(self, rid: int, node_id: Optional[int] = None):
+        t = now_iso()
         self._exec("UPDATE inference_request SET status='processing', started_at=?, node_id=?, "
-                   "attempts=attempts+1 WHERE id=?", (now_iso(), node_id, rid))
+                   "attempts=attempts+1 WHERE id=?", (t, node_id, rid))
+        r = self._live_rows.get(rid)
+        if r is not None:
+            r.update(status="processing", started_at=t, node_id=node_id,
+                     attempts=r["attempts"] + 1)
+
+    def _finish(self, rid: int, sets: str, args: tuple):
+        """One terminal UPDATE; the final row comes back by RETURNING (SQLite >= 3.35) in the
+        same statement instead of a second SELECT."""
+        def tx(c):
+            if self._returning:
+                return [dict(x) for x in c.execute(
+                    f"UPDATE inference_request SET {sets} WHERE id=? RETURNING *",
+                    (*args, rid)).fetchall()]
+            self._exec(f"UPDATE inference_request SET {sets} WHERE id=?", (*args, rid))
+            return self._query("SELECT * FROM inference_request WHERE id=?", (rid,))
+        rows = self._call(tx)
+        self._live_rows.pop(rid, None)
+        if rows:
+            self._remember_final(rows[0])
+        self._notify_final(rid)
 
     def mark_completed(self, rid: int, result: str, execution_time: Optional[float] = None):
-        def tx(_c):
-            self._exec("UPDATE inference_request SET status='completed', result=?, "
-                       "completed_at=?, execution_time=? WHERE id=?",
-                       (result, now_iso(), execution_time, rid))
-            return self._query("SELECT * FROM inference_request WHERE id=?", (rid,))
-        rows = self._call(tx)
-        if rows:
-            self._remember_final(rows[0])
-        self._notify_final(rid)
+        self._finish(rid, "status='completed', result=?, completed_at=?, execution_time=?",
+                     (result, now_iso(), execution_time))
 
     def mark_failed(self, rid: int, error: str):
-        def tx(_c):
-            self._exec("UPDATE inference_request SET status='failed', error=?, completed_at=? "
-                       "WHERE id=?", (error, now_iso(), rid))
-            return self._query("SELECT * FROM inference_request WHERE id=?", (rid,))
-        rows = self._call(tx)
-        if rows:
-            self._remember_final(rows[0])
-        self._notify_final(rid)
+        self._finish(rid, "status='failed', error=?, completed_at=?", (error, now_iso()))
 
     def _notify_final(self, rid: int):
         with self._wlock:
@@ -326,8 +397,18 @@ class Store:
             aws = self._awaiters.pop(rid, None)
         if ev is not None:
             ev.set()
-        for loop, fut in aws or ():
-            loop.call_soon_threadsafe(lambda f=fut: f.done() or f.set_result(True))
+        if not aws:
+            return
+        import asyncio
+        try:
+            here = asyncio.get_running_loop()
+        except RuntimeError:
+            here = None
+        for loop, fut in aws:
+            if loop is here:                   # the waiter's own loop: no cross-thread wake-up
+                fut.done() or fut.set_result(True)
+            else:
+                loop.call_soon_threadsafe(lambda f=fut: f.done() or f.set_result(True))
 
     async def wait_final_async(self, rid: int, timeout_s: float) -> Dict[str, Any]:
         """``wait_final`` for asyncio servers: no thread is held while waiting."""
@@ -337,10 +418,15 @@ class Store:
         with self._wlock:
             self._awaiters.setdefault(rid, []).append((loop, fut))
         deadline = loop.time() + max(0.0, timeout_s)
+        first = True
         try:
             while True:
                 r = self._final_rows.get(rid)
-                if r is None:
+                live = self._live_rows.get(rid) if first else None
+                first = False
+                if r is None and live is not None:
+                    r = dict(live)                # created here, not finished: no SELECT
+                elif r is None:
                     r = await asyncio.wrap_future(self.submit(
                         lambda c: [dict(x) for x in c.execute(
                             "SELECT * FROM inference_request WHERE id=?", (rid,)).fetchall()]))
@@ -387,6 +473,9 @@ class Store:
 
     def requeue(self, rid: int):
         self._final_rows.pop(rid, None)
+        r = self._live_rows.get(rid)
+        if r is not None:
+            r.update(status="pending", node_id=None)
         self._exec("UPDATE inference_request SET status='pending', node_id=NULL WHERE id=?", (rid,))
 
     def recent_requests(self, n: int = 10) -> List[Dict[str, Any]]:

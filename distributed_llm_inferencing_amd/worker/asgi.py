@@ -52,6 +52,14 @@ def create_asgi_app(flask_app):
         return receive
 
     async def app(scope, receive, send):
+        if scope["type"] == "lifespan":           # nothing to start: acknowledge
+            while True:
+                msg = await receive()
+                if msg["type"] == "lifespan.startup":
+                    await send({"type": "lifespan.startup.complete"})
+                elif msg["type"] == "lifespan.shutdown":
+                    await send({"type": "lifespan.shutdown.complete"})
+                    return
         if not (scope["type"] == "http" and scope["method"] == "POST"
                 and scope["path"] == "/inference"):
             await wsgi(scope, receive, send)

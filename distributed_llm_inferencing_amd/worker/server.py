@@ -612,9 +612,10 @@ def main(argv=None):
     ap.add_argument("--gpu", type=int, default=None, help="GPU index (implies USE_GPU=1)")
     ap.add_argument("--preload", default="", help="comma-separated models to load at start")
     ap.add_argument("--max-batch", type=int, default=None)
-    ap.add_argument("--server", default="werkzeug", choices=["werkzeug", "uvicorn"],
+    ap.add_argument("--server", default="werkzeug", choices=["werkzeug", "uvicorn", "aiohttp"],
                     help="uvicorn: ASGI front (worker/asgi.py: /inference as a coroutine per "
-                         "request) over the same Flask app")
+                         "request) over the same Flask app; aiohttp: the same ASGI front on "
+                         "aiohttp's C HTTP parser (utils/aioserve.py)")
     a = ap.parse_args(argv)
     setup_logging(f"worker{a.port}")
     s = get_settings()
@@ -626,6 +627,11 @@ def main(argv=None):
     app = create_worker_app(s, dev, kw)
     for m in [m for m in a.preload.split(",") if m]:
         app.extensions["dli_worker"].load_model(m)
+    if a.server == "aiohttp":
+        from ..utils.aioserve import run_asgi
+        from .asgi import create_asgi_app
+        run_asgi(create_asgi_app(app), host=a.host, port=a.port)
+        return
     if a.server == "uvicorn":
         import uvicorn
 

@@ -10,7 +10,7 @@
 # (N requests), then concurrency 1 (latency of a lone request through every hop).
 # Usage: bash scripts/serve_e2e.sh [requests] [concurrency] [max_batch] [server]
 set -u
-N=${1:-1024}; C=${2:-512}; B=${3:-512}; SRV=${4:-uvicorn}
+N=${1:-1024}; C=${2:-512}; B=${3:-512}; SRV=${4:-aiohttp}
 mkdir -p gpurun_out/logs
 export MASTER_DB=/tmp/dli_e2e_$$.sqlite3 DLI_LOG_DIR=gpurun_out/logs DISPATCH_WORKERS=$C
 export HSA_ENABLE_IPC_MODE_LEGACY=0

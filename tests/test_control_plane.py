@@ -2,6 +2,7 @@
 worker API contract (Appendix B), and master -> worker dispatch over real HTTP on localhost
 with the CPU engine (config 1: gpt2 on a CPU worker)."""
 import threading
+from pathlib import Path
 import time
 
 import pytest
@@ -462,3 +463,24 @@ def test_master_asgi_long_poll(tmp_path):
     assert done["status"] == "completed" and done["result"].startswith("Hello")
     assert missing.status_code == 500 and "No InferenceRequest" in missing.json()["message"]
     assert page.status_code == 200
+
+
+@pytest.mark.parametrize("server", ["aiohttp", "uvicorn"])
+def test_control_plane_capacity_harness(server):
+    """serve-master on an ASGI server (the aiohttp C-parser front and uvicorn) in front of a
+    fake worker, driven by the closed-loop load generator through the public API
+    (scripts/bench_control_plane.py): every request completes, the submit and long-poll
+    fast paths and the on-loop dispatcher included."""
+    import json as _json
+    import subprocess
+    import sys
+    root = Path(__file__).resolve().parents[1]
+    port = 8800 + (0 if server == "aiohttp" else 10)
+    out = subprocess.run([sys.executable, str(root / "scripts" / "bench_control_plane.py"),
+                          "--concurrency", "16", "--requests", "64", "--engine-s", "0.05",
+                          "--server", server, "--master-port", str(port),
+                          "--worker-port", str(port + 1)],
+                         capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    rep = _json.loads(out.stdout.strip().splitlines()[-1])
+    assert rep["completed"] == 64 and rep["failed"] == 0, rep
