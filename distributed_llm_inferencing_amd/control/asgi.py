@@ -142,6 +142,8 @@ def create_asgi_app(flask_app):
                         "id": r["id"], "status": r["status"], "model_name": r["model_name"],
                         "prompt": r["prompt"], "result": r["result"], "error": r["error"],
                         "created_at": r["created_at"], "completed_at": r["completed_at"]})
+                    if r["status"] in ("completed", "failed"):
+                        store.answered(r["id"])
                 except Exception as e:  # noqa: BLE001 — same answer as the Flask route
                     msg = e.args[0] if isinstance(e, NotFound) else str(e)
                     await respond(send, 500, {"status": "error",

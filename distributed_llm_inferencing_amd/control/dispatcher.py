@@ -352,6 +352,9 @@ class AsyncDispatcher(Dispatcher):
                 rel(rid)
 
     async def process_async(self, rid: int) -> None:
+        mark = getattr(self.store, "mark_time", None)
+        if mark is not None:
+            mark(rid, 1)
         try:
             fields = getattr(self.store, "request_fields", None)
             if fields is not None:
@@ -424,6 +427,9 @@ class AsyncDispatcher(Dispatcher):
             if shard_ids is not None:
                 payload["shard_ids"] = sorted(shard_ids)
             st, text = await self._post_async(node, "/inference", payload, HTTP_INFER_TIMEOUT)
+            mark = getattr(self.store, "mark_time", None)
+            if mark is not None:
+                mark(rid, 2)
         except (aiohttp.ClientError, asyncio.TimeoutError, OSError,
                 faults.InjectedFault) as e:
             self._forget(node["id"])

@@ -324,7 +324,12 @@ def create_master_app(settings: Optional[Settings] = None, store: Optional[Store
             "dispatcher": {"workers": st.dispatcher.num_workers,
                            "processed": st.dispatcher.processed,
                            "inflight": dict(st.dispatcher.inflight)},
-            "health_rounds": st.health.rounds})
+            "health_rounds": st.health.rounds,
+            # mean control-plane latency per request answered by a long poll of this process
+            "control_plane_latency_s": {
+                k: round(v / max(1, store.cp_timing["answered"]), 4)
+                for k, v in store.cp_timing.items() if k != "answered"}
+            | {"answered": store.cp_timing["answered"]}})
 
     @app.get("/healthz")
     def healthz():

@@ -24,6 +24,7 @@ import os
 import queue
 import sqlite3
 import threading
+import time
 from datetime import datetime, timezone
 from typing import Any, Dict, List, Optional
 
@@ -128,6 +129,10 @@ class Store:
         # a long poll re-reads the row every 2 s)
         self._live_rows: Dict[int, Dict[str, Any]] = {}
         self._returning = sqlite3.sqlite_version_info >= (3, 35, 0)
+        # control-plane latency of requests created here: [submitted, dispatched, worker
+        # answered] (perf_counter), folded into cp_timing when the long poll answers
+        self._tmarks: Dict[int, list] = {}
+        self.cp_timing = {"answered": 0, "queue_s": 0.0, "worker_s": 0.0, "answer_s": 0.0}
         self.topology_version = 0
         self._q: "queue.SimpleQueue[_Call]" = queue.SimpleQueue()
         self._conn_obj: Optional[sqlite3.Connection] = None
@@ -328,11 +333,34 @@ class Store:
         if len(self._live_rows) > 200_000:            # bounded: drop the oldest half
             for k in sorted(self._live_rows)[:100_000]:
                 self._live_rows.pop(k, None)
+        if len(self._tmarks) > 200_000:
+            self._tmarks.clear()
+        self._tmarks[rid] = [time.perf_counter(), 0.0, 0.0]
         self._live_rows[rid] = {"id": rid, "model_name": model_name, "prompt": prompt,
                                 "result": None, "error": None, "status": "pending",
                                 "created_at": t, "completed_at": None, "started_at": None,
                                 "node_id": None, "attempts": 0, "execution_time": None}
         return rid
+
+    def mark_time(self, rid: int, idx: int) -> None:
+        """Control-plane timing mark: 1 = picked by the dispatcher, 2 = the worker answered."""
+        t = self._tmarks.get(rid)
+        if t is not None and not t[idx]:
+            t[idx] = time.perf_counter()
+
+    def answered(self, rid: int) -> None:
+        """The status API delivered the final row: fold the request's marks into cp_timing
+        (queue = submit -> dispatch, worker = dispatch -> worker answer incl. the HTTP hop,
+        answer = worker answer -> final status delivered to the client)."""
+        t = self._tmarks.pop(rid, None)
+        if t is None or not (t[1] and t[2]):
+            return
+        now = time.perf_counter()
+        c = self.cp_timing
+        c["answered"] += 1
+        c["queue_s"] += t[1] - t[0]
+        c["worker_s"] += t[2] - t[1]
+        c["answer_s"] += now - t[2]
 
     def request_fields(self, rid: int):
         """(model_name, prompt) of a request: immutable, so served from this process's own

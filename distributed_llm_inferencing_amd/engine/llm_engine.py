@@ -151,9 +151,13 @@ class LLMEngine:
     def has_work(self) -> bool:
         return self.scheduler.has_work() or self._inflight is not None
 
-    def warmup(self, buckets=None):
-        """Capture decode graphs ahead of serving (and touch every GEMM plan)."""
+    def warmup(self, buckets=None, serving: bool = False):
+        """Capture decode graphs ahead of serving (and touch every GEMM plan). ``serving``:
+        also tune the GEMM plans of mixed prefill+decode steps (requests arriving while a
+        batch decodes; a closed benchmark wave has none)."""
         self.runner.capture(buckets)
+        if serving and self.mixed_steps:
+            self.runner.autotune_mixed(self.max_batch + self.scheduler.max_prefill_tokens)
 
     def step(self) -> List[RequestOutput]:
         """One engine iteration. With lookahead (default) it schedules and launches the next

@@ -221,6 +221,19 @@ class StageRunner:
                 G.autotune_grouped(rows, lp["w_gu"], "silu_mul", log=log)
                 G.autotune_grouped(rows, lp["w_down"], "none", log=log)
 
+    def autotune_mixed(self, max_rows: int) -> None:
+        """GEMM plans for mixed prefill+decode steps (a running batch's decode rows plus the
+        prompt tokens admitted with them: 512 < M <= 1024 for a full 512-row batch). They run
+        eagerly, and without these buckets their GEMMs took the fitted heuristic's 128-row
+        tiles, not the tuned decode plans."""
+        if (os.environ.get("DLI_GEMM_AUTOTUNE", "1") != "1" or self.device.type != "cuda"
+                or os.environ.get("DLI_TUNE_MIXED", "1") != "1"):
+            return
+        top = min(1024, max_rows)
+        buckets = [m for m in range(640, top + 128, 128) if m > self.max_batch and m <= 1024]
+        if buckets:
+            self.autotune(buckets)
+
     def capture(self, buckets=None):
         """Warm up and capture decode graphs for the given buckets (default: all)."""
         if not self.use_graphs:

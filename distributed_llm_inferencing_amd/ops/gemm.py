@@ -106,7 +106,10 @@ def _heuristic(M: int, N: int, K: int, epi: str) -> GemmPlan:
     (tile 22) with its fused epilogue (SiLU*up, bias+GELU, fp32) — no library GEMM on the
     hot path. ``DLI_GEMM_PREFILL_BLAS=1`` routes plain prefill GEMMs to hipBLASLt instead
     (ablation only)."""
-    if M >= LARGE_M:
+    # M > 512: mixed prefill+decode steps of a full batch and prefill — 256x256 8-phase
+    # tiles (the 128-row tiles below ran a 512 + 300-token mixed step's GEMMs ~2.5x slower
+    # than the tuned decode step: 26.7 ms per mixed step end to end, profiles/r3/e2e/)
+    if M >= LARGE_M or M > 512:
         if (os.environ.get("DLI_GEMM_PREFILL_BLAS", "0") == "1" and epi in ("none", "splitk")
                 and os.environ.get("DLI_GEMM_NO_BLAS", "0") != "1"):
             return GemmPlan("hipblaslt", 2, 1)
@@ -220,11 +223,15 @@ def autotune_grouped(rows: int, w: torch.Tensor, epi: str, iters: int = 5, log=N
 
 
 def _bucket(M: int) -> int:
-    """Plan-cache key for M: exact up to 1024 rows (decode graph buckets are a fixed small
+    """Plan-cache key for M: exact up to 512 rows (decode graph buckets are a fixed small
     set and their best plans differ: one plan per power of two let M=320's plan run M=512),
-    power-of-two above (prefill)."""
-    if M <= 1024:
+    a multiple of 128 up to 1024 (the sizes of mixed prefill+decode steps of a full batch,
+    tuned as a few buckets when serving: StageRunner.autotune_mixed), power-of-two above
+    (prefill)."""
+    if M <= 512:
         return M
+    if M <= 1024:
+        return -(-M // 128) * 128
     b = 1
     while b < M:
         b <<= 1

@@ -119,7 +119,7 @@ class WorkerState:
                 eng = LLMEngine(cfg, device=str(self.device), **self.engine_kwargs)
                 self.weights_source[name] = "random-init"
             if eng.device.type == "cuda":
-                eng.warmup()          # capture decode graphs (+ GEMM autotune) before serving
+                eng.warmup(serving=True)   # decode graphs (+ GEMM autotune, mixed-step plans)
             self.services[name] = EngineService(eng, name=name.replace("/", "_"))
             self.tokenizers[name] = eng.tokenizer
             return True

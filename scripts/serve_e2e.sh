@@ -20,6 +20,7 @@ MPID=$!
 python -m distributed_llm_inferencing_amd.cli serve-worker --port 5000 --gpu 0 --max-batch $B --server $SRV \
     --preload llama3-8b > gpurun_out/e2e_worker.log 2>&1 &
 WPID=$!
+cpu() { awk '{print $14 + $15}' /proc/$1/stat; }   # utime + stime, clock ticks
 ok=0
 for i in $(seq 1 600); do
   if curl -sf http://127.0.0.1:5000/health | grep -q llama3-8b; then ok=1; break; fi
@@ -34,7 +35,10 @@ if [ $ok = 1 ]; then
   # warm-up wave (same shape)
   timeout -k 10 600 $LG --requests $C --concurrency $C --seed 99 > gpurun_out/e2e_warmup.json && \
   curl -s http://127.0.0.1:5000/metrics > gpurun_out/e2e_metrics_before.json && \
+  cpu0="$(cpu $MPID) $(cpu $WPID) $(date +%s.%N)" && \
   timeout -k 10 900 $LG --requests $N --concurrency $C > gpurun_out/e2e_loadgen_c$C.json && \
+  cpu1="$(cpu $MPID) $(cpu $WPID) $(date +%s.%N)" && \
+  python -c "import json,sys,os; a=[float(x) for x in sys.argv[1].split()]; b=[float(x) for x in sys.argv[2].split()]; hz=os.sysconf('SC_CLK_TCK'); w=b[2]-a[2]; print(json.dumps({'wall_s': round(w,3), 'master_cores_busy': round((b[0]-a[0])/hz/w,3), 'worker_cores_busy': round((b[1]-a[1])/hz/w,3)}))" "$cpu0" "$cpu1" > gpurun_out/e2e_cpu.json && \
   curl -s http://127.0.0.1:5000/metrics > gpurun_out/e2e_metrics_after.json && \
   timeout -k 10 600 $LG --requests 16 --concurrency 1 --poll 0.01 > gpurun_out/e2e_loadgen_c1.json
   rc=$?

@@ -258,6 +258,17 @@ def test_prefill_gemm_plan_is_own_kernel(monkeypatch):
     assert G.plan(1024, 4096, 4096, "splitk") == G.GemmPlan("dli", 22, 4)      # 64 tiles
     assert G.plan(1200, 28672, 4096, "silu_mul").splits == 1
     assert all(p.backend == "dli" for p in G.candidate_plans(512, 4096, 4096, "none"))
+    # mixed prefill+decode steps of a full batch (512 < M < 1024): 8-phase tiles, and one
+    # plan-cache bucket per 128 rows (tuned when serving: StageRunner.autotune_mixed)
+    assert G.plan(800, 28672, 4096, "silu_mul") == G.GemmPlan("dli", 22, 1)
+    assert G.plan(600, 4096, 14336, "splitk").tile == 22
+    assert [G._bucket(m) for m in (512, 513, 640, 641, 1000, 1024, 1025)] == \
+        [512, 640, 640, 768, 1024, 1024, 2048]
+    G.set_plan(700, 4096, 4096, "splitk", G.GemmPlan("dli", 16, 4))
+    assert G.plan(650, 4096, 4096, "splitk") == G.GemmPlan("dli", 16, 4)   # same bucket
+    # 256x224 joins the autotune candidates where it lands on whole waves of the chip
+    assert not any(p.tile == 26 for p in G.candidate_plans(512, 28672, 4096, "silu_mul"))
+    assert any(p.tile == 26 for p in G.candidate_plans(512, 57344, 8192, "silu_mul"))
     G.clear_plans()
     monkeypatch.setenv("DLI_GEMM_PREFILL_BLAS", "1")
     assert G.plan(16384, 6144, 4096, "none").backend == "hipblaslt"
