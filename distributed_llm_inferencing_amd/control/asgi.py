@@ -113,6 +113,9 @@ def create_asgi_app(flask_app):
         if (os.environ.get("DLI_DISPATCH_ON_SERVER_LOOP", "0") == "1"
                 and hasattr(d, "start_on_loop") and not d._threads):
             d.start_on_loop(asyncio.get_running_loop())
+        n = getattr(state, "notifier", None)
+        if n is not None and not n._listening:          # peers' finished requests
+            asyncio.get_running_loop().create_task(n.listen(store._notify_final))
 
     async def app(scope, receive, send):
         if scope["type"] == "lifespan":

@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import logging
 import os
+import time
 from pathlib import Path
 from typing import Optional
 
@@ -46,24 +47,36 @@ class MasterState:
                  dispatch_workers: Optional[int] = None, health_interval: float = 10.0):
         self.settings = settings
         self.store = store
+        # serve-master --procs N: this process's rank; peers share the database and hear of
+        # each other's finished requests (control/peers.py)
+        self.rank = int(os.environ.get("DLI_MASTER_RANK", "0"))
+        self.nprocs = int(os.environ.get("DLI_MASTER_PROCS", "1"))
+        self.notifier = None
+        if self.nprocs > 1:
+            from .peers import PeerNotifier
+            self.notifier = PeerNotifier(self.rank, self.nprocs,
+                                         int(os.environ.get("DLI_MASTER_NOTIFY_PORT", "47600")))
+            store.on_final = self.notifier.publish
         self.queue = make_queue(settings.queue_backend, store, settings)
         self.health = HealthMonitor(store, settings, interval=health_interval)
         self.dispatcher = make_dispatcher(store, self.queue, settings,
                                           num_workers=dispatch_workers or
                                           settings.dispatch_workers,
                                           on_node_error=self.health.report_failure)
-        recovered = store.recover("requeue")
-        for rid in store.pending_ids():
-            self.queue.put(rid)
-        if recovered:
-            log.warning("re-queued %d requests orphaned in 'processing'", len(recovered))
+        if self.rank == 0:
+            recovered = store.recover("requeue")
+            for rid in store.pending_ids():
+                self.queue.put(rid)
+            if recovered:
+                log.warning("re-queued %d requests orphaned in 'processing'", len(recovered))
         if start_background:
             # an ASGI front (serve-master --server uvicorn / aiohttp) runs the async
             # dispatcher on its own event loop (control/asgi.py starts it there)
             if not (os.environ.get("DLI_DISPATCH_ON_SERVER_LOOP", "0") == "1"
                     and hasattr(self.dispatcher, "start_on_loop")):
                 self.dispatcher.start()
-            self.health.start()
+            if self.rank == 0:
+                self.health.start()
 
     def shutdown(self):
         self.dispatcher.stop()
@@ -348,15 +361,22 @@ def main(argv=None):
                          "ASGI front (control/asgi.py: async submit and status long polls) "
                          "over the same Flask app; aiohttp: the same ASGI front on aiohttp's "
                          "C HTTP parser (utils/aioserve.py)")
+    ap.add_argument("--procs", type=int, default=int(os.environ.get("DLI_MASTER_PROCS", "1")),
+                    help="aiohttp: N master processes on one port and one database "
+                         "(control/peers.py)")
     a = ap.parse_args(argv)
     if a.server in ("aiohttp", "uvicorn"):
         os.environ.setdefault("DLI_DISPATCH_ON_SERVER_LOOP", "1")
     if a.server == "aiohttp":
+        if a.procs > 1 and "DLI_MASTER_RANK" not in os.environ:
+            return _spawn_procs(a, argv)
         from .asgi import create_asgi_app
         from ..utils.aioserve import run_asgi
         from ..utils.log import setup_logging
-        setup_logging("master")
-        run_asgi(create_asgi_app(create_master_app()), host=a.host, port=a.port)
+        rank = os.environ.get("DLI_MASTER_RANK")
+        setup_logging("master" if rank in (None, "0") else f"master{rank}")
+        run_asgi(create_asgi_app(create_master_app()), host=a.host, port=a.port,
+                 reuse_port=a.procs > 1)
         return
     if a.server == "uvicorn":
         # ASGI front: status long polls as coroutines, the Flask app behind a WSGI adapter
@@ -372,6 +392,47 @@ def main(argv=None):
     setup_logging("master")
     app = create_master_app()
     app.run(host=a.host, port=a.port, threaded=True)
+
+
+def _spawn_procs(a, argv) -> int:
+    """serve-master --server aiohttp --procs N: N child processes (rank 0..N-1) serving the
+    same port (SO_REUSEPORT) and database; exits with the first child's failure."""
+    import signal
+    import subprocess
+    import sys
+    settings = get_settings()
+    if settings.master_db in ("", ":memory:"):
+        raise SystemExit("--procs > 1 needs a database file (MASTER_DB) the processes share")
+    procs = []
+    for r in range(a.procs):
+        env = dict(os.environ, DLI_MASTER_RANK=str(r), DLI_MASTER_PROCS=str(a.procs))
+        procs.append(subprocess.Popen([sys.executable, "-m", "distributed_llm_inferencing_amd.cli",
+                                       "serve-master", *(argv or [])], env=env))
+        if r == 0:
+            time.sleep(1.0)             # rank 0 creates the schema and re-queues first
+
+    def stop(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+    signal.signal(signal.SIGTERM, stop)
+    signal.signal(signal.SIGINT, stop)
+    rc = 0
+    try:
+        while True:
+            for p in procs:
+                r = p.poll()
+                if r is not None:
+                    stop()
+                    for q in procs:
+                        try:
+                            q.wait(10)
+                        except subprocess.TimeoutExpired:
+                            q.kill()
+                    return r or rc
+            time.sleep(0.5)
+    finally:
+        stop()
 
 
 if __name__ == "__main__":

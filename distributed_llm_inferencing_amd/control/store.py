@@ -133,6 +133,8 @@ class Store:
         # answered] (perf_counter), folded into cp_timing when the long poll answers
         self._tmarks: Dict[int, list] = {}
         self.cp_timing = {"answered": 0, "queue_s": 0.0, "worker_s": 0.0, "answer_s": 0.0}
+        # called with a request id when this process finished it (peer fan-out, peers.py)
+        self.on_final = None
         self.topology_version = 0
         self._q: "queue.SimpleQueue[_Call]" = queue.SimpleQueue()
         self._conn_obj: Optional[sqlite3.Connection] = None
@@ -411,6 +413,8 @@ class Store:
         if rows:
             self._remember_final(rows[0])
         self._notify_final(rid)
+        if self.on_final is not None:
+            self.on_final(rid)
 
     def mark_completed(self, rid: int, result: str, execution_time: Optional[float] = None):
         self._finish(rid, "status='completed', result=?, completed_at=?, execution_time=?",

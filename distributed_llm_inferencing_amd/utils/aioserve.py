@@ -62,7 +62,7 @@ def asgi_handler(asgi_app: Callable, host: str, port: int):
 
 
 def run_asgi(asgi_app: Any, host: str = "0.0.0.0", port: int = 8000,
-             backlog: int = 4096) -> None:
+             backlog: int = 4096, reuse_port: bool = False) -> None:
     from aiohttp import web
     app = web.Application(client_max_size=64 << 20)
     app.router.add_route("*", "/{tail:.*}", asgi_handler(asgi_app, host, port))
@@ -82,4 +82,4 @@ def run_asgi(asgi_app: Any, host: str = "0.0.0.0", port: int = 8000,
             pass
     app.on_startup.append(lifespan_startup)
     web.run_app(app, host=host, port=port, backlog=backlog, access_log=None,
-                print=None, keepalive_timeout=75)
+                print=None, keepalive_timeout=75, reuse_port=reuse_port or None)

@@ -81,6 +81,8 @@ def main():
     ap.add_argument("--master-port", type=int, default=8731)
     ap.add_argument("--worker-port", type=int, default=5731)
     ap.add_argument("--server", default="aiohttp", choices=["uvicorn", "aiohttp"])
+    ap.add_argument("--master-procs", type=int, default=1,
+                    help="serve-master --procs (aiohttp: processes sharing port + database)")
     ap.add_argument("--profile", default="", help="write a sampling profile of the master")
     ap.add_argument("--fake-worker", action="store_true", help=argparse.SUPPRESS)
     a = ap.parse_args()
@@ -104,7 +106,8 @@ def main():
                     "distributed_llm_inferencing_amd.cli"]
         procs.append(subprocess.Popen([sys.executable, *mcmd,
                                        "serve-master", "--port", str(a.master_port),
-                                       "--server", a.server], env=env,
+                                       "--server", a.server, "--procs", str(a.master_procs)],
+                                      env=env,
                                       stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL))
         master = f"http://127.0.0.1:{a.master_port}"
         if not (wait_http(f"http://127.0.0.1:{a.worker_port}/health")
@@ -121,8 +124,13 @@ def main():
                              str(a.concurrency), "--seed", "99"], env=env, check=True,
                        stdout=subprocess.DEVNULL)
         import psutil
-        ps = {"fake_worker": psutil.Process(procs[0].pid), "master": psutil.Process(procs[1].pid)}
-        cpu0 = {k: sum(p.cpu_times()[:2]) for k, p in ps.items()}
+        mp = psutil.Process(procs[1].pid)
+        ps = {"fake_worker": [psutil.Process(procs[0].pid)],
+              "master": [mp] + mp.children(recursive=True)}
+
+        def cpu_s(k):
+            return sum(sum(p.cpu_times()[:2]) for p in ps[k])
+        cpu0 = {k: cpu_s(k) for k in ps}
         import resource
         ru0 = resource.getrusage(resource.RUSAGE_CHILDREN)
         t0 = time.time()
@@ -130,7 +138,7 @@ def main():
                                    str(a.concurrency)], env=env, check=True,
                              capture_output=True, text=True)
         wall = time.time() - t0
-        cpu = {k: round((sum(p.cpu_times()[:2]) - cpu0[k]) / wall, 3) for k, p in ps.items()}
+        cpu = {k: round((cpu_s(k) - cpu0[k]) / wall, 3) for k in ps}
         ru1 = resource.getrusage(resource.RUSAGE_CHILDREN)
         cpu["loadgen"] = round((ru1.ru_utime + ru1.ru_stime - ru0.ru_utime - ru0.ru_stime)
                                / wall, 3)
@@ -141,7 +149,8 @@ def main():
                    control_plane_latency_s=round(a.concurrency / rep["requests_per_s"]
                                                  - a.engine_s, 4)
                    if rep.get("requests_per_s") else None,
-                   cpus=os.cpu_count(), cores_busy=cpu, master_server=a.server)
+                   cpus=os.cpu_count(), cores_busy=cpu, master_server=a.server,
+                   master_procs=a.master_procs)
         print(json.dumps(rep), flush=True)
         return 0
     finally:

@@ -465,22 +465,25 @@ def test_master_asgi_long_poll(tmp_path):
     assert page.status_code == 200
 
 
-@pytest.mark.parametrize("server", ["aiohttp", "uvicorn"])
-def test_control_plane_capacity_harness(server):
-    """serve-master on an ASGI server (the aiohttp C-parser front and uvicorn) in front of a
-    fake worker, driven by the closed-loop load generator through the public API
+@pytest.mark.parametrize("server,procs", [("aiohttp", 1), ("uvicorn", 1), ("aiohttp", 3)])
+def test_control_plane_capacity_harness(server, procs):
+    """serve-master on an ASGI server (the aiohttp C-parser front and uvicorn; 3 aiohttp
+    processes on one port and one database, control/peers.py) in front of a fake worker,
+    driven by the closed-loop load generator through the public API
     (scripts/bench_control_plane.py): every request completes, the submit and long-poll
-    fast paths and the on-loop dispatcher included."""
+    fast paths, the on-loop dispatcher and the cross-process completion fan-out included."""
     import json as _json
     import subprocess
     import sys
     root = Path(__file__).resolve().parents[1]
-    port = 8800 + (0 if server == "aiohttp" else 10)
+    port = 8800 + (0 if server == "aiohttp" else 10) + 20 * (procs - 1)
     out = subprocess.run([sys.executable, str(root / "scripts" / "bench_control_plane.py"),
                           "--concurrency", "16", "--requests", "64", "--engine-s", "0.05",
                           "--server", server, "--master-port", str(port),
-                          "--worker-port", str(port + 1)],
+                          "--worker-port", str(port + 1), "--master-procs", str(procs)],
                          capture_output=True, text=True, timeout=240)
     assert out.returncode == 0, out.stderr[-2000:]
     rep = _json.loads(out.stdout.strip().splitlines()[-1])
     assert rep["completed"] == 64 and rep["failed"] == 0, rep
+    # no long poll waited for its 2 s re-read: completions reached every process
+    assert rep["p99_latency_s"] < 1.5, rep
