@@ -37,6 +37,12 @@ class EngineStats:
     mixed_steps: int = 0            # prefill steps that also carried decode rows
     busy_s: float = 0.0
     finished: int = 0
+    # batch shape per launched step (serving diagnostics): decode rows of decode steps and of
+    # mixed steps, prompt tokens of mixed steps, and the scheduler's running / waiting counts
+    decode_rows: int = 0
+    mixed_decode_rows: int = 0
+    running_sum: int = 0
+    waiting_sum: int = 0
     latencies: List[float] = field(default_factory=list)
 
     def snapshot(self) -> dict:
@@ -47,6 +53,8 @@ class EngineStats:
                 "output_tokens": self.tokens_out,
                 "prompt_tokens": self.prompt_tokens, "finished_requests": self.finished,
                 "busy_s": round(self.busy_s, 4),
+                "decode_rows": self.decode_rows, "mixed_decode_rows": self.mixed_decode_rows,
+                "running_sum": self.running_sum, "waiting_sum": self.waiting_sum,
                 "tokens_per_s": (self.tokens_out / self.busy_s) if self.busy_s > 0 else 0.0,
                 "p50_latency_s": pct(0.5), "p99_latency_s": pct(0.99)}
 
@@ -188,13 +196,18 @@ class LLMEngine:
                 tokens = self.runner.run(meta, feed=prev[1] if prev is not None else None)
             launched = (meta, tokens, _HostTokens(tokens))
             self.stats.steps += 1
+            sch = self.scheduler
+            self.stats.running_sum += sch.num_running()
+            self.stats.waiting_sum += len(sch.waiting)
             if meta.kind == 1:
                 self.stats.prefill_steps += 1
                 self.stats.prompt_tokens += meta.num_tokens - meta.num_decode
                 if meta.num_decode:
                     self.stats.mixed_steps += 1
+                    self.stats.mixed_decode_rows += meta.num_decode
             else:
                 self.stats.decode_steps += 1
+                self.stats.decode_rows += meta.num_seqs
         if self.lookahead:
             self._inflight = launched
             done = prev
