@@ -90,6 +90,11 @@ class EngineService:
         sch = getattr(self.engine, "scheduler", None)
         if sch is not None:
             s["prefix_hit_tokens"] = sch.prefix_hit_tokens
+            s["preempted"] = sch.num_preempted
+            s["max_seqs"] = sch.max_seqs
+        bm = getattr(self.engine, "bm", None)
+        if bm is not None:
+            s["kv_free_blocks"] = bm.num_free
         if getattr(self.engine, "timer", None) is not None:
             s["phases"] = self.engine.timer.snapshot()     # host time per engine-loop phase
         s["queued"] = self._inbox.qsize()
