@@ -9,12 +9,13 @@
 // Numerics equal the unfused path: the GEMM result is rounded to bf16 before the residual add
 // / rotation, exactly as the bf16 GEMM output would be.
 #include "common.h"
+#include <stdlib.h>
 
 // SPL > 0: the split count is a compile-time constant, so every partial of a thread is
 // loaded before the first add (SPL x VPT x 2 16-B loads in flight per lane instead of 2 x VPT);
 // SPL == 0 reads `splits` partials in a runtime loop.
 template <int VPT, int SPL>
-__global__ void __launch_bounds__(256) splitk_add_rmsnorm_kernel(
+__global__ void __launch_bounds__(512) splitk_add_rmsnorm_kernel(
     u16* __restrict__ out, u16* __restrict__ residual, const float* __restrict__ ws, int splits,
     int M, int N, const u16* __restrict__ w, float eps) {
   __shared__ float red[16];
@@ -93,8 +94,17 @@ extern "C" int dli_splitk_add_rmsnorm(void* out, void* residual, const float* ws
   if (M <= 0) return 0;
   if (N % 8) return (int)hipErrorInvalidValue;
   const int nvec = N / 8;
+  // threads per row (one workgroup per row): 512, i.e. one 8-column vector per lane at
+  // N = 4096 (same-box A/B with the GEMMs that feed it, M = 512: O + reduce 33.85-33.92 ->
+  // 33.4 us, down + reduce 70.5-70.8 -> 69.95 us; profiles/r3/reduce_threads/);
+  // DLI_REDUCE_THREADS=256 / 128 / 64 for A/Bs
+  static const int cap = [] {
+    const char* e = getenv("DLI_REDUCE_THREADS");
+    const int v = e ? atoi(e) : 512;
+    return (v == 256 || v == 128 || v == 64) ? v : 512;
+  }();
   int threads = ((nvec + 63) / 64) * 64;
-  if (threads > 256) threads = 256;
+  if (threads > cap) threads = cap;
   const int vpt = (nvec + threads - 1) / threads;
   auto o = (u16*)out; auto r = (u16*)residual; auto wp = (const u16*)w;
   switch (vpt) {

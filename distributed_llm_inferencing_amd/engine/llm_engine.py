@@ -144,6 +144,8 @@ class LLMEngine:
         self.lookahead = (os.environ.get("DLI_LOOKAHEAD", "1") == "1"
                           if lookahead is None else bool(lookahead))
         self._inflight = None           # (meta, device tokens, host copy) of the in-flight step
+        tr = os.environ.get("DLI_STEP_TRACE")
+        self._trace = open(tr, "a", buffering=1) if tr else None   # line-buffered: survives a kill
 
     # ------------------------------------------------------------------ API
     def add_request(self, prompt: Union[str, List[int]], params: Optional[SamplingParams] = None,
@@ -199,6 +201,10 @@ class LLMEngine:
             sch = self.scheduler
             self.stats.running_sum += sch.num_running()
             self.stats.waiting_sum += len(sch.waiting)
+            if self._trace is not None:         # DLI_STEP_TRACE: one line per launched step
+                self._trace.write(f"{time.perf_counter():.6f} {meta.kind} {meta.num_seqs} "
+                                  f"{meta.num_decode} {meta.num_tokens} {sch.num_running()} "
+                                  f"{len(sch.waiting)}\n")
             if meta.kind == 1:
                 self.stats.prefill_steps += 1
                 self.stats.prompt_tokens += meta.num_tokens - meta.num_decode
