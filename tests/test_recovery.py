@@ -27,10 +27,20 @@ import requests
 import torch
 
 
+_USED_PORTS = set()
+
+
 def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    """A free loopback port not handed out before in this process (the OS may return the
+    same ephemeral port to two bind(0) calls once the first socket is closed: two stage
+    workers on one port made join-pipeline post shard 3 to stage 2's worker)."""
+    while True:
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            p = s.getsockname()[1]
+        if p not in _USED_PORTS:
+            _USED_PORTS.add(p)
+            return p
 
 
 def _wait_http(url, t=120):
