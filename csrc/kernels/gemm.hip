@@ -1499,6 +1499,11 @@ static int dispatch_gemv(int tile_cfg, const void* A, int lda, const void* W, in
   if (tile_cfg == 32)
     return M <= 1 ? launch_gemv<1, 4, EPI, 4>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st)
                   : (int)hipErrorInvalidValue;
+  // 33: 32 rows (SiLU gate/up pairs) with 4 K-steps in flight per lane (M = 1): 32 weight
+  // loads of 16 B outstanding per lane instead of 16 (tile 31)
+  if (tile_cfg == 33)
+    return M <= 1 ? launch_gemv<1, 8, EPI, 4>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st)
+                  : (int)hipErrorInvalidValue;
   if (M <= 1)
     return r32 ? launch_gemv<1, 8, EPI>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st)
                : launch_gemv<1, 4, EPI>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st);
@@ -1543,7 +1548,7 @@ static int dispatch_tile(int tile_cfg, const void* A, int lda, const void* W, in
     // M = 512 (64 tiles x split 4)
     case 28: return launch_8p128<EPI>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
     // skinny weight-streaming GEMM for M <= 4 (no grouped mode)
-    case 30: case 31: case 32:
+    case 30: case 31: case 32: case 33:
       if (go != nullptr) return (int)hipErrorInvalidValue;
       return dispatch_gemv<EPI>(tile_cfg, A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st);
 #undef DLI_CFG8

@@ -47,7 +47,7 @@ TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256), 4: (256, 128),
          28: (256, 128)}
 # weight-streaming skinny GEMM (gemm.hip gemv_kernel) for M <= GEMV_MAX_M rows: 16 / 32 output
 # rows per workgroup (31 for the SiLU*up gate/up pairing); not an MFMA tile, so kept apart
-GEMV_TILES = {30: 16, 31: 32, 32: 16}      # 32: 4 K-steps in flight per lane, M = 1
+GEMV_TILES = {30: 16, 31: 32, 32: 16, 33: 32}   # 32 / 33: 4 K-steps in flight per lane, M = 1
 GEMV_MAX_M = 4
 TILE_WAVES = {13: (2, 4), 14: (4, 2), 15: (2, 4), 16: (4, 2), 17: (2, 4),
               22: (2, 4), 23: (2, 4), 24: (2, 4), 25: (4, 2),
@@ -58,7 +58,7 @@ def tile_ok(tile: int, epi: str) -> bool:
     """The SiLU*up epilogue pairs 16-column gate/up blocks inside a wave's column range,
     which must therefore be a multiple of 32."""
     if tile in GEMV_TILES:
-        return epi != "silu_mul" or tile == 31
+        return epi != "silu_mul" or tile in (31, 33)
     if epi != "silu_mul":
         return True
     if tile == 26:              # the straddling gate/up pair meets through LDS
@@ -375,7 +375,7 @@ def candidate_plans(M: int, N: int, K: int, epi: str):
             out.append(GemmPlan("dli", tile, splits))
     if M <= GEMV_MAX_M:
         for tile in GEMV_TILES:
-            if tile in excl or not tile_ok(tile, epi) or (tile == 32 and M > 1):
+            if tile in excl or not tile_ok(tile, epi) or (tile in (32, 33) and M > 1):
                 continue
             for splits in (1, 2, 4, 8):
                 if K % (64 * splits) == 0 and K // splits >= 512:
