@@ -162,10 +162,12 @@ class LLMEngine:
         return self.scheduler.has_work() or self._inflight is not None
 
     def warmup(self, buckets=None, serving: bool = False):
-        """Capture decode graphs ahead of serving (and touch every GEMM plan). ``serving``:
+        """Capture decode graphs ahead of serving (and touch every GEMM plan), tune the
+        prefill GEMM plans (``StageRunner.autotune_prefill``). ``serving``:
         also tune the GEMM plans of mixed prefill+decode steps (requests arriving while a
         batch decodes; a closed benchmark wave has none)."""
         self.runner.capture(buckets)
+        self.runner.autotune_prefill(self.scheduler.max_prefill_tokens)
         if serving and self.mixed_steps:
             self.runner.autotune_mixed(self.max_batch + self.scheduler.max_prefill_tokens)
 

@@ -221,6 +221,30 @@ class StageRunner:
                 G.autotune_grouped(rows, lp["w_gu"], "silu_mul", log=log)
                 G.autotune_grouped(rows, lp["w_down"], "none", log=log)
 
+    def autotune_prefill(self, max_tokens: int) -> None:
+        """GEMM plans of prefill steps, one per power-of-two token bucket from 2048 up to the
+        bucket of ``max_tokens``: our 8-phase kernel against hipBLASLt, the faster pinned
+        (``ops.gemm.prefill_candidates``). Skipped like the decode autotune
+        (DLI_GEMM_AUTOTUNE=0, non-GPU) and by DLI_TUNE_PREFILL=0."""
+        if (os.environ.get("DLI_GEMM_AUTOTUNE", "1") != "1" or self.device.type != "cuda"
+                or os.environ.get("DLI_TUNE_PREFILL", "1") != "1"):
+            return
+        from ..ops import gemm as G
+        log = None
+        if os.environ.get("DLI_GEMM_AUTOTUNE_LOG", "0") == "1":
+            import sys
+            log = lambda m: print(m, file=sys.stderr, flush=True)  # noqa: E731
+        top = G._bucket(max(max_tokens, 2048))
+        c = self.model.cfg
+        qkv = (c.num_heads, c.num_kv_heads, c.head_dim) if c.arch != "gpt2" else None
+        b = 2048
+        while b <= top:
+            shapes, weights = self.gemm_shapes(b)
+            shapes = [s for s in shapes if s[3] != "f32"]     # prefill's LM head: last rows
+            G.autotune(shapes, weights, self.device, iters=3, log=log, cold_bytes=1,
+                       qkv_heads=qkv, candidates=G.prefill_candidates)
+            b *= 2
+
     def autotune_mixed(self, max_rows: int) -> None:
         """GEMM plans for mixed prefill+decode steps (a running batch's decode rows plus the
         prompt tokens admitted with them: 512 < M <= 1024 for a full 512-row batch). They run

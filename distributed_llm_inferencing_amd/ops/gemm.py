@@ -6,10 +6,12 @@ The projection GEMMs of a decode step are skinny (M = batch) and of a prefill st
 * a tile from {64x64, 64x128, 128x128, 128x256, 256x128} sized to M,
 * a split-K factor so the grid covers the 256 CUs (cdna_hip_programming.md §5 'Projection
   GEMM at M = 256': choose SPLITK so that tiles * SPLITK ~ 0.5-1x the CU count),
-* the backend: always our MFMA kernels (decode tiles autotuned at graph capture, on by
-  default; ``DLI_GEMM_AUTOTUNE=0`` disables it; prefill on the 8-phase 256x256 kernel).
-  hipBLASLt (torch.matmul) remains reachable only as an explicit ablation
-  (``DLI_GEMM_BACKEND=hipblaslt``, ``DLI_GEMM_PREFILL_BLAS=1``, ``DLI_GEMM_DECODE_BLAS=1``).
+* the backend: decode GEMMs (the hipGraph steps) always on our MFMA kernels, tiles
+  autotuned at graph capture (on by default; ``DLI_GEMM_AUTOTUNE=0`` disables it). Prefill
+  GEMMs: our 8-phase 256x256 kernel or hipBLASLt (torch.matmul + our epilogue pass),
+  whichever the warmup measures faster per token bucket (``prefill_candidates``;
+  ``DLI_GEMM_NO_BLAS=1`` keeps everything on our kernels). ``DLI_GEMM_BACKEND=hipblaslt``,
+  ``DLI_GEMM_PREFILL_BLAS=1`` and ``DLI_GEMM_DECODE_BLAS=1`` remain as ablations.
 
 Split-K partial slabs live in a grow-only per-device workspace; engines warm every shape
 up before hipGraph capture so no allocation happens inside a capture.
@@ -103,9 +105,10 @@ def _heuristic(M: int, N: int, K: int, epi: str) -> GemmPlan:
     """Fitted to profiles/r1_gemm/gemm_bench.json and profiles/r1_gemm8p/ (MI355X, random
     bf16 operands): skinny decode GEMMs (M <= 512) on the 2/3-stage tiles below (autotuned
     at capture); fat prefill GEMMs (M >= LARGE_M) on the 256x256 8-phase ping-pong kernel
-    (tile 22) with its fused epilogue (SiLU*up, bias+GELU, fp32) — no library GEMM on the
-    hot path. ``DLI_GEMM_PREFILL_BLAS=1`` routes plain prefill GEMMs to hipBLASLt instead
-    (ablation only)."""
+    (tile 22) with its fused epilogue (SiLU*up, bias+GELU, fp32) unless the prefill
+    autotune (``prefill_candidates``) measured hipBLASLt faster for the bucket.
+    ``DLI_GEMM_PREFILL_BLAS=1`` routes plain prefill GEMMs to hipBLASLt without measuring
+    (ablation)."""
     # M > 512: mixed prefill+decode steps of a full batch and prefill — 256x256 8-phase
     # tiles (the 128-row tiles below ran a 512 + 300-token mixed step's GEMMs ~2.5x slower
     # than the tuned decode step: 26.7 ms per mixed step end to end, profiles/r3/e2e/)
@@ -257,10 +260,11 @@ def set_plan(M: int, N: int, K: int, epi: str, p: GemmPlan) -> None:
 
 def clear_plans() -> None:
     _plan_cache.clear()
+    _tuned.clear()
 
 
 def autotune(shapes, weights: dict, device, iters: int = 6, log=None,
-             cold_bytes: int = 1 << 30, qkv_heads=None) -> dict:
+             cold_bytes: int = 1 << 30, qkv_heads=None, candidates=None) -> dict:
     """Measure every candidate plan for each (M, N, K, epi) and pin the fastest
     ("measure, don't guess"). ``weights[(N, K)]`` is a real [N, K] weight of that shape.
 
@@ -273,6 +277,7 @@ def autotune(shapes, weights: dict, device, iters: int = 6, log=None,
     QKV projection, whose consumer is the decode attention prologue (slab sum or bf16 read,
     RoPE, KV write), so its candidates are timed with the RoPE + cache-write kernel of the
     same input (``ops.linear_rope_cache``) instead of the add + RMSNorm one.
+    ``candidates(M, N, K, epi)`` replaces the plan list (``prefill_candidates``).
     Returns {shape: (plan, ms)}."""
     from .. import ops  # local import: ops imports this module
     out = {}
@@ -302,7 +307,7 @@ def autotune(shapes, weights: dict, device, iters: int = 6, log=None,
             cs = R.rope_cos_sin(16, hd, 10000.0, device=device)
         best = None
         t_shape = time.perf_counter()
-        for p in candidate_plans(M, N, K, epi):
+        for p in (candidates or candidate_plans)(M, N, K, epi):
             if p.backend == "hipblaslt" and epi not in ("none", "splitk", "silu_mul", "f32"):
                 continue
 
@@ -338,6 +343,23 @@ def autotune(shapes, weights: dict, device, iters: int = 6, log=None,
 _tuned: set = set()
 # candidates timed as graph replays (ops.benchmark graph=True); DLI_GEMM_TUNE_GRAPH=0: eager
 _GRAPH_TUNE = os.environ.get("DLI_GEMM_TUNE_GRAPH", "1") == "1"
+
+
+def prefill_candidates(M: int, N: int, K: int, epi: str):
+    """Prefill-sized GEMMs (M > 1024 rows): our 8-phase 256x256 kernel with the heuristic's
+    split count against hipBLASLt (+ our SiLU*up pass for gate/up; the residual add + RMSNorm
+    and RoPE/cache consumers run as their own kernels after either). At these sizes the GEMM
+    is MFMA-bound, so the autotuner times them warm (``cold_bytes`` 1). Measured at
+    M = 16384 on MI355X: ours 1.37-1.46 PF, hipBLASLt 1.57-1.62 PF on the plain projections
+    (profiles/r3/prefill_gemm/); ``DLI_GEMM_NO_BLAS=1`` or ``DLI_TUNE_PREFILL_BLAS=0`` keeps
+    every prefill GEMM on our kernels."""
+    out = [_heuristic(M, N, K, epi)]
+    if (epi in ("none", "splitk", "silu_mul", "f32")
+            and os.environ.get("DLI_GEMM_NO_BLAS", "0") != "1"
+            and os.environ.get("DLI_TUNE_PREFILL_BLAS", "1") == "1"
+            and out[0].backend != "hipblaslt"):
+        out.append(GemmPlan("hipblaslt", 0, 1))
+    return out
 
 
 def candidate_plans(M: int, N: int, K: int, epi: str):

@@ -138,6 +138,31 @@ def test_gemv_skinny(gpu, M, N, K, epi):
         G.clear_plans()
 
 
+def test_prefill_autotune_pins_a_correct_plan(gpu):
+    """StageRunner.autotune_prefill's measurement (ops.gemm.autotune over prefill_candidates:
+    our 8-phase kernel vs hipBLASLt) pins one plan per shape, and whichever it pins computes
+    each consumer (plain, SiLU*up, add + RMSNorm) like the fp32 reference."""
+    torch.manual_seed(14)
+    G.clear_plans()
+    M, K = 2048, 1024
+    w_gu, w_o = rnd(2048, K, dev=gpu, scale=0.05), rnd(1024, K, dev=gpu, scale=0.05)
+    shapes = [(M, 2048, K, "silu_mul"), (M, 1024, K, "splitk")]
+    got = G.autotune(shapes, {(2048, K): w_gu, (1024, K): w_o}, gpu, iters=2, cold_bytes=1,
+                     candidates=G.prefill_candidates)
+    assert set(got) == set(shapes)
+    for (m, n, k, epi), (p, ms) in got.items():
+        assert ms > 0 and G.plan(m, n, k, epi) == p
+        assert p in G.prefill_candidates(m, n, k, epi)
+    x = rnd(M, K, dev=gpu)
+    close(ops.linear(x, w_gu, epi="silu_mul"), R.silu_mul(R.linear(x, w_gu).float().to(BF)))
+    r0, nw = rnd(M, 1024, dev=gpu), rnd(1024, dev=gpu)
+    ref_out, ref_res = R.fused_add_rmsnorm(R.linear(x, w_o), r0, nw, 1e-5)
+    res = r0.clone()
+    close(ops.linear_add_rmsnorm(x, w_o, res, nw, 1e-5), ref_out, rtol=2e-2, atol=3e-2)
+    close(res, ref_res, rtol=1e-2, atol=2e-2)
+    G.clear_plans()
+
+
 def test_gemm_asymmetric_identity(gpu):
     """A = I with asymmetric B catches a transposed C write (cdna_hip_programming.md §3)."""
     n = 128

@@ -274,6 +274,15 @@ def test_prefill_gemm_plan_is_own_kernel(monkeypatch):
     assert G.plan(16384, 6144, 4096, "none").backend == "hipblaslt"
     assert G.plan(16384, 28672, 4096, "silu_mul").backend == "dli"
     G.clear_plans()
+    monkeypatch.delenv("DLI_GEMM_PREFILL_BLAS")
+    # prefill autotune (StageRunner.autotune_prefill): our 8-phase plan vs hipBLASLt
+    c = G.prefill_candidates(16384, 28672, 4096, "silu_mul")
+    assert c[0] == G.GemmPlan("dli", 22, 1) and c[1].backend == "hipblaslt"
+    assert [p.backend for p in G.prefill_candidates(2048, 4096, 4096, "splitk")] == \
+        ["dli", "hipblaslt"]
+    assert [p.backend for p in G.prefill_candidates(4096, 4096, 4096, "bias_gelu")] == ["dli"]
+    monkeypatch.setenv("DLI_GEMM_NO_BLAS", "1")
+    assert [p.backend for p in G.prefill_candidates(16384, 6144, 4096, "none")] == ["dli"]
 
 
 def test_slice_experts_releases_other_experts():
