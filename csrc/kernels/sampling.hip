@@ -150,10 +150,76 @@ __device__ __forceinline__ void row_scan(const float* __restrict__ x, int V, F&&
   for (int j = done + tid; j < V; j += nt) f(x[j], j);
 }
 
+// ---------------------------------------------------------------------------------------
+// Small batches (B <= SMP_SPLIT_MAX_B): one workgroup per row leaves ~255 CUs idle while it
+// walks a 128k-entry row several times (~45 us at batch 1, profiles/r3/b1_p). Two phases
+// instead: sample_chunk_kernel splits each row into P chunks (P workgroups per row); a chunk
+// keeps every logit >= its own Keff-th largest (radix select in LDS), in index order, in a
+// CAPC-slot candidate list (pads: -inf). The row's top-Keff is contained in the union of the
+// chunks' lists, which keep index order, so sample_kernel then runs its unchanged algorithm
+// over the P*CAPC candidates (ties still break on the lower vocab index) and maps the pick
+// back to a vocab id. Rows whose Keff exceeds CAPC, plain-temperature rows and rows where a
+// chunk had more than CAPC ties at its threshold (overflow flag) read the full row as before.
+#define SMP_CAPC 64
+#define SMP_CHUNK_MAX 4096
+#define SMP_SPLIT_MAX_B 8
+
+__device__ __forceinline__ bool smp_split_ok(float T, int K, float P) {
+  const bool greedy = T <= 0.f || K == 1;
+  return greedy || (K >= 1 && K <= SMP_CAPC);      // K <= 0 means 'no top-k': whole row
+}
+
+__global__ void __launch_bounds__(256) sample_chunk_kernel(
+    float* __restrict__ cand_v, int* __restrict__ cand_i, int* __restrict__ overflow,
+    const float* __restrict__ logits, long row_stride, int V, int L,
+    const float* __restrict__ temperature, const int* __restrict__ top_k,
+    const float* __restrict__ top_p) {
+  __shared__ uint32_t keys[SMP_CHUNK_MAX];
+  __shared__ uint32_t hist[256];
+  __shared__ float tmp[16];
+  __shared__ uint32_t sel[3];
+  const int row = blockIdx.y, c = blockIdx.x, tid = threadIdx.x, P = gridDim.x;
+  const float T = temperature[row];
+  const int K = top_k[row];
+  if (!smp_split_ok(T, K, top_p[row])) return;        // sample_kernel reads the full row
+  const int keff = (T <= 0.f || K == 1) ? 1 : K;
+  const int lo = c * L, n = max(0, min(V, lo + L) - lo);
+  const float* x = logits + (long)row * row_stride + lo;
+  for (int e = tid; e < n; e += 256) keys[e] = f2key(x[e]);
+  __syncthreads();
+  // the chunk's keff-th largest key (0: fewer than keff entries -> keep them all)
+  const uint32_t tau = n > 0 ? radix_kth(keys, n, (uint32_t)min(keff, n), hist, tmp, sel) : 0u;
+  // ordered compaction: thread t owns a contiguous slice, a block scan of the counts gives
+  // each survivor its slot
+  const int per = (n + 255) / 256, b0 = min(n, tid * per), b1 = min(n, b0 + per);
+  int cnt = 0;
+  for (int e = b0; e < b1; ++e) cnt += keys[e] >= tau && keys[e] != 0u;
+  const int incl = (int)block_scan((float)cnt, tmp);   // exact: counts < 2^24
+  int pos = incl - cnt;
+  const long base = ((long)row * P + c) * SMP_CAPC;
+  for (int e = b0; e < b1; ++e)
+    if (keys[e] >= tau && keys[e] != 0u) {
+      if (pos < SMP_CAPC) { cand_v[base + pos] = key2f(keys[e]); cand_i[base + pos] = lo + e; }
+      ++pos;
+    }
+  __shared__ int s_total;
+  if (tid == 255) s_total = incl;
+  __syncthreads();
+  if (s_total > SMP_CAPC) {
+    if (tid == 0) overflow[row] = 1;                   // the row falls back to the full scan
+  }
+  for (int e = s_total + tid; e < SMP_CAPC; e += 256) {
+    cand_v[base + e] = -INFINITY;
+    cand_i[base + e] = 0;
+  }
+}
+
 __global__ void __launch_bounds__(SMP_THREADS) sample_kernel(
     int* __restrict__ out_tokens, const float* __restrict__ logits, long row_stride, int V,
     const float* __restrict__ temperature, const int* __restrict__ top_k,
-    const float* __restrict__ top_p, const long long* __restrict__ seeds) {
+    const float* __restrict__ top_p, const long long* __restrict__ seeds,
+    const float* __restrict__ cand_v, const int* __restrict__ cand_i,
+    int* __restrict__ overflow, int ncand) {
   __shared__ uint32_t hist[256];
   __shared__ uint32_t ckey[2 * SMP_CAP];      // fast path: 512 threads x top-8 candidates
   __shared__ int cidx[2 * SMP_CAP];
@@ -170,12 +236,25 @@ __global__ void __launch_bounds__(SMP_THREADS) sample_kernel(
   const float P = top_p[row];
   const unsigned long long sd = (unsigned long long)seeds[row];
   const uint2 key = make_uint2((uint32_t)sd, (uint32_t)(sd >> 32));
+  // two-phase small-batch mode: read the row's candidate list unless a chunk overflowed
+  const int Vfull = V;
+  const int* map = nullptr;
+  if (cand_v != nullptr && smp_split_ok(T, K, P)) {
+    if (overflow[row] == 0) {
+      x = cand_v + (long)row * ncand;
+      map = cand_i + (long)row * ncand;
+      V = ncand;
+    }
+    __syncthreads();                                          // every thread read the flag
+    if (tid == 0) overflow[row] = 0;                          // zero for the next call
+  }
+  auto vocab_id = [&](int j) { return map != nullptr ? map[j] : j; };
 
   if (T <= 0.f || K == 1) {                                  // greedy
     ArgMax a{-INFINITY, 0x7fffffff};
     row_scan(x, V, [&](float v, int i) { a = amax(a, ArgMax{v, i}); });
     a = block_argmax(a, sv, si);
-    if (tid == 0) out_tokens[row] = a.i < V ? a.i : 0;
+    if (tid == 0) out_tokens[row] = a.i < V ? vocab_id(a.i) : 0;
     return;
   }
   const float invT = 1.f / T;
@@ -198,7 +277,7 @@ __global__ void __launch_bounds__(SMP_THREADS) sample_kernel(
     return;
   }
   int Keff = (K <= 0 || K > SMP_CAP) ? SMP_CAP : K;
-  if (Keff > V) Keff = V;
+  if (Keff > Vfull) Keff = Vfull;
 
   int n = 0;
   bool fast_ok = false;
@@ -356,15 +435,42 @@ __global__ void __launch_bounds__(SMP_THREADS) sample_kernel(
   for (int e = tid; e < c - 1; e += blockDim.x)
     if (cprob[e] > u) atomicMin(&s_cnt, (uint32_t)e);
   __syncthreads();
-  if (tid == 0) out_tokens[row] = cidx[s_cnt];
+  if (tid == 0) out_tokens[row] = vocab_id(cidx[s_cnt]);
 }
 
+// Bytes of the two-phase workspace dli_sample takes for a batch of B rows (0: one phase).
+extern "C" long dli_sample_workspace_bytes(int B, int V) {
+  if (B <= 0 || B > SMP_SPLIT_MAX_B) return 0;
+  return (long)SMP_SPLIT_MAX_B * 4 + (long)B * 64 * SMP_CAPC * 8;
+}
+
+// ws: nullable; when given (>= dli_sample_workspace_bytes, its first SMP_SPLIT_MAX_B ints
+// zero before the first call — the kernels leave them zero), batches of B <= 8 rows sample in
+// two phases (above).
 extern "C" int dli_sample(int* out_tokens, const float* logits, long row_stride, int B, int V,
                           const float* temperature, const int* top_k, const float* top_p,
-                          const long long* seeds, hipStream_t st) {
+                          const long long* seeds, void* ws, hipStream_t st) {
   if (B <= 0) return 0;
+  if (ws != nullptr && B <= SMP_SPLIT_MAX_B) {
+    // P chunks per row: >= 256 workgroups in all, each chunk <= SMP_CHUNK_MAX entries
+    int P = 1;
+    while (P < 64 && (B * P < 256 || (V + P - 1) / P > SMP_CHUNK_MAX)) P <<= 1;
+    const int L = (((V + P - 1) / P) + 3) & ~3;
+    if (L <= SMP_CHUNK_MAX) {
+      int* overflow = static_cast<int*>(ws);
+      float* cand_v = reinterpret_cast<float*>(overflow + SMP_SPLIT_MAX_B);
+      int* cand_i = reinterpret_cast<int*>(cand_v + (long)B * 64 * SMP_CAPC);
+      sample_chunk_kernel<<<dim3(P, B), 256, 0, st>>>(cand_v, cand_i, overflow, logits,
+                                                       row_stride, V, L, temperature, top_k,
+                                                       top_p);
+      sample_kernel<<<B, SMP_THREADS, 0, st>>>(out_tokens, logits, row_stride, V, temperature,
+                                               top_k, top_p, seeds, cand_v, cand_i, overflow,
+                                               P * SMP_CAPC);
+      DLI_RETURN_LAUNCH();
+    }
+  }
   sample_kernel<<<B, SMP_THREADS, 0, st>>>(out_tokens, logits, row_stride, V, temperature, top_k,
-                                           top_p, seeds);
+                                           top_p, seeds, nullptr, nullptr, nullptr, 0);
   DLI_RETURN_LAUNCH();
 }
 

@@ -419,6 +419,27 @@ def decode_attention(qkv, k_cache, v_cache, block_tables, context_lens, max_cont
 
 
 # ----------------------------------------------------------------------------- sampling
+_SAMPLE_SPLIT = __import__("os").environ.get("DLI_SAMPLE_SPLIT", "1") == "1"   # A/B switch
+_sample_wss: dict = {}
+
+
+def _sample_ws(device, B: int, V: int):
+    """Zero-initialised scratch of the two-phase small-batch sampler (sampling.hip
+    sample_chunk_kernel: B <= 8 rows split over up to 64 workgroups each), or None. One buffer
+    per device, sized for the largest batch; the kernels leave its overflow flags zero."""
+    if not _SAMPLE_SPLIT:
+        return None
+    lib = N.require_native()
+    if int(lib.dli_sample_workspace_bytes(B, V)) == 0:
+        return None
+    key = (device.type, device.index)
+    ws = _sample_wss.get(key)
+    if ws is None:
+        nbytes = int(lib.dli_sample_workspace_bytes(8, V))
+        ws = _sample_wss[key] = torch.zeros(nbytes, dtype=torch.uint8, device=device)
+    return ws
+
+
 def sample(logits, temperature, top_k, top_p, seeds, generator=None, ids=None):
     """logits fp32 [B, V] -> int32 tokens [B]. temperature<=0 -> greedy. With ``ids``
     [B, V] the row holds candidates (vocab-parallel LM head) in ascending token-id order,
@@ -430,7 +451,7 @@ def sample(logits, temperature, top_k, top_p, seeds, generator=None, ids=None):
     B, V = logits.shape
     out = torch.empty(B, dtype=torch.int32, device=logits.device)
     _native_call("dli_sample", _p(out), _p(logits), logits.stride(0), B, V, _p(temperature),
-                 _p(top_k), _p(top_p), _p(seeds), _st())
+                 _p(top_k), _p(top_p), _p(seeds), _p(_sample_ws(logits.device, B, V)), _st())
     if ids is not None:
         out = ids.gather(1, out.long().unsqueeze(1)).squeeze(1).to(torch.int32)
     return out

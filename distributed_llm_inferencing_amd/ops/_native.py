@@ -47,7 +47,8 @@ _SIGS = {
     "dli_decode_get_pipe": [],
     "dli_gemm_set_slab_store": [I],
     "dli_prefill_attention_paged": [P, I, P, I, P, P, P, P, P, I, I, I, I, I, I, I, F, P],
-    "dli_sample": [P, P, L, I, I, P, P, P, P, P],
+    "dli_sample": [P, P, L, I, I, P, P, P, P, P, P],
+    "dli_sample_workspace_bytes": [I, I],
     "dli_topk_rows": [P, P, P, L, I, I, I, I, P],
     "dli_gemm": [P, I, P, I, P, I, I, I, I, I, I, I, P, P, P, I, P],
     "dli_splitk_add_rmsnorm": [P, P, P, I, I, I, P, F, P],

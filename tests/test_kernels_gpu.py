@@ -495,6 +495,40 @@ def test_sampling_fallback_path_adversarial(gpu):
         assert (tok % 512 == 0).all()
 
 
+@pytest.mark.parametrize("B,V", [(1, 128256), (3, 50257), (8, 128256), (2, 1000)])
+def test_sampling_two_phase_matches_one_phase(gpu, B, V):
+    """Small batches sample in two phases (per-chunk candidate lists, sampling.hip
+    sample_chunk_kernel): the same tokens as the one-workgroup-per-row kernel for every
+    parameter mix — greedy, top-k 1 / 50 / 64 with top-p, top-k 100 and top-k 0 (full-row
+    paths) — and for rows whose chunks overflow their candidate slots (a tie-heavy row)."""
+    torch.manual_seed(15)
+    logits = torch.randn(B, V, device=gpu) * 3
+    if B >= 2:                                 # 300 ties above everything else in one
+        logits[1, V // 3:V // 3 + 300] = 30.0  # chunk: it overflows -> full-row path (a
+        # whole row of ties is not used: the one-phase kernel keeps an arbitrary 2048 of them)
+    lib = ops.N.require_native()
+    ws = ops._sample_ws(logits.device, B, V)
+    assert ws is not None
+    ones = torch.ones(B, device=gpu)
+    for T, K, P in [(0.0, 1, 1.0), (0.8, 1, 1.0), (0.8, 50, 0.95), (1.0, 64, 0.5),
+                    (0.7, 100, 0.9), (1.1, 0, 0.9), (0.9, 0, 1.0), (0.8, 5, 1.0)]:
+        temp = torch.full((B,), T, device=gpu)
+        topk = torch.full((B,), K, device=gpu, dtype=torch.int32)
+        topp = ones * P
+        for rep in range(3):
+            seeds = torch.arange(B, device=gpu, dtype=torch.int64) * 7919 + 31 * rep
+            one = torch.empty(B, dtype=torch.int32, device=gpu)
+            two = torch.empty(B, dtype=torch.int32, device=gpu)
+            for o, w in ((one, None), (two, ws)):
+                rc = lib.dli_sample(ops._p(o), ops._p(logits), logits.stride(0), B, V,
+                                    ops._p(temp), ops._p(topk), ops._p(topp), ops._p(seeds),
+                                    ops._p(w), ops._st())
+                assert rc == 0
+            assert torch.equal(one, two), (T, K, P, one, two)
+    torch.cuda.synchronize()
+    assert int(ws[:32].view(torch.int32).abs().sum()) == 0        # overflow flags reset
+
+
 @pytest.mark.parametrize("epi", ["none", "silu_mul"])
 def test_grouped_8phase_rows_bound(gpu, epi):
     """Grouped tile 22 with M = the largest group's rows (the MoE prefill launch) over groups
