@@ -18,6 +18,7 @@ up before hipGraph capture so no allocation happens inside a capture.
 """
 from __future__ import annotations
 
+import math
 import os
 import threading
 import time
@@ -305,6 +306,16 @@ def autotune(shapes, weights: dict, device, iters: int = 6, log=None,
             kc = torch.empty(-(-M // 16), hkv, 16, hd, dtype=w0.dtype, device=device)
             vc = torch.empty_like(kc)
             cs = R.rope_cos_sin(16, hd, 10000.0, device=device)
+            # decode-sized QKV: its consumer is the fused reduce + RoPE + KV write + attention
+            # kernel where the plan's split count allows it (ops.linear_rope_attention), else
+            # the RoPE/cache kernel + attention; time each plan with the path it will run
+            # (one-token contexts: the launch and dependency structure, not the KV stream)
+            decode_qkv = (M <= 512 and candidates is None
+                          and os.environ.get("DLI_TUNE_QKV_ATTN", "1") == "1")
+            if decode_qkv:
+                bt = (slots // 16).to(torch.int32).unsqueeze(1).contiguous()
+                ctx = torch.ones(M, dtype=torch.int32, device=device)
+                sc = 1.0 / math.sqrt(hd)
         best = None
         t_shape = time.perf_counter()
         for p in (candidates or candidate_plans)(M, N, K, epi):
@@ -313,7 +324,10 @@ def autotune(shapes, weights: dict, device, iters: int = 6, log=None,
 
             def run(p=p):
                 for w in ws_:
-                    if is_qkv:
+                    if is_qkv and decode_qkv:
+                        _qkv_decode(ops, x, w, p, pos, slots, cs, kc, vc, bt, ctx, hq, hkv,
+                                    hd, sc)
+                    elif is_qkv:
                         ops.linear_rope_cache(x, w, pos, slots, cs, kc, vc, hq, hkv, hd,
                                               plan=p)
                     elif epi == "splitk":
@@ -338,6 +352,41 @@ def autotune(shapes, weights: dict, device, iters: int = 6, log=None,
                 log(f"[gemm autotune] M={M} N={N} K={K} {epi}: {best[0]} {best[1]*1e3:.1f} us "
                     f"({time.perf_counter() - t_shape:.1f} s)")
     return out
+
+
+def _qkv_decode(ops, x, w, p, pos, slots, cs, kc, vc, bt, ctx, hq, hkv, hd, scale):
+    """One decode step's QKV projection + attention under plan ``p``, as the model runs it
+    (models/model.py ``_llama_layers``): the fused kernel when ``p`` allows it, else the
+    RoPE/cache kernel and the decode attention."""
+    with _forced_plan(x.shape[0], w.shape[0], x.shape[1], p):
+        out = ops.linear_rope_attention(x, w, pos, slots, cs, kc, vc, bt, ctx, 1, hq, hkv, hd,
+                                        scale)
+        if out is None:
+            qkv = ops.linear_rope_cache(x, w, pos, slots, cs, kc, vc, hq, hkv, hd, plan=p)
+            ops.decode_attention(qkv, kc, vc, bt, ctx, 1, hq, hkv, hd, scale)
+
+
+class _forced_plan:
+    """Pin the plan of one shape for the duration of a timing call (the fused attention path
+    reads its plan from the cache, not from an argument): the "splitk" entry, and for an
+    unsplit plan also the "none" entry its plain GEMM takes."""
+
+    def __init__(self, M, N, K, p):
+        b = _bucket(M)
+        self.keys = [(b, N, K, "splitk")] + ([(b, N, K, "none")] if p.splits == 1 else [])
+        self.p = p
+
+    def __enter__(self):
+        self.old = [_plan_cache.get(k) for k in self.keys]
+        for k in self.keys:
+            _plan_cache[k] = self.p
+
+    def __exit__(self, *exc):
+        for k, o in zip(self.keys, self.old):
+            if o is None:
+                _plan_cache.pop(k, None)
+            else:
+                _plan_cache[k] = o
 
 
 _tuned: set = set()

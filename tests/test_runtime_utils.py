@@ -283,6 +283,16 @@ def test_prefill_gemm_plan_is_own_kernel(monkeypatch):
     assert [p.backend for p in G.prefill_candidates(4096, 4096, 4096, "bias_gelu")] == ["dli"]
     monkeypatch.setenv("DLI_GEMM_NO_BLAS", "1")
     assert [p.backend for p in G.prefill_candidates(16384, 6144, 4096, "none")] == ["dli"]
+    # decode QKV timing pins the candidate for the fused attention path, then restores
+    p1, p4 = G.GemmPlan("dli", 30, 1), G.GemmPlan("dli", 32, 4)
+    G.set_plan(1, 6144, 4096, "none", p4)
+    with G._forced_plan(1, 6144, 4096, p1):
+        assert G.plan(1, 6144, 4096, "splitk") == p1 and G.plan(1, 6144, 4096, "none") == p1
+    assert G._plan_cache[(1, 6144, 4096, "none")] == p4
+    assert (1, 6144, 4096, "splitk") not in G._plan_cache
+    with G._forced_plan(1, 6144, 4096, p4):
+        assert G.plan(1, 6144, 4096, "splitk") == p4
+    G.clear_plans()
 
 
 def test_slice_experts_releases_other_experts():
