@@ -27,6 +27,8 @@ struct RcclApi {
   ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
   ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
   ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*comm_abort)(ncclComm_t) = nullptr;
+  ncclResult_t (*async_error)(ncclComm_t, ncclResult_t*) = nullptr;
   ncclResult_t (*send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) =
       nullptr;
   ncclResult_t (*recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
@@ -48,6 +50,9 @@ RcclApi* api() {
     a.get_unique_id = reinterpret_cast<decltype(a.get_unique_id)>(sym("ncclGetUniqueId"));
     a.comm_init_rank = reinterpret_cast<decltype(a.comm_init_rank)>(sym("ncclCommInitRank"));
     a.comm_destroy = reinterpret_cast<decltype(a.comm_destroy)>(sym("ncclCommDestroy"));
+    a.comm_abort = reinterpret_cast<decltype(a.comm_abort)>(sym("ncclCommAbort"));
+    a.async_error =
+        reinterpret_cast<decltype(a.async_error)>(sym("ncclCommGetAsyncError"));
     a.send = reinterpret_cast<decltype(a.send)>(sym("ncclSend"));
     a.recv = reinterpret_cast<decltype(a.recv)>(sym("ncclRecv"));
     a.group_start = reinterpret_cast<decltype(a.group_start)>(sym("ncclGroupStart"));
@@ -101,6 +106,28 @@ int dli_comm_destroy(void* comm) {
   auto* a = api();
   if (!a->ok || comm == nullptr) return 0;
   return rc(a->comm_destroy((ncclComm_t)comm));
+}
+
+// Failure handling ("RCCL async-error polling (ncclCommGetAsyncError) with
+// communicator abort + rebuild"). dli_comm_async_error: 0 healthy, else -(ncclResult_t) of
+// the communicator's asynchronous error (a peer died, a network / xGMI fault). The pipeline
+// watchdog polls it next to the stage liveness probe. dli_comm_abort: ncclCommAbort — frees
+// the communicator WITHOUT waiting for the peers and makes its kernels still queued on a
+// stream return, so a stage blocked on a dead neighbour drains; a new communicator is then
+// built for the re-formed ring.
+int dli_comm_async_error(void* comm) {
+  auto* a = api();
+  if (!a->ok || comm == nullptr || a->async_error == nullptr) return 0;
+  ncclResult_t e = ncclSuccess;
+  const int r = rc(a->async_error((ncclComm_t)comm, &e));
+  return r != 0 ? r : rc(e);
+}
+
+int dli_comm_abort(void* comm) {
+  auto* a = api();
+  if (!a->ok || comm == nullptr) return 0;
+  if (a->comm_abort == nullptr) return -100;
+  return rc(a->comm_abort((ncclComm_t)comm));
 }
 
 // One tick's exchange: n_send buffers to their peers and n_recv buffers from theirs, grouped

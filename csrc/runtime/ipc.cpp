@@ -8,15 +8,17 @@
 // work as binary semaphores: READY (in dst's flag page) and FREE (in src's page, initially
 // 1). A message goes
 //
-//   src stream: wait FREE == 1; FREE = 0; hipMemcpyAsync(mailbox <- payload); READY = 1
-//   dst stream: wait READY == 1; READY = 0; hipMemcpyAsync(target <- mailbox); FREE = 1
+//   src stream: wait FREE == 1; FREE = 0; put kernel (mailbox <- header + payload); READY = 1
+//   dst stream: wait READY == 1; READY = 0; get kernel (target <- payload, header checked); FREE = 1
 //
-// (waits = hipStreamWaitValue64 Eq, stores = hipStreamWriteValue64; the copy is an xGMI peer
-// write on an 8-GPU node, a local D2D copy when the ranks share one GPU). No sequence number
-// lives on the host, so an exchange captured in a hipGraph is correct on every replay, and
-// eager and captured exchanges interleave freely. The sender runs at most one message ahead
-// per edge, which the anti-diagonal pipeline schedule never needs to exceed: every wait
-// depends on a strictly earlier tick, so it cannot deadlock.
+// (waits = one-lane wait kernels with a wall-clock budget, signals = release-store kernels;
+// DLI_IPC_SYNC=stream uses hipStreamWaitValue64 / hipStreamWriteValue64 outside graph
+// capture instead, unbounded). The put kernel's stores are xGMI peer writes on an 8-GPU
+// node, local stores when the ranks share one GPU. No sequence number lives on the host, so
+// an exchange captured in a hipGraph is correct on every replay, and eager and captured
+// exchanges interleave freely. The sender runs at most one message ahead per edge, which the
+// anti-diagonal pipeline schedule never needs to exceed: every wait depends on a strictly
+// earlier tick, so it cannot deadlock.
 //
 // All of it is enqueued on the caller's stream (the stage's compute stream): the send is
 // ordered after the kernels that produced the payload and the receive before the kernels
@@ -28,6 +30,35 @@
 // shared-memory page registered with HIP ("host" flags): then the host can observe how far
 // every queue has got and ABORT a ring whose peer died by setting every flag it could be
 // waiting on (dli_ipc_abort), which a device-only wait could never be released from.
+//
+// Memory model across GPUs. A sender writes the peer's mailbox over xGMI; the receiver then
+// reads it from its own HBM. With ordinary (coarse-grained) allocations the receiver's L2
+// may still hold lines of the PREVIOUS message it read from the same mailbox (a peer's
+// remote write does not invalidate them, and a coarse-grained local line is not invalidated
+// at a kernel boundary), so mailboxes and flag pages are allocated UNCACHED
+// (hipExtMallocWithFlags hipDeviceMallocUncached, the kind RCCL uses for its own flags and
+// LL buffers): no XCD's L2 ever holds a copy, every load and store goes to memory. Flags are
+// written with system-scope release stores after the payload kernel and polled with
+// system-scope acquire loads. DLI_IPC_MEM = uncached (default) | fine | coarse selects the
+// allocation (coarse = the round-3 layout, for A/B only); the kind in use is reported by
+// dli_ipc_mem_kind.
+//
+// Every message carries a 16-byte header {sequence, bytes}. Each rank keeps a 64-bit
+// counter per edge and direction in its own device memory, advanced by the copy kernels
+// themselves (so a captured exchange advances it on every replay): the sender stamps
+// ++seq_out[peer], the receiver checks header.seq == ++seq_in[peer]. A stale mailbox (an old
+// message read again) or a lost / duplicated message sets bit 2 of the error word instead of
+// silently yielding wrong activations. (Sizes are not compared on the device: a captured
+// decode graph moves its padded bucket while the eager peer moves the live rows; the CPU
+// model of the protocol, parallel/fifo.py, does assert equal sizes of the unpadded schedule.)
+//
+// Error word: bit 0 = a bounded wait ran out of budget (a peer stopped signalling), bit 1 =
+// sequence / size mismatch, bit 2 = aborted. It lives twice: in pinned host memory (the host
+// polls it every pipeline tick with a plain load, no HIP call) and in the flag page (the
+// device mirror that wait and signal kernels test first). Once set the endpoint is
+// sticky-failed: every later wait returns at once and no signal is sent, so a broken ring
+// drains its queues in microseconds and the host fails the session (HTTP 503) instead of
+// serving tokens computed from stale data.
 //
 // C ABI (ctypes): 0 / >= 0 on success, negative hipError_t (or -1000 - reason) on failure.
 #include <fcntl.h>
@@ -47,13 +78,15 @@
 namespace {
 
 constexpr size_t kFlagStride = 16;   // words between flags (128 B: one flag per line)
+constexpr long long kHdr = 16;       // message header {sequence, bytes} in front of a payload
+enum : uint64_t { kErrWait = 1, kErrSeq = 2, kErrAbort = 4 };
 
 struct Edge {                        // one peer, both directions
   // outbound (me -> peer)
   uint8_t* peer_mailbox = nullptr;   // peer's mailbox for my messages (mapped)
   uint64_t* peer_ready = nullptr;    // peer's READY word for me (mapped)
   uint64_t* my_free = nullptr;       // my FREE word for this edge (peer sets it)
-  long long out_bytes = 0;           // mailbox capacity
+  long long out_bytes = 0;           // mailbox payload capacity
   // inbound (peer -> me)
   uint8_t* my_mailbox = nullptr;
   uint64_t* my_ready = nullptr;
@@ -61,34 +94,100 @@ struct Edge {                        // one peer, both directions
   long long in_bytes = 0;
 };
 
-// Payload copies: a plain vectorised copy kernel on the caller's stream (default) or
-// hipMemcpyAsync (DLI_IPC_COPY=memcpy). The kernel keeps a hop to one launch on the compute
-// queue; hipMemcpyAsync between IPC-mapped buffers may be routed to an SDMA engine, measured
-// at ~40 GB/s for 4 MB messages on one MI355X (profiles/r3/ipc_probe_*.jsonl).
-__global__ void __launch_bounds__(256) ipc_copy_kernel(uint4* __restrict__ dst,
-                                                       const uint4* __restrict__ src, long n16,
-                                                       uint32_t* __restrict__ dtail,
-                                                       const uint32_t* __restrict__ stail,
-                                                       int ntail) {
+// error bookkeeping shared by every kernel of an endpoint
+struct ErrRef {
+  uint64_t* dev;                     // device mirror (flag page): tested by wait / signal
+  uint64_t* host;                    // pinned host word (device address): polled by the host
+};
+
+__device__ __forceinline__ void raise_err(ErrRef e, uint64_t bit) {
+  __hip_atomic_fetch_or(e.dev, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_fetch_or(e.host, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Sender: payload -> peer mailbox (after the header), header {++seq, bytes}. A plain
+// vectorised copy on the caller's stream keeps a hop to one launch on the compute queue
+// (hipMemcpyAsync between IPC-mapped buffers may be routed to an SDMA engine, measured at
+// ~40 GB/s for 4 MB messages on one MI355X: profiles/r3/ipc_probe_*.jsonl).
+__global__ void __launch_bounds__(256) ipc_put_kernel(uint8_t* __restrict__ mbox,
+                                                      const uint8_t* __restrict__ src,
+                                                      long long bytes, int vec,
+                                                      uint64_t* __restrict__ seq_out,
+                                                      ErrRef err) {
+  // a failed / aborted endpoint writes nothing more into a peer's memory (the peer may be
+  // gone): one load of the error mirror, uniform over the grid
+  if (__hip_atomic_load(err.dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0ull) return;
   const long stride = (long)gridDim.x * blockDim.x;
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  for (; i + 3 * stride < n16; i += 4 * stride) {
-    const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride],
-                d = src[i + 3 * stride];
-    dst[i] = a;
-    dst[i + stride] = b;
-    dst[i + 2 * stride] = c;
-    dst[i + 3 * stride] = d;
+  if (i == 0) {
+    const uint64_t s = *seq_out + 1;
+    *seq_out = s;
+    reinterpret_cast<uint64_t*>(mbox)[0] = s;
+    reinterpret_cast<uint64_t*>(mbox)[1] = (uint64_t)bytes;
   }
-  for (; i < n16; i += stride) dst[i] = src[i];
-  if (blockIdx.x == 0 && (int)threadIdx.x < ntail) dtail[threadIdx.x] = stail[threadIdx.x];
+  if (vec) {                       // 16-B aligned source: uint4 copy, 4 loads in flight
+    const uint4* s4 = reinterpret_cast<const uint4*>(src);
+    uint4* d4 = reinterpret_cast<uint4*>(mbox + kHdr);
+    const long n16 = bytes / 16;
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+      const uint4 a = s4[i], b = s4[i + stride], c = s4[i + 2 * stride], d = s4[i + 3 * stride];
+      d4[i] = a;
+      d4[i + stride] = b;
+      d4[i + 2 * stride] = c;
+      d4[i + 3 * stride] = d;
+    }
+    for (; i < n16; i += stride) d4[i] = s4[i];
+    i = n16 * 4 + (long)blockIdx.x * blockDim.x + threadIdx.x;   // the 4-B tail
+  }
+  const uint32_t* s1 = reinterpret_cast<const uint32_t*>(src);
+  uint32_t* d1 = reinterpret_cast<uint32_t*>(mbox + kHdr);
+  for (const long n4 = bytes / 4; i < n4; i += stride) d1[i] = s1[i];
+}
+
+// Receiver: mailbox payload -> target, the header's sequence number checked against
+// ++seq_in. Sizes may legitimately differ by bucket padding (a stage's captured decode graph
+// receives / sends its whole padded bucket while the eager side moves the live rows), so the
+// copy takes min(sent, expected) bytes: padding rows keep stale values, which nothing reads.
+__global__ void __launch_bounds__(256) ipc_get_kernel(uint8_t* __restrict__ dst,
+                                                      const uint8_t* __restrict__ mbox,
+                                                      long long bytes, int vec,
+                                                      uint64_t* __restrict__ seq_in, ErrRef err) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t* h = reinterpret_cast<const uint64_t*>(mbox);
+  if (i == 0) {
+    const uint64_t s = *seq_in + 1;
+    *seq_in = s;
+    if (h[0] != s) raise_err(err, kErrSeq);
+  }
+  const long long sent = (long long)h[1];
+  bytes = sent < bytes ? sent : bytes;
+  if (vec) {
+    const uint4* s4 = reinterpret_cast<const uint4*>(mbox + kHdr);
+    uint4* d4 = reinterpret_cast<uint4*>(dst);
+    const long n16 = bytes / 16;
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+      const uint4 a = s4[i], b = s4[i + stride], c = s4[i + 2 * stride], d = s4[i + 3 * stride];
+      d4[i] = a;
+      d4[i + stride] = b;
+      d4[i + 2 * stride] = c;
+      d4[i + 3 * stride] = d;
+    }
+    for (; i < n16; i += stride) d4[i] = s4[i];
+    i = n16 * 4 + (long)blockIdx.x * blockDim.x + threadIdx.x;
+  }
+  const uint32_t* s1 = reinterpret_cast<const uint32_t*>(mbox + kHdr);
+  uint32_t* d1 = reinterpret_cast<uint32_t*>(dst);
+  for (const long n4 = bytes / 4; i < n4; i += stride) d1[i] = s1[i];
 }
 
 // ---- expert-parallel all-to-all on the mailboxes: row counts live on the device -------
-// A dispatch message on edge s -> p is [int64 count | 16-B pad | ids int32 x cap | rows x
-// row_bytes] (return messages use the same offsets, no ids). Only `count` rows move; the
-// grid is sized for the mailbox capacity and threads past the count exit, so no routing
-// value is ever read on the host and the whole exchange can be captured in a graph.
+// A dispatch message on edge s -> p is [int64 count | uint64 sequence | ids int32 x cap |
+// rows x row_bytes] (return messages use the same offsets, no ids). Only `count` rows move;
+// the grid is sized for the mailbox capacity and threads past the count exit, so no routing
+// value is ever read on the host and the whole exchange can be captured in a graph. The
+// receiver clamps the count to the region it reserved for the source (recv_cap): rows past
+// it are dropped and flagged (kErrSeq), never written past the region.
 __device__ __forceinline__ long ep_ids_off() { return 16; }
 __device__ __forceinline__ long ep_rows_off(int cap) {
   return 16 + (((long)cap * 4 + 15) / 16) * 16;
@@ -97,9 +196,17 @@ __device__ __forceinline__ long ep_rows_off(int cap) {
 __global__ void __launch_bounds__(256) ep_put_kernel(uint8_t* __restrict__ mbox, int cap,
                                                      const int* __restrict__ count,
                                                      const uint4* __restrict__ x, int row16,
-                                                     const int* __restrict__ ids) {
+                                                     const int* __restrict__ ids,
+                                                     uint64_t* __restrict__ seq_out,
+                                                     ErrRef err) {
+  if (__hip_atomic_load(err.dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0ull) return;
   const int n = min(*count, cap);
-  if (blockIdx.x == 0 && threadIdx.x == 0) *reinterpret_cast<long long*>(mbox) = n;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const uint64_t s = *seq_out + 1;
+    *seq_out = s;
+    reinterpret_cast<long long*>(mbox)[0] = n;
+    reinterpret_cast<uint64_t*>(mbox)[1] = s;
+  }
   int* mid = reinterpret_cast<int*>(mbox + ep_ids_off());
   uint4* mrow = reinterpret_cast<uint4*>(mbox + ep_rows_off(cap));
   const long stride = (long)gridDim.x * blockDim.x;
@@ -113,27 +220,36 @@ __global__ void __launch_bounds__(256) ep_put_kernel(uint8_t* __restrict__ mbox,
 __global__ void __launch_bounds__(256) ep_get_kernel(const uint8_t* __restrict__ mbox, int cap,
                                                      uint4* __restrict__ x, int row16,
                                                      int* __restrict__ ids, int fill,
-                                                     int* __restrict__ count_out) {
-  const int n = (int)min(*reinterpret_cast<const long long*>(mbox), (long long)cap);
+                                                     int maxn, int* __restrict__ count_out,
+                                                     uint64_t* __restrict__ seq_in, ErrRef err) {
+  const long long hn = *reinterpret_cast<const long long*>(mbox);
+  const int n = (int)min(min(hn, (long long)cap), (long long)maxn);
   const int* mid = reinterpret_cast<const int*>(mbox + ep_ids_off());
   const uint4* mrow = reinterpret_cast<const uint4*>(mbox + ep_rows_off(cap));
   const long stride = (long)gridDim.x * blockDim.x;
   const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (count_out != nullptr && tid == 0) *count_out = n;
+  if (tid == 0) {
+    const uint64_t s = *seq_in + 1;
+    *seq_in = s;
+    if (reinterpret_cast<const uint64_t*>(mbox)[1] != s || hn > maxn || hn < 0)
+      raise_err(err, kErrSeq);
+    if (count_out != nullptr) *count_out = n;
+  }
   if (ids != nullptr)
     for (long i = tid; i < fill; i += stride) ids[i] = i < n ? mid[i] : -1;
   const long total = (long)n * row16;
   for (long i = tid; i < total; i += stride) x[i] = mrow[i];
 }
 
-// the rank's own bucket: send region -> receive region (ids -1 past the count)
+// the rank's own bucket: send region -> receive region (ids -1 past the count), at most
+// maxn rows (the destination region)
 __global__ void __launch_bounds__(256) ep_local_kernel(const int* __restrict__ count,
                                                        const uint4* __restrict__ xs, int row16,
                                                        const int* __restrict__ ids_s,
                                                        uint4* __restrict__ xd,
                                                        int* __restrict__ ids_d, int fill,
-                                                       int* __restrict__ count_out) {
-  const int n = *count;
+                                                       int maxn, int* __restrict__ count_out) {
+  const int n = min(*count, maxn);
   const long stride = (long)gridDim.x * blockDim.x;
   const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (count_out != nullptr && tid == 0) *count_out = n;
@@ -143,43 +259,56 @@ __global__ void __launch_bounds__(256) ep_local_kernel(const int* __restrict__ c
   for (long i = tid; i < total; i += stride) xd[i] = xs[i];
 }
 
-// Semaphore waits / signals as kernels, used while a stream is being captured into a
-// hipGraph (stream write/wait-value operations captured into a graph were measured to lose
-// their ordering against the copy kernels on replay: profiles/r3/ipc_probe_*.jsonl, check
-// "graph"). One lane polls with acquire loads and a bounded wall-clock budget, so every wave
-// finishes even if the peer never signals (then *err is set and the caller's host sees it).
-__global__ void ipc_wait_kernel(uint64_t* flag, uint64_t* err, unsigned long long budget) {
+// Semaphore waits / signals as kernels: the default (bounded waits), and always while a
+// stream is being captured into a hipGraph (stream write/wait-value operations captured
+// into a graph were measured to lose their ordering against the copy kernels on replay:
+// profiles/r3/ipc_probe_*.jsonl, check "graph"). One lane polls the flag and the error
+// mirror with system-scope acquire loads and a wall-clock budget. A wait that runs out of
+// budget raises kErrWait and leaves the flag alone; once the error word is set every later
+// wait returns at once and no signal is sent (sticky failure: the queue drains).
+__global__ void ipc_wait_kernel(uint64_t* flag, ErrRef err, unsigned long long budget) {
   if (threadIdx.x != 0) return;
   const unsigned long long t0 = wall_clock64();
-  while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != 1ull) {
+  while (true) {
+    if (__hip_atomic_load(err.dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0ull) return;
+    if (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == 1ull) break;
     __builtin_amdgcn_s_sleep(4);
     if (wall_clock64() - t0 > budget) {
-      __hip_atomic_store(err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      break;
+      raise_err(err, kErrWait);
+      return;
     }
   }
   __hip_atomic_store(flag, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ void ipc_signal_kernel(uint64_t* flag) {
-  if (threadIdx.x == 0) __hip_atomic_store(flag, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+__global__ void ipc_signal_kernel(uint64_t* flag, ErrRef err) {
+  if (threadIdx.x != 0) return;
+  if (__hip_atomic_load(err.dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0ull) return;
+  __hip_atomic_store(flag, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+
+__global__ void ipc_bump_kernel(uint64_t* ctr, uint64_t d) { if (threadIdx.x == 0) *ctr += d; }
+
+enum MemKind { kCoarse = 0, kFine = 1, kUncached = 2 };
 
 struct Endpoint {
   int world = 0, rank = 0;
-  int sync_mode = 0;                  // 0: stream ops, graph capture -> kernels; 1: kernels
+  int sync_mode = 1;                  // 1: wait / signal kernels (bounded); 0: stream ops
   unsigned long long wait_budget = 0; // wall-clock ticks a wait kernel polls at most
-  uint64_t* err_word = nullptr;       // set by a wait kernel that ran out of budget
+  long long khz = 100000;             // wall clock rate
+  ErrRef err{nullptr, nullptr};       // device addresses of the two error words
+  uint64_t* err_host = nullptr;       // pinned host error word (host address)
+  uint64_t* seq = nullptr;            // device: seq_out[world], seq_in[world]
   bool host_flags = false;
-  bool copy_kernel = true;
+  int mem_kind = kUncached;
   hipStream_t abort_stream = nullptr; // device-flag abort: its own (SDMA) queue
-  uint64_t* abort_src = nullptr;      // pinned page of FREE/READY = 1 patterns
+  uint64_t* abort_src = nullptr;      // pinned page of FREE/READY = 1 patterns + error bit
   uint8_t* mailbox = nullptr;        // local, all inbound edges
   size_t mailbox_bytes = 0;
   uint64_t* flags = nullptr;         // local flag page (device or registered host memory)
   uint64_t* flags_dev = nullptr;     // its device address
   size_t flag_bytes = 0;
-  std::vector<long long> cap;        // mailbox bytes per edge [src * world + dst]
+  std::vector<long long> cap;        // mailbox payload bytes per edge [src * world + dst]
   std::vector<Edge> edge;
   std::vector<void*> opened;         // mapped peer allocations (device flags / mailboxes)
   std::vector<uint64_t*> host_pages; // host flag mode: every rank's page, mapped here
@@ -190,15 +319,44 @@ struct Endpoint {
 inline Endpoint* E(void* h) { return reinterpret_cast<Endpoint*>(h); }
 inline int herr(hipError_t e) { return e == hipSuccess ? 0 : -(int)e; }
 
-// flag page of rank r: READY[src] for every src, then FREE[dst] for every dst
+// flag page of rank r: READY[src] for every src, then FREE[dst] for every dst, then the
+// device error mirror
 inline size_t ready_word(int src) { return (size_t)src * kFlagStride; }
 inline size_t free_word(const Endpoint* e, int dst) {
   return ((size_t)e->world + dst) * kFlagStride;
 }
+inline size_t err_word(const Endpoint* e) { return 2 * (size_t)e->world * kFlagStride; }
+inline long long slot_bytes(long long cap) { return cap > 0 ? kHdr + ((cap + 15) / 16) * 16 : 0; }
 inline size_t mailbox_off(const Endpoint* e, int dst, int src) {
   size_t off = 0;
-  for (int s = 0; s < src; ++s) off += (size_t)e->cap[s * e->world + dst];
+  for (int s = 0; s < src; ++s) off += (size_t)slot_bytes(e->cap[s * e->world + dst]);
   return off;
+}
+
+// Shared device memory of the requested kind that can be exported with hipIpcGetMemHandle;
+// falls back towards coarse-grained (the kind actually used is returned in *kind).
+hipError_t alloc_shared(void** p, size_t bytes, int* kind) {
+  const char* m = getenv("DLI_IPC_MEM");
+  int want = kUncached;
+  if (m != nullptr && std::string(m) == "fine") want = kFine;
+  if (m != nullptr && std::string(m) == "coarse") want = kCoarse;
+  for (int k = want; k >= kCoarse; --k) {
+    hipError_t r;
+    if (k == kUncached) r = hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached);
+    else if (k == kFine) r = hipExtMallocWithFlags(p, bytes, hipDeviceMallocFinegrained);
+    else r = hipMalloc(p, bytes);
+    if (r != hipSuccess) { (void)hipGetLastError(); continue; }
+    hipIpcMemHandle_t h;
+    if (hipIpcGetMemHandle(&h, *p) != hipSuccess) {   // not exportable: next kind
+      (void)hipGetLastError();
+      (void)hipFree(*p);
+      *p = nullptr;
+      continue;
+    }
+    *kind = k;
+    return hipSuccess;
+  }
+  return hipErrorOutOfMemory;
 }
 
 std::string page_name(const std::string& prefix, int r) {
@@ -232,20 +390,31 @@ void set_word(uint64_t* w, uint64_t v) {
   reinterpret_cast<std::atomic<uint64_t>*>(w)->store(v, std::memory_order_release);
 }
 
-int copy_async(const Endpoint* e, void* dst, const void* src, long long bytes, hipStream_t s) {
-  if (bytes <= 0) return 0;
-  if (!e->copy_kernel || ((uintptr_t)dst | (uintptr_t)src | (uintptr_t)bytes) % 4)
-    return herr(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToDevice, s));
-  const long n16 = bytes / 16;
-  const int ntail = (int)((bytes % 16) / 4);
-  long blocks = (n16 + 4 * 256 - 1) / (4 * 256);
-  if (blocks < 1) blocks = 1;
-  if (blocks > 2048) blocks = 2048;
-  ipc_copy_kernel<<<dim3((unsigned)blocks), dim3(256), 0, s>>>(
-      reinterpret_cast<uint4*>(dst), reinterpret_cast<const uint4*>(src), n16,
-      reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(dst) + n16 * 16),
-      reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(src) + n16 * 16), ntail);
-  return herr(hipGetLastError());
+unsigned blocks_for(long n16) {
+  long b = (n16 + 4 * 256 - 1) / (4 * 256);
+  return (unsigned)(b < 1 ? 1 : (b > 2048 ? 2048 : b));
+}
+
+bool capturing(hipStream_t s) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive;
+}
+
+// wait until *w == 1 then reset it (bounded kernel, or a stream op); signal *w = 1
+int wait_flag(Endpoint* e, hipStream_t s, uint64_t* w) {
+  if (e->sync_mode == 1 || capturing(s)) {
+    ipc_wait_kernel<<<1, 64, 0, s>>>(w, e->err, e->wait_budget);
+    return herr(hipGetLastError());
+  }
+  int r = herr(hipStreamWaitValue64(s, w, 1, hipStreamWaitValueEq));
+  return r ? r : herr(hipStreamWriteValue64(s, w, 0, 0));
+}
+int signal_flag(Endpoint* e, hipStream_t s, uint64_t* w) {
+  if (e->sync_mode == 1 || capturing(s)) {
+    ipc_signal_kernel<<<1, 64, 0, s>>>(w, e->err);
+    return herr(hipGetLastError());
+  }
+  return herr(hipStreamWriteValue64(s, w, 1, 0));
 }
 
 }  // namespace
@@ -255,8 +424,8 @@ extern "C" {
 int dli_ipc_handle_bytes() { return (int)sizeof(hipIpcMemHandle_t); }
 
 // Allocate this rank's inbound mailboxes and flag page. cap: world x world matrix of mailbox
-// bytes (row = src, col = dst; 0 = no edge), identical on every rank. host_prefix: shm page
-// name prefix (rank r's page is "<prefix>_<r>"), or "" for device flags.
+// payload bytes (row = src, col = dst; 0 = no edge), identical on every rank. host_prefix:
+// shm page name prefix (rank r's page is "<prefix>_<r>"), or "" for device flags.
 void* dli_ipc_create(int world, int rank, const long long* cap, const char* host_prefix) {
   if (world < 1 || rank < 0 || rank >= world) return nullptr;
   auto* e = new Endpoint();
@@ -265,17 +434,30 @@ void* dli_ipc_create(int world, int rank, const long long* cap, const char* host
   e->cap.assign(cap, cap + (size_t)world * world);
   e->edge.resize(world);
   e->host_flags = host_prefix != nullptr && host_prefix[0] != '\0';
-  const char* cm = getenv("DLI_IPC_COPY");
-  e->copy_kernel = !(cm != nullptr && std::string(cm) == "memcpy");
-  for (int s = 0; s < world; ++s) e->mailbox_bytes += (size_t)e->cap[s * world + rank];
-  if (e->mailbox_bytes && (hipMalloc(&e->mailbox, e->mailbox_bytes) != hipSuccess ||
-                           hipMemset(e->mailbox, 0, e->mailbox_bytes) != hipSuccess)) {
+  for (int s = 0; s < world; ++s) e->mailbox_bytes += (size_t)slot_bytes(e->cap[s * world + rank]);
+  auto fail = [&]() -> void* {
+    if (e->mailbox) (void)hipFree(e->mailbox);
+    if (e->seq) (void)hipFree(e->seq);
+    if (e->err_host) (void)hipHostFree(e->err_host);
     delete e;
     return nullptr;
-  }
+  };
+  if (e->mailbox_bytes &&
+      (alloc_shared(reinterpret_cast<void**>(&e->mailbox), e->mailbox_bytes, &e->mem_kind) !=
+           hipSuccess ||
+       hipMemset(e->mailbox, 0, e->mailbox_bytes) != hipSuccess))
+    return fail();
+  if (hipMalloc(reinterpret_cast<void**>(&e->seq), 2 * (size_t)world * 8) != hipSuccess ||
+      hipMemset(e->seq, 0, 2 * (size_t)world * 8) != hipSuccess)
+    return fail();
+  if (hipHostMalloc(reinterpret_cast<void**>(&e->err_host), 64,
+                    hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+    return fail();
+  std::memset(e->err_host, 0, 64);
+  e->err.host = dev_addr(e->err_host);
   e->flag_bytes = (((2 * (size_t)world + 1) * kFlagStride * 8 + 4095) / 4096) * 4096;
   const char* sm = getenv("DLI_IPC_SYNC");
-  e->sync_mode = (sm != nullptr && std::string(sm) == "kernel") ? 1 : 0;
+  e->sync_mode = (sm != nullptr && std::string(sm) == "stream") ? 0 : 1;
   {
     int khz = 0;
     int dev = 0;
@@ -283,11 +465,12 @@ void* dli_ipc_create(int world, int rank, const long long* cap, const char* host
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess ||
         khz <= 0)
       khz = 100000;
+    e->khz = khz;
     const char* bs = getenv("DLI_IPC_WAIT_S");
-    const double secs = bs ? atof(bs) : 120.0;
+    const double secs = bs ? atof(bs) : 20.0;
     e->wait_budget = (unsigned long long)(secs * 1000.0 * khz);
   }
-  // FREE words start at 1 (every mailbox empty), READY words at 0
+  // FREE words start at 1 (every mailbox empty), READY words and the error mirror at 0
   std::vector<uint64_t> init(e->flag_bytes / 8, 0);
   for (int d = 0; d < world; ++d) init[free_word(e, d)] = 1;
   if (e->host_flags) {
@@ -295,26 +478,19 @@ void* dli_ipc_create(int world, int rank, const long long* cap, const char* host
     const std::string name = page_name(e->shm_prefix, rank);
     shm_unlink(name.c_str());
     uint64_t* p = map_host_page(name, e->flag_bytes, true);
-    if (p == nullptr) {
-      (void)hipFree(e->mailbox);
-      delete e;
-      return nullptr;
-    }
+    if (p == nullptr) return fail();
     std::memcpy(p, init.data(), e->flag_bytes);
     e->flags = p;
     e->flags_dev = dev_addr(p);
-    e->err_word = e->flags_dev + 2 * (size_t)world * kFlagStride;
     e->host_pages.assign(world, nullptr);
     e->host_pages[rank] = p;
   } else {
-    if (hipMalloc(reinterpret_cast<void**>(&e->flags), e->flag_bytes) != hipSuccess ||
-        hipMemcpy(e->flags, init.data(), e->flag_bytes, hipMemcpyHostToDevice) != hipSuccess) {
-      (void)hipFree(e->mailbox);
-      delete e;
-      return nullptr;
-    }
+    int k = kCoarse;
+    if (alloc_shared(reinterpret_cast<void**>(&e->flags), e->flag_bytes, &k) != hipSuccess ||
+        hipMemcpy(e->flags, init.data(), e->flag_bytes, hipMemcpyHostToDevice) != hipSuccess)
+      return fail();
+    if (e->mailbox_bytes == 0) e->mem_kind = k;
     e->flags_dev = e->flags;
-    e->err_word = e->flags + 2 * (size_t)world * kFlagStride;
     if (hipStreamCreateWithFlags(&e->abort_stream, hipStreamNonBlocking) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void**>(&e->abort_src), e->flag_bytes,
                       hipHostMallocDefault) != hipSuccess) {
@@ -323,8 +499,10 @@ void* dli_ipc_create(int world, int rank, const long long* cap, const char* host
     } else {
       std::memset(e->abort_src, 0, e->flag_bytes);
       for (size_t i = 0; i < 2 * (size_t)world; ++i) e->abort_src[i * kFlagStride] = 1;
+      e->abort_src[err_word(e)] = kErrAbort;
     }
   }
+  e->err.dev = e->flags_dev + err_word(e);
   (void)hipDeviceSynchronize();
   return e;
 }
@@ -407,7 +585,7 @@ int dli_ipc_connect(void* h, const void* handles) {
 
 // One exchange, enqueued on `stream`: every send, then every receive (see the protocol at
 // the top). A message larger than its edge's mailbox is refused (-1003) before anything is
-// enqueued; a zero-byte message still hands the mailbox over once.
+// enqueued; a zero-byte message still hands the mailbox over once (header only).
 int dli_ipc_exchange(void* h, void* stream, int n_send, void* const* send_ptrs,
                      const long long* send_bytes, const int* send_peers, int n_recv,
                      void* const* recv_ptrs, const long long* recv_bytes,
@@ -417,47 +595,43 @@ int dli_ipc_exchange(void* h, void* stream, int n_send, void* const* send_ptrs,
   for (int i = 0; i < n_send; ++i) {
     const Edge& g = e->edge[send_peers[i]];
     if (g.peer_ready == nullptr || send_bytes[i] > g.out_bytes) return -1003;
+    if ((uintptr_t)send_ptrs[i] % 4 || send_bytes[i] % 4) return -1007;
   }
   for (int i = 0; i < n_recv; ++i) {
     const Edge& g = e->edge[recv_peers[i]];
     if (g.my_ready == nullptr || recv_bytes[i] > g.in_bytes) return -1003;
+    if ((uintptr_t)recv_ptrs[i] % 4 || recv_bytes[i] % 4) return -1007;
   }
-  bool kern = e->sync_mode == 1;
-  if (!kern) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive)
-      kern = true;
-  }
-  // wait until *w == 1 then reset it; signal *w = 1
-  auto wait = [&](uint64_t* w) -> int {
-    if (kern) {
-      ipc_wait_kernel<<<1, 64, 0, s>>>(w, e->err_word, e->wait_budget);
-      return herr(hipGetLastError());
-    }
-    int r = herr(hipStreamWaitValue64(s, w, 1, hipStreamWaitValueEq));
-    return r ? r : herr(hipStreamWriteValue64(s, w, 0, 0));
-  };
-  auto signal = [&](uint64_t* w) -> int {
-    if (kern) {
-      ipc_signal_kernel<<<1, 64, 0, s>>>(w);
-      return herr(hipGetLastError());
-    }
-    return herr(hipStreamWriteValue64(s, w, 1, 0));
-  };
   int r = 0;
   for (int i = 0; i < n_send && r == 0; ++i) {
-    const Edge& g = e->edge[send_peers[i]];
-    r = wait(g.my_free);
-    if (!r) r = copy_async(e, g.peer_mailbox, send_ptrs[i], send_bytes[i], s);
-    if (!r) r = signal(g.peer_ready);
+    const int p = send_peers[i];
+    const Edge& g = e->edge[p];
+    const long long nb = send_bytes[i];
+    const int vec = (uintptr_t)send_ptrs[i] % 16 == 0;
+    r = wait_flag(e, s, g.my_free);
+    if (!r) {
+      ipc_put_kernel<<<blocks_for(vec ? nb / 16 : nb / 64), 256, 0, s>>>(
+          g.peer_mailbox, reinterpret_cast<const uint8_t*>(send_ptrs[i]), nb, vec, e->seq + p,
+          e->err);
+      r = herr(hipGetLastError());
+    }
+    if (!r) r = signal_flag(e, s, g.peer_ready);
     e->sends++;
-    e->bytes_out += (uint64_t)send_bytes[i];
+    e->bytes_out += (uint64_t)nb;
   }
   for (int i = 0; i < n_recv && r == 0; ++i) {
-    const Edge& g = e->edge[recv_peers[i]];
-    r = wait(g.my_ready);
-    if (!r) r = copy_async(e, recv_ptrs[i], g.my_mailbox, recv_bytes[i], s);
-    if (!r) r = signal(g.peer_free);
+    const int p = recv_peers[i];
+    const Edge& g = e->edge[p];
+    const long long nb = recv_bytes[i];
+    const int vec = (uintptr_t)recv_ptrs[i] % 16 == 0;
+    r = wait_flag(e, s, g.my_ready);
+    if (!r) {
+      ipc_get_kernel<<<blocks_for(vec ? nb / 16 : nb / 64), 256, 0, s>>>(
+          reinterpret_cast<uint8_t*>(recv_ptrs[i]), g.my_mailbox, nb, vec,
+          e->seq + e->world + p, e->err);
+      r = herr(hipGetLastError());
+    }
+    if (!r) r = signal_flag(e, s, g.peer_free);
     e->recvs++;
   }
   return r;
@@ -470,13 +644,15 @@ int dli_ipc_exchange(void* h, void* stream, int n_send, void* const* send_ptrs,
 //     in recv_x + recv_base[q] rows (region capacity recv_cap[q]; ids -> recv_e +
 //     recv_base[q], -1 past the count; count -> recv_cnt[q] on the device).
 //   return: the roles swap: the recv_cnt[q] result rows at recv_x + recv_base[q] go back to
-//     q, and peer p's results for my rows land at send_x + send_base[p] (no ids).
+//     q, and peer p's results for my rows land at send_x + send_base[p] (no ids), at most
+//     send_cap rows per peer.
 // cap_rows[p] / in_cap_rows[q]: capacity in rows of the mailbox of edge me -> p / q -> me
-// (sized by the caller with dli_ipc_ep_bytes).
+// (sized by the caller with dli_ipc_ep_bytes). Every received count is clamped to the
+// region it lands in; an over-long message raises the sequence error bit.
 int dli_ipc_ep(void* h, void* stream, int ret, int row_bytes, void* send_x, int* send_e,
                const int* send_base, int* send_cnt, void* recv_x, int* recv_e,
                const int* recv_base, const int* recv_cap, int* recv_cnt, const int* cap_rows,
-               const int* in_cap_rows) {
+               const int* in_cap_rows, int send_cap) {
   auto* e = E(h);
   auto s = (hipStream_t)stream;
   const int W = e->world, me = e->rank;
@@ -490,31 +666,9 @@ int dli_ipc_ep(void* h, void* stream, int ret, int row_bytes, void* send_x, int*
     if (ep_bytes(cap_rows[p]) > g.out_bytes || ep_bytes(in_cap_rows[p]) > g.in_bytes)
       return -1003;
   }
-  bool kern = e->sync_mode == 1;
-  if (!kern) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive)
-      kern = true;
-  }
-  auto wait = [&](uint64_t* w) -> int {
-    if (kern) {
-      ipc_wait_kernel<<<1, 64, 0, s>>>(w, e->err_word, e->wait_budget);
-      return herr(hipGetLastError());
-    }
-    int r = herr(hipStreamWaitValue64(s, w, 1, hipStreamWaitValueEq));
-    return r ? r : herr(hipStreamWriteValue64(s, w, 0, 0));
-  };
-  auto signal = [&](uint64_t* w) -> int {
-    if (kern) {
-      ipc_signal_kernel<<<1, 64, 0, s>>>(w);
-      return herr(hipGetLastError());
-    }
-    return herr(hipStreamWriteValue64(s, w, 1, 0));
-  };
-  auto blocks = [&](long rows) {
-    long b = (rows * row16 + 4 * 256 - 1) / (4 * 256);
-    return (unsigned)(b < 1 ? 1 : (b > 2048 ? 2048 : b));
-  };
+  auto blocks = [&](long rows) { return blocks_for(rows * row16); };
+  uint64_t* seq_out = e->seq;
+  uint64_t* seq_in = e->seq + W;
   auto* sx = reinterpret_cast<uint8_t*>(send_x);
   auto* rx = reinterpret_cast<uint8_t*>(recv_x);
   const long rb = row_bytes;
@@ -523,33 +677,34 @@ int dli_ipc_ep(void* h, void* stream, int ret, int row_bytes, void* send_x, int*
     for (int p = 0; p < W && r == 0; ++p) {
       if (p == me) continue;
       const Edge& g = e->edge[p];
-      r = wait(g.my_free);
+      r = wait_flag(e, s, g.my_free);
       if (r) break;
       ep_put_kernel<<<blocks(cap_rows[p]), 256, 0, s>>>(
           g.peer_mailbox, cap_rows[p], send_cnt + p,
           reinterpret_cast<const uint4*>(sx + (long)send_base[p] * rb), row16,
-          send_e + send_base[p]);
+          send_e + send_base[p], seq_out + p, e->err);
       r = herr(hipGetLastError());
-      if (!r) r = signal(g.peer_ready);
+      if (!r) r = signal_flag(e, s, g.peer_ready);
       e->sends++;
     }
     if (r == 0) {
       ep_local_kernel<<<blocks(recv_cap[me]), 256, 0, s>>>(
           send_cnt + me, reinterpret_cast<const uint4*>(sx + (long)send_base[me] * rb), row16,
           send_e + send_base[me], reinterpret_cast<uint4*>(rx + (long)recv_base[me] * rb),
-          recv_e + recv_base[me], recv_cap[me], recv_cnt + me);
+          recv_e + recv_base[me], recv_cap[me], recv_cap[me], recv_cnt + me);
       r = herr(hipGetLastError());
     }
     for (int q = 0; q < W && r == 0; ++q) {
       if (q == me) continue;
       const Edge& g = e->edge[q];
-      r = wait(g.my_ready);
+      r = wait_flag(e, s, g.my_ready);
       if (r) break;
       ep_get_kernel<<<blocks(recv_cap[q]), 256, 0, s>>>(
           g.my_mailbox, in_cap_rows[q], reinterpret_cast<uint4*>(rx + (long)recv_base[q] * rb),
-          row16, recv_e + recv_base[q], recv_cap[q], recv_cnt + q);
+          row16, recv_e + recv_base[q], recv_cap[q], recv_cap[q], recv_cnt + q, seq_in + q,
+          e->err);
       r = herr(hipGetLastError());
-      if (!r) r = signal(g.peer_free);
+      if (!r) r = signal_flag(e, s, g.peer_free);
       e->recvs++;
     }
     return r;
@@ -557,37 +712,39 @@ int dli_ipc_ep(void* h, void* stream, int ret, int row_bytes, void* send_x, int*
   for (int q = 0; q < W && r == 0; ++q) {
     if (q == me) continue;
     const Edge& g = e->edge[q];
-    r = wait(g.my_free);
+    r = wait_flag(e, s, g.my_free);
     if (r) break;
     ep_put_kernel<<<blocks(recv_cap[q]), 256, 0, s>>>(
         g.peer_mailbox, cap_rows[q], recv_cnt + q,
-        reinterpret_cast<const uint4*>(rx + (long)recv_base[q] * rb), row16, nullptr);
+        reinterpret_cast<const uint4*>(rx + (long)recv_base[q] * rb), row16, nullptr,
+        seq_out + q, e->err);
     r = herr(hipGetLastError());
-    if (!r) r = signal(g.peer_ready);
+    if (!r) r = signal_flag(e, s, g.peer_ready);
     e->sends++;
   }
   if (r == 0) {
     ep_local_kernel<<<blocks(recv_cap[me]), 256, 0, s>>>(
         recv_cnt + me, reinterpret_cast<const uint4*>(rx + (long)recv_base[me] * rb), row16,
-        nullptr, reinterpret_cast<uint4*>(sx + (long)send_base[me] * rb), nullptr, 0, nullptr);
+        nullptr, reinterpret_cast<uint4*>(sx + (long)send_base[me] * rb), nullptr, 0, send_cap,
+        nullptr);
     r = herr(hipGetLastError());
   }
   for (int p = 0; p < W && r == 0; ++p) {
     if (p == me) continue;
     const Edge& g = e->edge[p];
-    r = wait(g.my_ready);
+    r = wait_flag(e, s, g.my_ready);
     if (r) break;
     ep_get_kernel<<<blocks(in_cap_rows[p]), 256, 0, s>>>(
         g.my_mailbox, in_cap_rows[p], reinterpret_cast<uint4*>(sx + (long)send_base[p] * rb),
-        row16, nullptr, 0, nullptr);
+        row16, nullptr, 0, send_cap, nullptr, seq_in + p, e->err);
     r = herr(hipGetLastError());
-    if (!r) r = signal(g.peer_free);
+    if (!r) r = signal_flag(e, s, g.peer_free);
     e->recvs++;
   }
   return r;
 }
 
-// Mailbox bytes an expert-parallel edge of `cap_rows` rows needs.
+// Mailbox payload bytes an expert-parallel edge of `cap_rows` rows needs.
 long long dli_ipc_ep_bytes(int cap_rows, int row_bytes) {
   return 16 + ((long long)cap_rows * 4 + 15) / 16 * 16 + (long long)cap_rows * row_bytes;
 }
@@ -602,15 +759,19 @@ long long dli_ipc_pending(void* h, int peer) {
 }
 
 // Release whatever this rank's queue waits on (a dead peer): set every READY and FREE word
-// of this rank to 1. A queue resets a word after each wait, so a caller draining a stream
-// repeats this until the stream is idle. Host flags: CPU stores. Device flags: an H2D copy
-// of the pattern on the endpoint's own non-blocking stream (a DMA queue, not the blocked
-// compute queue), polled for up to timeout_s; -1004 when it did not complete.
+// of this rank to 1 and the error mirror to "aborted", so every wait kernel already queued
+// returns at once and no further signal is sent (sticky). A stream-op wait (DLI_IPC_SYNC=
+// stream) resets its word after each wait, so a caller draining such a stream repeats this
+// until the stream is idle. Host flags: CPU stores. Device flags: an H2D copy of the pattern
+// on the endpoint's own non-blocking stream (a DMA queue, not the blocked compute queue),
+// polled for up to timeout_s; -1004 when it did not complete.
 int dli_ipc_abort(void* h, double timeout_s) {
   auto* e = E(h);
   const size_t n = 2 * (size_t)e->world;
+  reinterpret_cast<std::atomic<uint64_t>*>(e->err_host)->fetch_or(kErrAbort);
   if (e->host_flags) {
     for (size_t i = 0; i < n; ++i) set_word(e->flags + i * kFlagStride, 1);
+    set_word(e->flags + err_word(e), kErrAbort);
     return 0;
   }
   if (e->abort_stream == nullptr) return -1005;
@@ -626,19 +787,31 @@ int dli_ipc_abort(void* h, double timeout_s) {
   return 0;
 }
 
-// 1 when a wait kernel ran out of its wall-clock budget (a peer stopped signalling).
+// The error bits (kErrWait | kErrSeq | kErrAbort) set so far: one load of a pinned host word,
+// cheap enough to poll every pipeline tick.
 int dli_ipc_error(void* h) {
   auto* e = E(h);
-  if (e->host_flags)
-    return reinterpret_cast<std::atomic<uint64_t>*>(e->flags + 2 * (size_t)e->world * kFlagStride)
-               ->load(std::memory_order_acquire) ? 1 : 0;
-  if (e->abort_stream == nullptr) return -1;
-  uint64_t v = 0;
-  if (hipMemcpyAsync(&v, e->err_word, 8, hipMemcpyDeviceToHost, e->abort_stream) != hipSuccess ||
-      hipStreamSynchronize(e->abort_stream) != hipSuccess)
-    return -1;
-  return v ? 1 : 0;
+  return (int)reinterpret_cast<std::atomic<uint64_t>*>(e->err_host)->load(
+      std::memory_order_acquire);
 }
+
+// Bounded-wait budget in seconds (wait kernels enqueued after the call).
+void dli_ipc_set_wait(void* h, double secs) {
+  auto* e = E(h);
+  e->wait_budget = (unsigned long long)(secs * 1000.0 * (double)e->khz);
+}
+
+// Test hook: advance this rank's outbound sequence counter for `peer` by `d` on `stream`, so
+// the next message on that edge carries a wrong sequence number (the receiver must flag it).
+int dli_ipc_debug_bump_seq(void* h, void* stream, int peer, long long d) {
+  auto* e = E(h);
+  if (peer < 0 || peer >= e->world) return -1;
+  ipc_bump_kernel<<<1, 64, 0, (hipStream_t)stream>>>(e->seq + peer, (uint64_t)d);
+  return herr(hipGetLastError());
+}
+
+// 0 coarse-grained, 1 fine-grained, 2 uncached: the allocation the mailboxes use
+int dli_ipc_mem_kind(void* h) { return E(h)->mem_kind; }
 
 void dli_ipc_stats(void* h, long long* out3) {
   auto* e = E(h);
@@ -666,6 +839,8 @@ void dli_ipc_destroy(void* h) {
   if (e->abort_stream) (void)hipStreamDestroy(e->abort_stream);
   if (e->abort_src) (void)hipHostFree(e->abort_src);
   if (e->mailbox) (void)hipFree(e->mailbox);
+  if (e->seq) (void)hipFree(e->seq);
+  if (e->err_host) (void)hipHostFree(e->err_host);
   delete e;
 }
 

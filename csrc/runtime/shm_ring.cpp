@@ -268,6 +268,20 @@ long long dli_ring_min_consumed(void* h) {
   return (long long)m;
 }
 
+// Liveness of the ring's processes (the pipeline watchdog polls this every ~0.2 s, so a
+// stage that dies is noticed in well under a second instead of when a wait times out):
+// -1 all alive, consumer index c (>= 0) if consumer c's process is gone, 1000 if the
+// producer's is. Consumers that never opened (pid 0) count as alive.
+int dli_ring_dead(void* h) {
+  auto* hd = R(h)->hdr;
+  if (!pid_alive(hd->producer_pid)) return 1000;
+  for (uint64_t c = 0; c < hd->consumers; ++c) {
+    const int64_t pid = (int64_t)hd->consumer_pid[c].v.load(std::memory_order_acquire);
+    if (pid > 0 && !pid_alive(pid)) return (int)c;
+  }
+  return -1;
+}
+
 void dli_ring_close(void* h) {
   auto* r = R(h);
   if (r && r->hdr) r->hdr->closed.store(1, std::memory_order_release);

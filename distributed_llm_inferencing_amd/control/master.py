@@ -390,7 +390,14 @@ def main(argv=None):
         return
     from ..utils.log import setup_logging
     setup_logging("master")
-    app = create_master_app()
+    # werkzeug's thread-per-request server + the threaded dispatcher: the store's database
+    # thread (inline mode is for the event-loop fronts above, whose callers are one loop;
+    # with many request threads one RLock on the caller's thread convoys). DLI_STORE_INLINE
+    # overrides.
+    s = get_settings()
+    env_inline = os.environ.get("DLI_STORE_INLINE")
+    app = create_master_app(s, store=Store(s.master_db, inline=(
+        env_inline == "1" if env_inline is not None else False)))
     app.run(host=a.host, port=a.port, threaded=True)
 
 

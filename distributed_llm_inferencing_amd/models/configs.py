@@ -32,6 +32,9 @@ class ModelConfig:
     tie_embeddings: bool = False
     bos_token_id: int = 1
     eos_token_id: int = 2
+    # HF ``rope_scaling`` as sorted (key, value) pairs: () = none; rope_type "llama3"
+    # (Llama-3.1 / 3.2 checkpoints: low-frequency inv_freq rescaled) or "linear"
+    rope_scaling: tuple = ()
 
     @property
     def is_moe(self) -> bool:
@@ -86,7 +89,10 @@ class ModelConfig:
     @classmethod
     def from_dict(cls, d: dict) -> "ModelConfig":
         fields = cls.__dataclass_fields__.keys()
-        return cls(**{k: v for k, v in d.items() if k in fields})
+        kw = {k: v for k, v in d.items() if k in fields}
+        if "rope_scaling" in kw:         # JSON turned the pairs into lists
+            kw["rope_scaling"] = tuple(tuple(p) for p in (kw["rope_scaling"] or ()))
+        return cls(**kw)
 
 
 GPT2 = ModelConfig(

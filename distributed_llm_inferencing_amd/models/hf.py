@@ -76,14 +76,36 @@ def config_from_hf(c: dict, name: Optional[str] = None) -> ModelConfig:
         raise ValueError(f"unsupported HF model_type '{mt}' (llama, mistral, mixtral, gpt2)")
     d, nh = int(c["hidden_size"]), int(c["num_attention_heads"])
     rope = c.get("rope_theta")
+    params = c.get("rope_parameters") or {}
     if rope is None:
-        rope = (c.get("rope_parameters") or {}).get("rope_theta", 10000.0)
+        rope = params.get("rope_theta", 10000.0)
+    # rope scaling (Llama-3.1 / 3.2 "llama3", "linear"): absorbed into the cos/sin table;
+    # transformers 5 keeps it in rope_parameters, older configs in rope_scaling
+    sc = dict(c.get("rope_scaling") or {})
+    if not sc and params.get("rope_type", "default") not in ("default", None):
+        sc = {k: v for k, v in params.items() if k != "rope_theta"}
+    if sc:
+        from ..ops.reference import rope_scaled_inv_freq
+        import torch as _t
+        rope_scaled_inv_freq(_t.ones(2, dtype=_t.float64), sc)     # refuse unknown types now
+    max_pos = int(c.get("max_position_embeddings", 8192))
+    # sliding-window attention (Mistral): full attention equals it while a sequence fits the
+    # window, so the model's context is capped there instead of silently diverging past it
+    sw = c.get("sliding_window")
+    if sw and int(sw) < max_pos:
+        import logging
+        logging.getLogger(__name__).warning(
+            "sliding_window=%s < max_position_embeddings=%s: context capped at the window "
+            "(sliding-window attention is not implemented)", sw, max_pos)
+        max_pos = int(sw)
     return ModelConfig(
         name=name, arch="llama", hidden_size=d, num_layers=int(c["num_hidden_layers"]),
         num_heads=nh, num_kv_heads=int(c.get("num_key_value_heads") or nh),
         head_dim=int(c.get("head_dim") or d // nh),
         intermediate_size=int(c["intermediate_size"]), vocab_size=int(c["vocab_size"]),
-        max_position=int(c.get("max_position_embeddings", 8192)), rope_theta=float(rope),
+        max_position=max_pos, rope_theta=float(rope),
+        rope_scaling=tuple(sorted((str(k), v) for k, v in sc.items()
+                                  if isinstance(v, (int, float, str)))),
         norm_eps=float(c.get("rms_norm_eps", 1e-5)),
         num_experts=int(c.get("num_local_experts", 0)) if mt == "mixtral" else 0,
         top_k_experts=int(c.get("num_experts_per_tok", 2)),

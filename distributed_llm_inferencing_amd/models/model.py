@@ -44,7 +44,7 @@ class TransformerLM:
         self.cos_sin = None
         if cfg.arch == "llama":
             self.cos_sin = R.rope_cos_sin(cfg.max_position, cfg.head_dim, cfg.rope_theta,
-                                          device=self.device)
+                                          device=self.device, scaling=cfg.rope_scaling)
         self.moe_fn: Callable = self._moe_local
         # tensor-parallel mode (parallel/tensor.py): all-reduce(sum) of the row-parallel
         # O / down projections before their residual add

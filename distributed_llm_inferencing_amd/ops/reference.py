@@ -108,12 +108,40 @@ def linear_silu_mul(x, w_gu):
 
 
 # ----------------------------------------------------------------------------- RoPE + KV write (K5, K6)
-def rope_cos_sin(max_pos: int, head_dim: int, theta: float, device=None) -> torch.Tensor:
-    """[max_pos, head_dim] fp32 table: cols [0, hd/2) = cos, [hd/2, hd) = sin."""
+def rope_cos_sin(max_pos: int, head_dim: int, theta: float, device=None,
+                 scaling=()) -> torch.Tensor:
+    """[max_pos, head_dim] fp32 table: cols [0, hd/2) = cos, [hd/2, hd) = sin. ``scaling``:
+    the HF ``rope_scaling`` of the checkpoint as (key, value) pairs (ModelConfig)."""
     half = head_dim // 2
     inv = 1.0 / (theta ** (torch.arange(0, half, dtype=torch.float64) * 2.0 / head_dim))
+    inv = rope_scaled_inv_freq(inv, dict(scaling))
     ang = torch.arange(max_pos, dtype=torch.float64)[:, None] * inv[None, :]
     return torch.cat([ang.cos(), ang.sin()], dim=1).float().to(device)
+
+
+def rope_scaled_inv_freq(inv: torch.Tensor, sc: dict) -> torch.Tensor:
+    """HF ``rope_scaling`` applied to the inverse frequencies (the table absorbs it, so the
+    kernels are unchanged). ``llama3``: wavelengths longer than original_max / low_freq_factor
+    are divided by ``factor``, shorter than original_max / high_freq_factor kept, the band
+    between interpolated (transformers ``_compute_llama3_parameters``); ``linear``: every
+    frequency divided by ``factor`` (= positions / factor). Other types are refused."""
+    kind = sc.get("rope_type", sc.get("type", "default")) if sc else "default"
+    if kind in ("default", None):
+        return inv
+    factor = float(sc["factor"])
+    if kind == "linear":
+        return inv / factor
+    if kind == "llama3":
+        lo, hi = float(sc.get("low_freq_factor", 1.0)), float(sc.get("high_freq_factor", 4.0))
+        old = float(sc.get("original_max_position_embeddings", 8192))
+        lo_wl, hi_wl = old / lo, old / hi
+        wl = 2 * math.pi / inv
+        out = torch.where(wl > lo_wl, inv / factor, inv)
+        smooth = (old / wl - lo) / (hi - lo)
+        smoothed = (1 - smooth) * out / factor + smooth * out
+        medium = (wl >= hi_wl) & (wl <= lo_wl)
+        return torch.where(medium, smoothed, out)
+    raise ValueError(f"unsupported rope_scaling type {kind!r} (supported: llama3, linear)")
 
 
 def apply_rope(x: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor) -> torch.Tensor:

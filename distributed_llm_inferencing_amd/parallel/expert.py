@@ -130,10 +130,13 @@ class ExpertParallelMoE:
         if base is None:
             base = torch.tensor(send_base, dtype=torch.int32, device=dev)
             self._bases[key] = base
+        # receive region of source q: a peer replaying a decode graph routes EVERY row of its
+        # padded bucket (up to graph_tokens rows, not its announced token count), so an eager
+        # rank (idle, or running a small prefill) reserves at least the largest bucket for it
         if self.static:          # a captured graph: regions sized for any decode batch
             rcap = [self.graph_tokens * pt] * N
         else:
-            rcap = [t * pt for t in self.peer_tokens]
+            rcap = [max(t, self.graph_tokens) * pt for t in self.peer_tokens]
         recv_base = [0] * N
         for q in range(1, N):
             recv_base[q] = recv_base[q - 1] + rcap[q - 1]
@@ -148,7 +151,7 @@ class ExpertParallelMoE:
         recv_cnt = torch.zeros(N, dtype=torch.int32, device=dev)
         st = torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else 0
         self.ep.ep(st, False, self.row_bytes, send_x, send_e, send_base, cnt, recv_x, recv_e,
-                   recv_base, rcap, recv_cnt, self.caps, self.caps)
+                   recv_base, rcap, recv_cnt, self.caps, self.caps, send_cap=C)
         if R > 0:
             y = ops.moe_mlp(recv_x[:R], lp["w_gu"], lp["w_down"],
                             torch.ones(R, 1, dtype=torch.float32, device=dev),
@@ -156,7 +159,7 @@ class ExpertParallelMoE:
         else:
             y = recv_x
         self.ep.ep(st, True, self.row_bytes, send_x, send_e, send_base, cnt, y, None,
-                   recv_base, rcap, recv_cnt, self.caps, self.caps)
+                   recv_base, rcap, recv_cnt, self.caps, self.caps, send_cap=C)
         self.exchanges += 1
         self.rows_routed += T * self.k
         if dev.type != "cuda":           # host model: counts are readable for the tests
@@ -259,7 +262,13 @@ class ExpertParallelEngine:
         if not cfg.is_moe:
             raise ValueError(f"{model} has no experts")
         self.cfg = cfg
-        self.comm = comm or os.environ.get("DLI_EP_COMM", "torch")
+        from datetime import timedelta
+        from .transport import resolve_comm
+        self.ctrl_group = dist.new_group(backend="gloo", timeout=timedelta(days=365))
+        # "auto" (default): the device mailboxes when every rank is a GPU process on this
+        # host and they pass their self-test, else the torch all-to-all (resolve_comm)
+        requested = comm or os.environ.get("DLI_EP_COMM", "auto")
+        self.comm = resolve_comm(requested, dev, self.ctrl_group)
         self.moe = ExpertParallelMoE(cfg.num_experts, cfg.top_k_experts)
         er = self.moe.expert_range()
         if model_dir is not None:
@@ -276,8 +285,14 @@ class ExpertParallelEngine:
         lm.moe_fn = self.moe
         ipc = self.comm == "ipc"
         if ipc:
+            from .transport import ipc_selftest
             self.moe.setup_ipc(dev, cfg.hidden_size, dtype,
                                max(max_prefill_tokens, max_batch), max_batch)
+            if not ipc_selftest(self.moe.ep, self.ctrl_group):
+                if requested == "ipc":
+                    raise RuntimeError("IPC expert data plane failed its self-test")
+                self.moe.close()
+                self.comm, ipc = "torch", False
         # with the mailbox data plane the decode forward is captured (graphs); the torch
         # data plane needs host-side split sizes per layer and runs eagerly
         graphs = ipc and dev.type == "cuda" and os.environ.get("DLI_NO_GRAPHS", "0") != "1"
@@ -328,6 +343,11 @@ class ExpertParallelEngine:
         rank, then launch the forward (an empty one when this rank has none) and apply the
         tokens of the step that completes. Returns (outputs, any rank had work)."""
         eng = self.engine
+        if self.moe.ep is not None:
+            bits = self.moe.ep.error()
+            if bits:
+                from .transport import DataPlaneError
+                raise DataPlaneError(bits)
         meta = eng.plan_step()
         work = meta is not None or eng.has_work()
         info = self._exchange(work, 0 if meta is None else meta.num_tokens)

@@ -59,7 +59,7 @@ class ShmMailboxTransport:
         self.timeout_s = timeout_s
         W = world
         # layout: flags [READY[src] x W][FREE[dst] x W] (one line each), then per inbound
-        # edge an 8-byte size header + the mailbox
+        # edge a 16-byte header {size, sequence} + the mailbox (ipc.cpp's message header)
         self._flag_bytes = 2 * W * _LINE * 8
         self._off = {}
         off = self._flag_bytes
@@ -67,7 +67,7 @@ class ShmMailboxTransport:
             c = int(self.cap[s, rank])
             if c > 0:
                 self._off[s] = off
-                off += 8 + ((c + 7) // 8) * 8
+                off += 16 + ((c + 7) // 8) * 8
         self._size = off
         self.shm = _segment(self._name(rank), off)
         flags = np.ndarray((2 * W * _LINE,), dtype=np.int64, buffer=self.shm.buf)
@@ -77,6 +77,10 @@ class ShmMailboxTransport:
         self.peers: Dict[int, shared_memory.SharedMemory] = {}
         self.sends = self.recvs = 0
         self.bytes_out = 0
+        self.seq_out = [0] * W          # per-edge sequence numbers, as ipc.cpp keeps on device
+        self.seq_in = [0] * W
+        self.err = 0
+        self.mem_kind = "shm"
 
     def _name(self, r: int) -> str:
         return f"{self.prefix.strip('/')}_{r}"
@@ -114,7 +118,7 @@ class ShmMailboxTransport:
             if s == self.rank:
                 return off
             if c > 0:
-                off += 8 + ((c + 7) // 8) * 8
+                off += 16 + ((c + 7) // 8) * 8
         raise KeyError(peer)
 
     def send(self, t: torch.Tensor, peer: int) -> None:
@@ -128,9 +132,10 @@ class ShmMailboxTransport:
         self._wait(mine, (W + peer) * _LINE, f"FREE[{self.rank}->{peer}]")
         pshm = self.peers[peer]
         off = self._peer_off(peer)
-        np.ndarray((1,), np.int64, buffer=pshm.buf, offset=off)[0] = b.nbytes
+        self.seq_out[peer] += 1
+        np.ndarray((2,), np.int64, buffer=pshm.buf, offset=off)[:] = (b.nbytes, self.seq_out[peer])
         if b.nbytes:
-            np.ndarray((b.nbytes,), np.uint8, buffer=pshm.buf, offset=off + 8)[:] = b
+            np.ndarray((b.nbytes,), np.uint8, buffer=pshm.buf, offset=off + 16)[:] = b
         self._flags(pshm)[self.rank * _LINE] = 1        # READY in the peer's page
         self.sends += 1
         self.bytes_out += b.nbytes
@@ -139,17 +144,42 @@ class ShmMailboxTransport:
         mine = self._flags(self.shm)
         self._wait(mine, peer * _LINE, f"READY[{peer}->{self.rank}]")
         off = self._off[peer]
-        n = int(np.ndarray((1,), np.int64, buffer=self.shm.buf, offset=off)[0])
+        n, seq = (int(v) for v in np.ndarray((2,), np.int64, buffer=self.shm.buf, offset=off))
+        self._check_seq(peer, seq)
         want = buf.numel() * buf.element_size()
         if n != want:
             raise FifoMismatch(f"rank {self.rank} <- {peer}: the message at the head of the edge "
                                f"has {n} B, the receive posted {want} B (send / receive order "
                                f"differs between the two ranks)")
         if n:
-            src = np.ndarray((n,), np.uint8, buffer=self.shm.buf, offset=off + 8)
+            src = np.ndarray((n,), np.uint8, buffer=self.shm.buf, offset=off + 16)
             buf.view(-1).view(torch.uint8).copy_(torch.from_numpy(src.copy()))
         self._flags(self.peers[peer])[(self.world + self.rank) * _LINE] = 1   # FREE
         self.recvs += 1
+
+    def _check_seq(self, peer: int, seq: int) -> None:
+        self.seq_in[peer] += 1
+        if seq != self.seq_in[peer]:
+            self.err |= 2
+            raise FifoMismatch(f"rank {self.rank} <- {peer}: message sequence {seq}, expected "
+                               f"{self.seq_in[peer]} (stale, lost or duplicated message)")
+
+    # ---- the device endpoint's error / test surface (ipc.cpp) --------------------------
+    def error(self) -> int:
+        return self.err
+
+    def set_wait(self, seconds: float) -> None:
+        self.timeout_s = float(seconds)
+
+    def debug_bump_seq(self, peer: int, stream=None, d: int = 1) -> None:
+        self.seq_out[peer] += int(d)
+
+    def abort(self, timeout_s: float = 5.0) -> None:
+        """Release every wait of this rank (a dead peer): set all of its flags."""
+        self.err |= 4
+        flags = self._flags(self.shm)
+        for i in range(2 * self.world):
+            flags[i * _LINE] = 1
 
     # ---- variable-length messages (expert-parallel rows: the count travels with them) ---
     def send_raw(self, b: np.ndarray, peer: int) -> None:
@@ -161,14 +191,16 @@ class ShmMailboxTransport:
         mine = self._flags(self.shm)
         self._wait(mine, peer * _LINE, f"READY[{peer}->{self.rank}]")
         off = self._off[peer]
-        n = int(np.ndarray((1,), np.int64, buffer=self.shm.buf, offset=off)[0])
-        out = np.ndarray((n,), np.uint8, buffer=self.shm.buf, offset=off + 8).copy()
+        n, seq = (int(v) for v in np.ndarray((2,), np.int64, buffer=self.shm.buf, offset=off))
+        self._check_seq(peer, seq)
+        out = np.ndarray((n,), np.uint8, buffer=self.shm.buf, offset=off + 16).copy()
         self._flags(self.peers[peer])[(self.world + self.rank) * _LINE] = 1   # FREE
         self.recvs += 1
         return out
 
     def ep(self, stream, ret: bool, row_bytes: int, send_x, send_e, send_base, send_cnt,
-           recv_x, recv_e, recv_base, recv_cap, recv_cnt, cap_rows, in_cap_rows) -> None:
+           recv_x, recv_e, recv_base, recv_cap, recv_cnt, cap_rows, in_cap_rows,
+           send_cap=None) -> None:
         """Host model of ``IpcEndpoint.ep`` (csrc/runtime/ipc.cpp ``dli_ipc_ep``): the same
         message order and per-edge FIFO, counts read from the tensors."""
         W, me = self.world, self.rank

@@ -323,10 +323,13 @@ class PipelineHead:
         ph = self.phase_s
         pc = time.perf_counter
         tt = time.thread_time       # this thread's CPU time: host cost without preemption
+        check = ch.check if N > 1 and getattr(ch, "ipc", None) is not None else None
         while True:
             t0 = pc()
             c0 = tt()
             wait_s = wait_c = 0.0
+            if check is not None:
+                check()                      # device data plane healthy (one host load)
             s = k - M
             if s in started:
                 m, _ = started.pop(s)
@@ -459,11 +462,13 @@ def install_piped(stage: StageWorker, channel) -> bool:
     send (to r + 1; on a tail without the vocab-parallel head, its sampled tokens to rank 0)
     INTO its decode graphs, so a decode tick costs one metadata H2D + one graph launch. The
     mailbox semaphores inside a captured graph are wait / signal kernels
-    (csrc/runtime/ipc.cpp), which replay correctly because no sequence number is baked in."""
+    (csrc/runtime/ipc.cpp), which replay correctly: the per-edge sequence numbers live on the
+    device and the put / get kernels advance them on every replay."""
     r, N = channel.rank, channel.world
     run = stage.runner
     if (channel.ipc is None or r == 0 or not run.use_graphs or run.hidden_in is None
-            or os.environ.get("DLI_PP_PIPED_GRAPHS", "1") != "1"):
+            or os.environ.get("DLI_PP_PIPED_GRAPHS", "1") != "1"
+            or os.environ.get("DLI_PP_SCHEDULE", "piped") == "grouped"):
         return False
     tail = r == N - 1
     if tail and stage.vocab_parallel:
@@ -497,9 +502,12 @@ def _serve_session_piped(stage: StageWorker, channel, bufs: _StageBuffers) -> in
     prev_out = None                 # tail + vocab-parallel head: my output of tick k-1
     prev_vp = False
     my_cand = None
+    chk = getattr(channel, "check", None)
     while True:
         if faults.active():
             faults.check("pipeline.stage", tick=k)
+        if chk is not None:
+            chk()                            # device data plane healthy (one host load)
         meta = None
         if k >= r:
             h, p = channel.recv_ctrl()
@@ -565,7 +573,10 @@ def serve_session(stage: StageWorker, channel, bufs: Optional[_StageBuffers] = N
     returns either its final hidden (to every rank) or its sampled tokens (to rank 0). The
     host never waits on this GPU: receives, replays and sends are all stream-ordered."""
     bufs = bufs or _StageBuffers(stage, channel)
-    if channel.ipc is not None:
+    # the mailbox plane runs the piped schedule; DLI_PP_SCHEDULE=grouped runs THIS (the
+    # torch / RCCL) schedule over it instead, so the tag-blind FIFO model of the mailboxes
+    # (fifo.py) checks the grouped schedule's message order too (tests/test_fifo_transport.py)
+    if channel.ipc is not None and os.environ.get("DLI_PP_SCHEDULE", "piped") != "grouped":
         return _serve_session_piped(stage, channel, bufs)
     r, N, k = channel.rank, channel.world, 0
     tail = r == N - 1
@@ -765,6 +776,7 @@ class DistributedPipelineEngine:
     def warmup(self):
         install_piped(self.stage, self.channel)
         self.stage.runner.capture()
+        self.channel.start_watchdog()
 
     def add_request(self, prompt, params: Optional[SamplingParams] = None, request_id=None):
         assert self.head is not None, "requests enter at rank 0"

@@ -30,6 +30,7 @@ from __future__ import annotations
 import itertools
 import os
 import socket
+import threading
 from datetime import timedelta
 from typing import List, Optional, Sequence, Tuple
 
@@ -77,15 +78,18 @@ class PipeChannel:
         self.device = torch.device(device)
         self.dtype = dtype
         # data plane: "torch" (torch.distributed p2p), "rccl" (comm.cpp on the compute
-        # stream) or "ipc" (device mailboxes, ipc.cpp; on CPU its host model, fifo.py)
-        self.comm = comm or os.environ.get("DLI_PP_COMM", "torch")
-        if self.comm not in ("torch", "rccl", "ipc"):
-            raise ValueError(f"DLI_PP_COMM={self.comm}: expected torch | rccl | ipc")
-        self.nccl = dist.get_backend() == "nccl" or (self.comm == "ipc"
-                                                     and self.device.type == "cuda")
+        # stream) or "ipc" (device mailboxes, ipc.cpp; on CPU its host model, fifo.py);
+        # "auto" (default) = ipc when every rank is a GPU process on this host and the
+        # mailboxes pass their self-test, torch otherwise (resolve_comm)
         # collective over all ranks (called once per engine). Idle serving ranks block on
         # the control plane between sessions: no timeout that could fire while idle.
         self.ctrl_group = dist.new_group(backend="gloo", timeout=timedelta(days=365))
+        requested = comm or os.environ.get("DLI_PP_COMM", "auto")
+        self.comm = resolve_comm(requested, self.device, self.ctrl_group)
+        if self.comm not in ("torch", "rccl", "ipc"):
+            raise ValueError(f"DLI_PP_COMM={self.comm}: expected auto | torch | rccl | ipc")
+        self.nccl = dist.get_backend() == "nccl" or (self.comm == "ipc"
+                                                     and self.device.type == "cuda")
         self.data_device = self.device if self.nccl else torch.device("cpu")
         self._ctrl_sends: List = []
         self.ring = None
@@ -114,10 +118,21 @@ class PipeChannel:
         # protocol on shared-memory mailboxes (fifo.py); default: torch.distributed
         self.rccl = None
         self.ipc = None
+        self.dead_peer: Optional[str] = None    # set by the watchdog: who died
+        self._wd_stop = threading.Event()
+        self._wd = None
         if self.world > 1 and self.comm == "rccl" and dist.get_backend() == "nccl":
             self._init_rccl()
         if self.world > 1 and self.comm == "ipc":
             self._init_ipc(*msg_bytes)
+            ok = ipc_selftest(self.ipc, self.ctrl_group)
+            if not ok:
+                if requested == "ipc":
+                    raise RuntimeError("IPC data plane failed its self-test")
+                self._close_ipc()
+                self.comm = "torch"
+                self.nccl = dist.get_backend() == "nccl"
+                self.data_device = self.device if self.nccl else torch.device("cpu")
 
     # ------------------------------------------------------------------ setup
     def _init_rccl(self) -> None:
@@ -157,11 +172,92 @@ class PipeChannel:
         dist.barrier(group=self.ctrl_group)
         self.ipc = ep
         self.data_device = self.device
-        t = torch.full((1,), float(self.rank), device=self.device)
-        r = torch.empty(1, device=self.device)
-        self.ipc.exchange([(t, self.next)], [(r, self.prev)], self._stream())
-        if int(r.item()) != self.prev:
-            raise RuntimeError(f"IPC ring check failed on rank {self.rank}")
+
+    def _close_ipc(self) -> None:
+        if self.ipc is not None:
+            if self.device.type == "cuda" and not self.drain():
+                # a queue still blocked after the bounded drain: leak the endpoint rather
+                # than free mailboxes a kernel may still touch
+                self.ipc = None
+                return
+            self.ipc.close()
+            self.ipc = None
+
+    def check(self) -> None:
+        """Raise if a ring process died (watchdog) or the device data plane flagged an error
+        (a peer stopped signalling, a stale or mis-ordered message, an abort): one load of
+        a pinned host word, called every tick by the head and by every stage, so a broken
+        ring fails its session instead of serving tokens computed from stale activations."""
+        if self.dead_peer is not None:
+            raise PeerDied(self.dead_peer)
+        if self.ipc is not None:
+            bits = self.ipc.error()
+            if bits:
+                raise DataPlaneError(bits)
+
+    # ------------------------------------------------------------------ failure detection
+    def start_watchdog(self, period_s: float = 0.2) -> None:
+        """Poll the liveness of every process on the ring (the shared-memory control ring
+        records each one's pid) and the RCCL communicator's async error every ``period_s``;
+        on a death abort the data plane AT ONCE (every wait this rank's queue holds on the
+        dead peer is released, the device plane turns sticky-failed) so the next ``check``
+        of the tick loop raises. Detection within ~``period_s`` instead of a wait budget or
+        the RCCL watchdog's ``DLI_PP_TIMEOUT_S``. SURVEY.md §5.3."""
+        if self.world == 1 or self._wd is not None:
+            return
+        if self.ring is None and self.rccl is None:
+            return                      # gloo control plane across hosts: sockets tell
+        self._wd = threading.Thread(target=self._watch, args=(float(period_s),), daemon=True,
+                                    name=f"dli-pp-watchdog-{self.rank}")
+        self._wd.start()
+
+    def _watch(self, period: float) -> None:
+        while not self._wd_stop.wait(period):
+            ring = self.ring
+            d = ring.dead() if ring is not None else -1
+            err = self.rccl.async_error() if self.rccl is not None else 0
+            if d == -1 and err == 0:
+                continue
+            if d == 1000:
+                self.dead_peer = "pipeline head (rank 0) exited"
+            elif d >= 0:
+                self.dead_peer = f"pipeline stage {d + 1} exited"
+            else:
+                self.dead_peer = f"RCCL communicator error {err}"
+            self.abort_data_plane()
+            return
+
+    def abort_data_plane(self, timeout_s: float = 5.0) -> None:
+        """Release this rank's queue from a dead peer: IPC mailboxes aborted (sticky
+        error, every flag set), the direct RCCL communicator aborted (ncclCommAbort)."""
+        if self.ipc is not None and hasattr(self.ipc, "abort"):
+            try:
+                self.ipc.abort(timeout_s)
+            except Exception:  # noqa: BLE001
+                pass
+        if self.rccl is not None:
+            try:
+                self.rccl.abort()
+            except Exception:  # noqa: BLE001
+                pass
+
+    def drain(self, timeout_s: float = 10.0) -> bool:
+        """Wait (bounded) until this rank's compute stream has finished everything queued,
+        re-aborting the mailboxes meanwhile (a stream-op wait, DLI_IPC_SYNC=stream, takes
+        one release per queued wait). True when the stream drained."""
+        if self.device.type != "cuda":
+            return True
+        import time as _t
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        t0 = _t.monotonic()
+        while not ev.query():
+            if self.dead_peer is not None or (self.ipc is not None and self.ipc.error()):
+                self.abort_data_plane(1.0)
+            if _t.monotonic() - t0 > timeout_s:
+                return False
+            _t.sleep(0.005)
+        return True
 
     def _stream(self) -> int:
         return (torch.cuda.current_stream(self.device).cuda_stream
@@ -323,19 +419,91 @@ class PipeChannel:
             w.wait()
 
     def close(self) -> None:
+        self._wd_stop.set()
         if getattr(self, "rccl", None) is not None:
-            self.rccl.close()
+            if self.dead_peer is not None:
+                self.rccl.abort()
+            else:
+                self.rccl.close()
             self.rccl = None
         if getattr(self, "ipc", None) is not None:
-            if self.device.type == "cuda":
-                torch.cuda.synchronize(self.device)
-            self.ipc.close()
-            self.ipc = None
+            self._close_ipc()
         if self.ring is not None:
             if self.rank == 0:
                 self.ring.close()
             self.ring.destroy()
             self.ring = None
+
+
+class PeerDied(RuntimeError):
+    """The pipeline watchdog saw a ring process exit (or RCCL report an async error)."""
+
+
+class DataPlaneError(RuntimeError):
+    """The device mailbox data plane raised error bits (csrc/runtime/ipc.cpp)."""
+
+    def __init__(self, bits: int):
+        what = [n for b, n in ((1, "a peer stopped signalling (wait budget exceeded)"),
+                               (2, "stale / lost / mis-ordered message (sequence check)"),
+                               (4, "ring aborted")) if bits & b]
+        super().__init__(f"IPC data plane error {bits}: " + "; ".join(what))
+        self.bits = bits
+
+
+def resolve_comm(requested: str, device: torch.device, group) -> str:
+    """``auto`` -> ``ipc`` when this is a GPU rank and every rank of ``group`` runs on this
+    host (the hipIpc mailboxes need one node), else ``torch``. Explicit values pass through.
+    A collective over ``group`` (gloo) when ``auto``."""
+    requested = (requested or "auto").lower()
+    if requested != "auto":
+        return requested
+    hosts = [None] * dist.get_world_size(group)
+    dist.all_gather_object(hosts, (socket.gethostname(), device.type == "cuda"), group=group)
+    same_host = len({h for h, _ in hosts}) == 1
+    return "ipc" if same_host and all(g for _, g in hosts) else "torch"
+
+
+def ipc_selftest(ep, group, wait_s: float = 10.0) -> bool:
+    """One message over EVERY edge of the endpoint (all sends, then all receives: the
+    mailboxes start empty, so this order cannot block), each a rank/peer-specific pattern
+    checked on arrival, under a short wait budget; then the error word. Every rank learns
+    every rank's verdict (``group``, gloo), so all of them keep or drop the data plane
+    together. On a GPU this is the first end-to-end use of the mapped peer memory: a node
+    whose peer writes never land fails here and the caller falls back to torch/RCCL."""
+    cap = np.asarray(ep.cap)
+    W, me = cap.shape[0], dist.get_rank(group)
+    dev = torch.device("cuda", torch.cuda.current_device()) if _is_gpu_ep(ep) else \
+        torch.device("cpu")
+    n = 256
+    ok = True
+    try:
+        ep.set_wait(wait_s)
+        sends = [(torch.arange(n, dtype=torch.int32, device=dev) + (me * W + p) * 1000, p)
+                 for p in range(W) if p != me and cap[me, p] >= 4 * n]
+        recvs = [(torch.empty(n, dtype=torch.int32, device=dev), q)
+                 for q in range(W) if q != me and cap[q, me] >= 4 * n]
+        st = torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else 0
+        ep.exchange(sends, recvs, st)
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        for buf, q in recvs:
+            want = torch.arange(n, dtype=torch.int32, device=dev) + (q * W + me) * 1000
+            ok = ok and bool(torch.equal(buf, want))
+        ok = ok and ep.error() == 0
+    except Exception:  # noqa: BLE001 — a failing endpoint is reported, not raised
+        ok = False
+    finally:
+        try:
+            ep.set_wait(float(os.environ.get("DLI_IPC_WAIT_S", "20")))
+        except Exception:  # noqa: BLE001
+            pass
+    verdicts = [None] * dist.get_world_size(group)
+    dist.all_gather_object(verdicts, ok, group=group)
+    return all(verdicts)
+
+
+def _is_gpu_ep(ep) -> bool:
+    return type(ep).__name__ == "IpcEndpoint"
 
 
 def init_distributed(backend: Optional[str] = None, device: Optional[torch.device] = None,

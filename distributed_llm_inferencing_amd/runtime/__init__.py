@@ -69,9 +69,12 @@ _SIGS = {
     "dli_ring_peek_len": ([_P, ctypes.c_double], _LL),
     "dli_ring_published": ([_P], _LL),
     "dli_ring_min_consumed": ([_P], _LL),
+    "dli_ring_dead": ([_P], _I),
     "dli_ring_close": ([_P], None),
     "dli_ring_destroy": ([_P], None),
     "dli_comm_available": ([], _I),
+    "dli_comm_async_error": ([_P], _I),
+    "dli_comm_abort": ([_P], _I),
     "dli_comm_error_string": ([_I], ctypes.c_char_p),
     "dli_comm_unique_id": ([_P], _I),
     "dli_comm_id_bytes": ([], _I),
@@ -87,7 +90,10 @@ _SIGS = {
     "dli_ipc_abort": ([_P, ctypes.c_double], _I),
     "dli_ipc_stats": ([_P, _P], None),
     "dli_ipc_error": ([_P], _I),
-    "dli_ipc_ep": ([_P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P], _I),
+    "dli_ipc_ep": ([_P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I], _I),
+    "dli_ipc_set_wait": ([_P, ctypes.c_double], None),
+    "dli_ipc_debug_bump_seq": ([_P, _P, _I, _LL], _I),
+    "dli_ipc_mem_kind": ([_P], _I),
     "dli_ipc_ep_bytes": ([_I, _I], _LL),
     "dli_ipc_host_flags": ([_P], _I),
     "dli_ipc_destroy": ([_P], None),
@@ -437,6 +443,11 @@ class ShmRing:
     def min_consumed(self) -> int:
         return int(lib().dli_ring_min_consumed(self._h))
 
+    def dead(self) -> int:
+        """-1 while every process on the ring lives; else the index of a consumer whose
+        process is gone, or 1000 for the producer."""
+        return int(lib().dli_ring_dead(self._h)) if self._h else -1
+
     def close(self):
         if self._h:
             lib().dli_ring_close(self._h)
@@ -503,6 +514,17 @@ class RcclComm:
         if r != 0:
             raise RuntimeError(f"RCCL exchange failed: {lib().dli_comm_error_string(r).decode()}")
 
+    def async_error(self) -> int:
+        """0 while healthy, else -(ncclResult_t) of the communicator's asynchronous error."""
+        return int(lib().dli_comm_async_error(self._h)) if self._h is not None else 0
+
+    def abort(self) -> None:
+        """ncclCommAbort: release the communicator without waiting for peers (a dead
+        neighbour); queued RCCL kernels return so the stream drains."""
+        h, self._h = self._h, None
+        if h is not None:
+            lib().dli_comm_abort(h)
+
     def close(self) -> None:
         if self._h is not None:
             lib().dli_comm_destroy(self._h)
@@ -525,10 +547,13 @@ def _pack_io(items):
 
 class IpcEndpoint:
     """Device-memory mailbox transport of one rank (``csrc/runtime/ipc.cpp``): one mailbox
-    per directed edge in the receiver's HBM, filled by a stream-ordered copy and handed over
-    by ``hipStreamWriteValue64`` / ``hipStreamWaitValue64`` binary semaphores (no host-side
-    sequence numbers, so captured exchanges replay correctly). FIFO per edge (RCCL's
-    matching rule), everything enqueued on the caller's stream.
+    per directed edge in the receiver's HBM (uncached: no L2 keeps a copy of a line a peer
+    writes over xGMI), filled by a stream-ordered put kernel and handed over by READY / FREE
+    binary semaphores (bounded wait kernels; no host-side sequence numbers, so captured
+    exchanges replay correctly). Every message carries a device-side sequence number that
+    the receiver checks: a stale or out-of-order mailbox sets ``error()`` instead of
+    yielding wrong activations. FIFO per edge (RCCL's matching rule), everything enqueued on
+    the caller's stream.
 
     Setup is three steps so the caller can move the handles over any side channel:
     ``ep = IpcEndpoint(world, rank, cap)``; gather ``ep.handles()`` from every rank;
@@ -536,6 +561,9 @@ class IpcEndpoint:
     (0 = no edge), the same matrix on every rank. ``host_prefix``: keep the flag words in
     POSIX shared-memory pages (host-visible progress; ``abort()`` releases a dead peer's
     waits)."""
+
+    ERR_WAIT, ERR_SEQ, ERR_ABORT = 1, 2, 4
+    MEM_KINDS = {0: "coarse", 1: "fine", 2: "uncached"}
 
     def __init__(self, world: int, rank: int, cap, host_prefix: str = ""):
         L = lib()
@@ -546,6 +574,7 @@ class IpcEndpoint:
             raise RuntimeError("IPC endpoint: allocation failed")
         self.world, self.rank = world, rank
         self.host_flags = bool(L.dli_ipc_host_flags(self._h))
+        self.mem_kind = self.MEM_KINDS.get(int(L.dli_ipc_mem_kind(self._h)), "?")
 
     def handles(self) -> bytes:
         hb = lib().dli_ipc_handle_bytes()
@@ -588,23 +617,41 @@ class IpcEndpoint:
         return int(lib().dli_ipc_ep_bytes(int(cap_rows), int(row_bytes)))
 
     def ep(self, stream: int, ret: bool, row_bytes: int, send_x, send_e, send_base, send_cnt,
-           recv_x, recv_e, recv_base, recv_cap, recv_cnt, cap_rows, in_cap_rows) -> None:
+           recv_x, recv_e, recv_base, recv_cap, recv_cnt, cap_rows, in_cap_rows,
+           send_cap: Optional[int] = None) -> None:
         """Expert-parallel dispatch (``ret`` False) or return over the mailboxes (see
         ``dli_ipc_ep``): row counts stay on the device (``send_cnt`` / ``recv_cnt`` int32
-        tensors), only the routed rows move."""
+        tensors), only the routed rows move. ``send_cap``: rows of each per-peer send region
+        (a returned count is clamped to it)."""
         W = self.world
         ia = lambda v: (ctypes.c_int * W)(*[int(x) for x in v])  # noqa: E731
+        if send_cap is None:
+            send_cap = max(int(c) for c in cap_rows)
         r = lib().dli_ipc_ep(self._h, ctypes.c_void_p(stream), int(bool(ret)), int(row_bytes),
                              send_x.data_ptr(), send_e.data_ptr() if send_e is not None else None,
                              ia(send_base), send_cnt.data_ptr(), recv_x.data_ptr(),
                              recv_e.data_ptr() if recv_e is not None else None, ia(recv_base),
-                             ia(recv_cap), recv_cnt.data_ptr(), ia(cap_rows), ia(in_cap_rows))
+                             ia(recv_cap), recv_cnt.data_ptr(), ia(cap_rows), ia(in_cap_rows),
+                             int(send_cap))
         if r != 0:
             raise RuntimeError(f"IPC expert exchange failed ({r})")
 
-    def error(self) -> bool:
-        """A captured wait ran out of its budget (DLI_IPC_WAIT_S): a peer stopped."""
-        return lib().dli_ipc_error(self._h) == 1
+    def error(self) -> int:
+        """Error bits raised by this rank's queue so far (0 = healthy): ``ERR_WAIT`` a bounded
+        wait ran out of budget (a peer stopped), ``ERR_SEQ`` a message's sequence number or
+        size did not match (stale / lost / mis-ordered), ``ERR_ABORT`` the ring was aborted.
+        One load of a pinned host word: cheap enough for every tick."""
+        return int(lib().dli_ipc_error(self._h))
+
+    def set_wait(self, seconds: float) -> None:
+        """Budget of the wait kernels enqueued from now on."""
+        lib().dli_ipc_set_wait(self._h, float(seconds))
+
+    def debug_bump_seq(self, peer: int, stream: int, d: int = 1) -> None:
+        """Test hook: the next message to ``peer`` carries a wrong sequence number."""
+        r = lib().dli_ipc_debug_bump_seq(self._h, ctypes.c_void_p(stream), int(peer), int(d))
+        if r != 0:
+            raise RuntimeError(f"IPC bump failed ({r})")
 
     def stats(self) -> Dict[str, int]:
         out = (ctypes.c_longlong * 3)()

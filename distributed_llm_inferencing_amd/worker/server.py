@@ -241,50 +241,48 @@ class WorkerState:
             eng = eng or self._pipe_engine
             self._pipe_engine = None
             try:
-                if eng is not None:
-                    eng.channel.close()
-                import torch.distributed as dist
-                if dist.is_initialized():
-                    dist.destroy_process_group()
+                self._abort_ring(eng)
             except Exception as e2:  # noqa: BLE001
                 log.warning("pipeline teardown after a failed join: %s", e2)
 
     def _abort_ring(self, eng) -> None:
-        """Tear down a broken ring's transports + process group without a goodbye: IPC
-        mailboxes are released (a queue blocked on a dead peer drains), RCCL communicators
-        are aborted rather than destroyed (a destroy would wait on the dead rank)."""
+        """Tear down a broken ring's transports + process group without a goodbye: the data
+        plane is aborted (IPC mailboxes sticky-failed with every flag set, a direct RCCL
+        communicator ncclCommAbort'ed), the compute stream is drained with a bound (the
+        channel re-aborts while it waits), and the torch process group is aborted through
+        the public ``ProcessGroup.abort()`` rather than destroyed (a destroy would wait on
+        the dead rank). Called WITHOUT the worker lock: /health and a re-forming
+        ``/load_shard`` stay responsive meanwhile."""
         import torch.distributed as dist
         ch = getattr(eng, "channel", None) if eng is not None else None
-        ipc = getattr(ch, "ipc", None)
-        if ipc is not None and hasattr(ipc, "abort"):
+        if ch is not None:
             try:
-                ipc.abort()
-            except Exception as e:  # noqa: BLE001
-                log.warning("ipc abort: %s", e)
-        try:
-            if ch is not None:
+                if ch.dead_peer is None:
+                    ch.dead_peer = "ring aborted by the worker"
+                ch.abort_data_plane()
+                if not ch.drain(timeout_s=10.0):
+                    log.warning("compute stream did not drain within 10 s after the abort")
                 ch.close()
-        except Exception as e:  # noqa: BLE001
-            log.warning("channel close after a ring failure: %s", e)
+            except Exception as e:  # noqa: BLE001
+                log.warning("channel teardown after a ring failure: %s", e)
         if dist.is_initialized():
             try:
                 if dist.get_backend() == "nccl":
-                    from torch.distributed.distributed_c10d import _abort_process_group
-                    _abort_process_group()
-                else:
-                    dist.destroy_process_group()
+                    dist.group.WORLD.abort()
+                dist.destroy_process_group()
             except Exception as e:  # noqa: BLE001
                 log.warning("process group teardown after a ring failure: %s", e)
 
     def _pipeline_failed(self, err) -> None:
         """Head's session raised (PipelineService.on_failure): abort the ring, keep serving
-        503s (the service keeps its error) until a new pipeline spec re-forms it."""
+        503s (the service keeps its error) until a new pipeline spec re-forms it. The abort
+        runs outside the worker lock (it drains a GPU stream)."""
         log.error("pipeline %s failed: %s", getattr(self, "pipeline_model", None), err)
         with self.lock:
-            self._abort_ring(self._pipe_engine)
-            self._pipe_engine = None
+            eng, self._pipe_engine = self._pipe_engine, None
             if self.pipeline is not None:
                 self.pipeline["state"], self.pipeline["error"] = "failed", str(err)
+        self._abort_ring(eng)
         if self.device.type == "cuda":
             torch.cuda.empty_cache()
 

@@ -107,8 +107,9 @@ def test_fifo_transport_orders_and_checks_sizes():
 
 
 # ------------------------------------------------------------------------------ pipeline
-def _pp_worker(rank, world, port, q, vp, mixed, chunk):
-    _env(rank, world, port, DLI_PP_VOCAB_PARALLEL=vp, DLI_MIXED_STEPS=mixed)
+def _pp_worker(rank, world, port, q, vp, mixed, chunk, schedule="piped"):
+    _env(rank, world, port, DLI_PP_VOCAB_PARALLEL=vp, DLI_MIXED_STEPS=mixed,
+         DLI_PP_SCHEDULE=schedule)
     import torch.distributed as dist
     from distributed_llm_inferencing_amd.parallel.pipeline import DistributedPipelineEngine
     eng = DistributedPipelineEngine("llama-tiny", "cpu", max_batch=4, max_model_len=64,
@@ -147,11 +148,16 @@ def _pp_worker(rank, world, port, q, vp, mixed, chunk):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,vp,mixed,chunk", [(2, "0", "1", 16384), (3, "0", "1", 16),
-                                                  (2, "1", "0", 16384), (4, "auto", "1", 16),
-                                                  (8, "auto", "1", 16), (8, "0", "0", 16384)])
-def test_pipeline_over_fifo_mailboxes_matches_single_stage(world, vp, mixed, chunk):
-    (res,) = _spawn(_pp_worker, world, vp, mixed, chunk)
+@pytest.mark.parametrize("world,vp,mixed,chunk,schedule", [
+    (2, "0", "1", 16384, "piped"), (3, "0", "1", 16, "piped"), (2, "1", "0", 16384, "piped"),
+    (4, "auto", "1", 16, "piped"), (8, "auto", "1", 16, "piped"), (8, "0", "0", 16384, "piped"),
+    # the grouped schedule of the torch / RCCL data plane (serve_session + the head's one
+    # grouped exchange per tick), through the same tag-blind FIFO model
+    (2, "0", "1", 16384, "grouped"), (3, "1", "1", 16, "grouped"),
+    (4, "auto", "1", 16, "grouped"), (8, "auto", "0", 16384, "grouped"),
+    (8, "0", "1", 16, "grouped")])
+def test_pipeline_over_fifo_mailboxes_matches_single_stage(world, vp, mixed, chunk, schedule):
+    (res,) = _spawn(_pp_worker, world, vp, mixed, chunk, schedule)
     eng = LLMEngine("llama-tiny", device="cpu", dtype=torch.float32, max_batch=8,
                     max_model_len=64, num_blocks=64)
     assert res[0] == [o.all_ids for o in eng.generate(PROMPTS, SamplingParams(
@@ -212,3 +218,114 @@ def test_expert_parallel_over_fifo_mailboxes_matches_dense(tmp_path, model, worl
         assert exch == steps * L and la
         assert syncs == steps + 1                    # the one lockstep exchange per step
         assert sent <= routed                        # no padding rows cross ranks
+
+
+# ------------------------------------------------------------------------------ hardening
+def _ep_overflow_worker(rank, world, port, q):
+    """Rank 0 'replays' a decode graph of bucket 8 holding 5 live rows (every row of the
+    bucket is routed), rank 1 is idle (an eager forward of zero rows): rank 1 must reserve a
+    region for rank 0's whole bucket, not for its 5 announced tokens."""
+    _env(rank, world, port, DLI_EP_COMM="ipc")
+    import torch.distributed as dist
+    from distributed_llm_inferencing_amd.parallel.expert import ExpertParallelEngine
+    eng = ExpertParallelEngine("mixtral-tiny", "cpu", max_batch=8, max_model_len=64,
+                               num_blocks=64, dtype=torch.float32)
+    moe = eng.moe
+    D = eng.cfg.hidden_size
+    lp = eng.engine.model.layers[0]
+    torch.manual_seed(3)
+    h = torch.randn(8, D)
+    out = {}
+    try:
+        if rank == 0:
+            # graph replay: the forward runs the padded bucket of 8 rows (a replay performs no
+            # host-side check; the lockstep exchange told the peers 5 tokens)
+            moe.begin_step([8, 0])
+            moe.static = True
+            y = moe(h, lp, 0)
+            moe.static = False
+            moe.begin_step([8, 0])           # the same rows, eagerly, as a reference
+            ref = moe(h, lp, 0)
+            out["equal"] = bool(torch.allclose(y, ref))
+        else:
+            moe.begin_step([5, 0])
+            moe(h[:0], lp, 0)
+            moe.begin_step([8, 0])
+            moe(h[:0], lp, 0)
+        out["ok"] = True
+    except Exception as e:  # noqa: BLE001
+        out["ok"] = f"{type(e).__name__}: {e}"
+    q.put((rank, out))
+    dist.barrier()
+    moe.close()
+    dist.destroy_process_group()
+
+
+def test_expert_receive_region_covers_a_replayed_bucket():
+    res = dict(_spawn(_ep_overflow_worker, 2, n_results=2))
+    assert res[0]["ok"] is True and res[1]["ok"] is True, res
+    assert res[0]["equal"]
+
+
+def _seq_worker(rank, world, port, q):
+    _env(rank, world, port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    from distributed_llm_inferencing_amd.parallel.fifo import (FifoMismatch,
+                                                               ShmMailboxTransport, mailbox_caps)
+    ep = ShmMailboxTransport(world, rank, mailbox_caps(world, 4096, 4096),
+                             f"/dli_fifo_s_{port}", timeout_s=20)
+    dist.barrier()
+    ep.connect()
+    dist.barrier()
+    out = {}
+    x = torch.arange(16, dtype=torch.int32)
+    buf = torch.empty(16, dtype=torch.int32)
+    if rank == 0:
+        ep.exchange([(x, 1)], [])
+        ep.debug_bump_seq(1)                 # the next message carries a wrong sequence
+        ep.exchange([(x, 1)], [])
+    else:
+        ep.exchange([], [(buf, 0)])
+        out["first"] = bool(torch.equal(buf, x))
+        try:
+            ep.exchange([], [(buf, 0)])
+            out["second"] = None
+        except FifoMismatch as e:
+            out["second"] = str(e)
+        out["err"] = ep.error()
+    q.put((rank, out))
+    dist.barrier()
+    ep.close()
+    dist.destroy_process_group()
+
+
+def test_mailbox_sequence_check_flags_a_bad_message():
+    """Every message carries its edge sequence number (ipc.cpp header); a receiver that
+    finds the wrong one (stale / lost / duplicated message) raises instead of delivering."""
+    res = dict(_spawn(_seq_worker, 2, n_results=2))
+    assert res[1]["first"]
+    assert "sequence" in res[1]["second"]
+    assert res[1]["err"] & 2
+
+
+def _resolve_worker(rank, world, port, q):
+    _env(rank, world, port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    from distributed_llm_inferencing_amd.parallel.transport import resolve_comm
+    g = dist.new_group(backend="gloo")
+    out = {"gpu": resolve_comm("auto", torch.device("cuda", 0), g),
+           "cpu": resolve_comm("auto", torch.device("cpu"), g),
+           "explicit": resolve_comm("torch", torch.device("cuda", 0), g)}
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_comm_auto_resolves_to_ipc_for_same_host_gpu_ranks():
+    """DLI_PP_COMM / DLI_EP_COMM default "auto": GPU ranks on one host take the device
+    mailboxes (the data plane the first 8-GPU run uses); CPU ranks keep torch/gloo."""
+    res = dict(_spawn(_resolve_worker, 2, n_results=2))
+    for r in (0, 1):
+        assert res[r] == {"gpu": "ipc", "cpu": "torch", "explicit": "torch"}

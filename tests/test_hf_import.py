@@ -128,3 +128,45 @@ def test_shard_model_from_hf_then_sharded_inference(tmp_path):
     hb = _hf_greedy(m.to(torch.bfloat16), IDS, 20)
     agree = sum(a == b for a, b in zip(out.all_ids, hb))
     assert agree >= 16, (out.all_ids, hb)
+
+
+@pytest.mark.parametrize("scaling", [
+    {"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0, "high_freq_factor": 4.0,
+     "original_max_position_embeddings": 16},
+    {"rope_type": "linear", "factor": 4.0}])
+def test_rope_scaling_matches_hf(tmp_path, scaling):
+    """A Llama-3.1-style ``rope_scaling`` (llama3: long wavelengths divided by the factor,
+    the band between smoothed; linear) changes every attention score past the first
+    positions; it is absorbed into our cos/sin table and must give HF's logits. The same
+    checkpoint read WITHOUT the scaling must not (the test has teeth)."""
+    import dataclasses
+    import transformers as tf
+    cfg = get_config("llama-tiny")
+    kw = dict(vocab_size=cfg.vocab_size, hidden_size=cfg.hidden_size,
+              intermediate_size=cfg.intermediate_size, num_hidden_layers=cfg.num_layers,
+              num_attention_heads=cfg.num_heads, num_key_value_heads=cfg.num_kv_heads,
+              head_dim=cfg.head_dim, rms_norm_eps=cfg.norm_eps, max_position_embeddings=256,
+              bos_token_id=1, eos_token_id=2, tie_word_embeddings=False)
+    c = tf.LlamaConfig(rope_scaling=dict(scaling, rope_theta=10000.0), rope_theta=10000.0, **kw)
+    torch.manual_seed(4)
+    m = tf.LlamaForCausalLM(c).float().eval()
+    m.save_pretrained(str(tmp_path / "ck"), safe_serialization=True)
+    c2, params = load_hf_dir(tmp_path / "ck", dtype=torch.float32)
+    assert dict(c2.rope_scaling).get("factor") == scaling["factor"]
+    ids = [(7 * i + 3) % cfg.vocab_size for i in range(60)]
+    with torch.no_grad():
+        ref = m(torch.tensor([ids])).logits[0, -1]
+    ours = our_last_logits(c2, params, ids)
+    assert torch.allclose(ours, ref, atol=2e-4, rtol=1e-3), (ours - ref).abs().max()
+    plain = our_last_logits(dataclasses.replace(c2, rope_scaling=()), params, ids)
+    assert not torch.allclose(plain, ref, atol=2e-4, rtol=1e-3)
+
+
+def test_unsupported_rope_scaling_and_sliding_window():
+    base = {"model_type": "mistral", "hidden_size": 64, "num_attention_heads": 4,
+            "num_hidden_layers": 2, "intermediate_size": 128, "vocab_size": 100,
+            "max_position_embeddings": 32768}
+    with pytest.raises(ValueError, match="unsupported rope_scaling"):
+        config_from_hf(dict(base, rope_scaling={"rope_type": "yarn", "factor": 4.0}), "x")
+    c = config_from_hf(dict(base, sliding_window=4096), "x")
+    assert c.max_position == 4096          # context capped at the window, not silently wrong

@@ -99,6 +99,34 @@ def test_gemm_256x224_pingpong(gpu, M, N, K, epi, tile):
         close(out, ref, rtol=2e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("tile", [34, 35, 36, 37, 41, 42])
+@pytest.mark.parametrize("M,N,K,epi", [(2048, 6144, 4096, "none"), (4096, 4096, 4096, "none"),
+                                       (8192, 28672, 4096, "silu_mul"),
+                                       (16384, 4096, 14336, "none"), (512, 28672, 4096, "silu_mul"),
+                                       (1100, 4096, 14336, "none"), (777, 50257, 4096, "f32"),
+                                       (300, 2304, 768, "bias_gelu")])
+def test_gemm_4wave_256(gpu, M, N, K, epi, tile):
+    """The one-wave-per-SIMD 256x256 kernel (tiles 34-37: AGPR-pinned accumulators, buffer
+    LDS-DMA with range-checked rows) at the prefill token buckets of the Llama-3-8B
+    projections (QKV / O / gate-up / down), a decode batch, partial row and column tiles
+    (M = 1100 / 777 / 300, N = 50257) and every epilogue, split-K 1/2/4, against the fp32
+    reference."""
+    torch.manual_seed(11)
+    x, w = rnd(M, K, dev=gpu), rnd(N, K, dev=gpu, scale=0.05)
+    bias = rnd(N, dev=gpu) if epi == "bias_gelu" else None
+    if epi == "silu_mul":
+        ref = R.silu_mul(R.linear(x, w).float().to(BF))
+    elif epi == "bias_gelu":
+        ref = R.gelu_tanh(R.linear(x, w).float() + bias.float())
+    else:
+        ref = R.linear(x, w, out_dtype=torch.float32)
+    for splits in (1, 2, 4):
+        if K % (64 * splits) or (splits > 1 and M * N > (1 << 27)):
+            continue
+        out = ops._gemm_native(x, w, epi, plan=G.GemmPlan("dli", tile, splits), bias=bias)
+        close(out, ref, rtol=2e-2, atol=2e-2)
+
+
 @pytest.mark.parametrize("M", [1, 2, 3, 4])
 @pytest.mark.parametrize("N,K,epi", [(6144, 4096, "none"), (4096, 14336, "none"),
                                      (28672, 4096, "silu_mul"), (50257, 768, "f32"),

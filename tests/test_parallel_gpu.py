@@ -32,13 +32,18 @@ def _env(rank, world, port, **extra):
 
 
 def _pp_worker(rank, world, port, q, vp, comm="torch"):
-    _env(rank, world, port, DLI_PP_VOCAB_PARALLEL=vp, DLI_PP_COMM=comm)
+    # comm "auto": no data-plane override at all (the default must resolve to the mailboxes)
+    _env(rank, world, port, DLI_PP_VOCAB_PARALLEL=vp,
+         **({} if comm == "auto" else {"DLI_PP_COMM": comm}))
+    if comm == "auto":
+        os.environ.pop("DLI_PP_COMM", None)
     import torch.distributed as dist
     from distributed_llm_inferencing_amd.parallel.pipeline import DistributedPipelineEngine
     eng = DistributedPipelineEngine("llama-tiny", "cuda", max_batch=8, max_model_len=64,
                                     num_blocks=256)
     x0 = 0
-    if comm == "ipc":
+    if comm == "auto":
+        assert eng.channel.comm == "ipc" and eng.channel.ipc.mem_kind == "uncached"
         eng.warmup()                  # captures the receive / send into the decode graphs
         x0 = eng.channel.exchanges    # captured calls counted once, at capture
     if rank == 0:
@@ -49,7 +54,7 @@ def _pp_worker(rank, world, port, q, vp, comm="torch"):
         q.put(res)
     else:
         eng.serve()
-    if rank != 0 and comm == "ipc":
+    if rank != 0 and comm == "auto":
         from distributed_llm_inferencing_amd.engine.batch import DECODE, PREFILL
         run = eng.stage.runner
         q.put(("stage", rank, run.piped is not None, run.replays, run.uploads,
@@ -68,7 +73,7 @@ def _run(target, world, *args):
     for p in procs:
         p.start()
     try:
-        n = world if (target in (_ep_worker, _ep_ipc_worker) or "ipc" in args) else 1
+        n = world if (target in (_ep_worker, _ep_ipc_worker) or "auto" in args) else 1
         res = [q.get(timeout=240) for _ in range(n)]
     finally:
         for p in procs:
@@ -99,11 +104,12 @@ def test_pipeline_two_ranks_on_gpu_match_single_stage(gpu, vp):
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("world,vp", [(2, "0"), (2, "1"), (4, "0"), (4, "1")])
 def test_pipeline_over_ipc_mailboxes_on_gpu(gpu, world, vp):
-    """The device data plane with N ranks on ONE GPU: every activation / token / candidate
-    message goes through hipIpc-mapped mailboxes (stream-ordered copies +
-    hipStreamWaitValue64 / WriteValue64 semaphores, csrc/runtime/ipc.cpp), token-identical
-    to the single-stage engine."""
-    out = _run(_pp_worker, world, vp, "ipc")
+    """The DEFAULT data plane (no DLI_PP_COMM) with N ranks on ONE GPU resolves to the
+    device mailboxes: every activation / token / candidate message goes through
+    hipIpc-mapped uncached mailboxes (stream-ordered put / get kernels with sequence-checked
+    headers, bounded wait / signal kernels, csrc/runtime/ipc.cpp), token-identical to the
+    single-stage engine."""
+    out = _run(_pp_worker, world, vp, "auto")
     (res,) = [x for x in out if x[0] != "stage"]
     stages = [x for x in out if x[0] == "stage"]
     assert len(stages) == world - 1
@@ -128,7 +134,7 @@ def test_pipeline_over_ipc_mailboxes_on_gpu(gpu, world, vp):
 
 
 def _ep_worker(rank, world, port, q):
-    _env(rank, world, port)
+    _env(rank, world, port, DLI_EP_COMM="torch")
     import torch.distributed as dist
     from distributed_llm_inferencing_amd.parallel.expert import ExpertParallelEngine
     eng = ExpertParallelEngine("mixtral-tiny", "cuda", max_batch=8, max_model_len=64,
@@ -159,11 +165,13 @@ def test_expert_parallel_two_ranks_on_gpu_match_dense(gpu):
 
 
 def _ep_ipc_worker(rank, world, port, q):
-    _env(rank, world, port, DLI_EP_COMM="ipc")
+    _env(rank, world, port)
+    os.environ.pop("DLI_EP_COMM", None)          # the default must resolve to the mailboxes
     import torch.distributed as dist
     from distributed_llm_inferencing_amd.parallel.expert import ExpertParallelEngine
     eng = ExpertParallelEngine("mixtral-tiny", "cuda", max_batch=8, max_model_len=64,
                                num_blocks=64)
+    assert eng.comm == "ipc" and eng.moe.ep.mem_kind == "uncached"
     eng.warmup()                      # every decode bucket captured, exchanges included
     mine = PROMPTS[rank::world]
     out = [o.all_ids for o in eng.generate(mine, GREEDY)]
