@@ -1189,6 +1189,15 @@ __global__ void __launch_bounds__(512) gemm8p128_kernel(
   }
 }
 
+// 16-B buffer load of `base` (a range-checked descriptor over `nbytes`: lanes past it read
+// zeros) straight into LDS at the wave-uniform `lds` + 16 * lane; voff per lane, soff uniform
+__device__ __forceinline__ void buf_lds16(const void* base, int nbytes, char* lds, int voff,
+                                          int soff) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, nbytes, 0x00020000);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds, 16, voff, soff, 0, 0);
+}
+
 // ---------------------------------------------------------------------------------------
 // 256x256 GEMM with ONE wave per SIMD and 128x128 wave tiles ("4-wave"): the structure of
 // the library kernels the prefill projections used to fall back to (hipBLASLt's
@@ -1263,10 +1272,11 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(
   // & 7: only the parity of i changes the lane's offset, the rest is the scalar soffset
   // i * 8 rows + K-tile. Rows past the matrix read as zeros (buffer range check) instead of
   // needing a clamped address per row, so a lane keeps 4 offset VGPRs, not 16 pointers.
-  const __amdgpu_buffer_rsrc_t a_rs = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(Ab + (long)m0 * lda), 0, min(Mg - m0, BM) * lda * 2, 0x00020000);
-  const __amdgpu_buffer_rsrc_t w_rs = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(Wg + (long)n0 * ldw), 0, min(N - n0, BN) * ldw * 2, 0x00020000);
+  // (the descriptors are built inside buf_lds16: a lambda capturing an
+  // __amdgpu_buffer_rsrc_t made hipcc drop the kernel's host-side handle)
+  const u16* a_base = Ab + (long)m0 * lda;
+  const u16* w_base = Wg + (long)n0 * ldw;
+  const int a_bytes = min(Mg - m0, BM) * lda * 2, w_bytes = min(N - n0, BN) * ldw * 2;
   const int prow = 64 * wid + (lane >> 3);
   const int ce = (lane & 7) ^ ((lane >> 4) & 7), co = (lane & 7) ^ (((lane >> 4) + 4) & 7);
   const int a_off[2] = {prow * lda * 2 + (kb + ce * 8) * 2, prow * lda * 2 + (kb + co * 8) * 2};
@@ -1292,13 +1302,11 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(
     const int i = f & 7;
     if (f < 8) {
       if (ka >= 0)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            a_rs, (lds_void*)(abase(ka) + (64 * wid + 8 * i) * 128), 16, a_off[i & 1],
-            i * 16 * lda + kpos(ka) * (BK * 2), 0, 0);
+        buf_lds16(a_base, a_bytes, abase(ka) + (64 * wid + 8 * i) * 128, a_off[i & 1],
+                  i * 16 * lda + kpos(ka) * (BK * 2));
     } else if (kw >= 0) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          w_rs, (lds_void*)(wbase(kw, ws) + (64 * wid + 8 * i) * 128), 16, w_off[i & 1],
-          i * 16 * ldw + kpos(kw) * (BK * 2), 0, 0);
+      buf_lds16(w_base, w_bytes, wbase(kw, ws) + (64 * wid + 8 * i) * 128, w_off[i & 1],
+                i * 16 * ldw + kpos(kw) * (BK * 2));
     }
   };
   auto stage = [&](int ka, int kw, int ws) {

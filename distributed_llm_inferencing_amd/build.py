@@ -134,8 +134,11 @@ def build(force: bool = False, jobs: int = 0, verbose: bool = True) -> dict:
     k_srcs, k_hdrs, _ = _group_sources("kernels")
     r_srcs, r_hdrs, _ = _group_sources("runtime")
     out = {}
+    # --no-undefined: a kernel whose host-side handle hipcc failed to emit (it happens
+    # silently, e.g. for a lambda capturing an __amdgpu_buffer_rsrc_t) fails the link here
+    # instead of the library failing to load on the GPU box
     out["kernels"] = _build_group(k_srcs, k_hdrs, KERNEL_FLAGS, LIBDIR / "libdli_kernels.so", jobs,
-                                  kind="kernels")
+                                  extra=("-Wl,--no-undefined",), kind="kernels")
     if r_srcs:
         out["runtime"] = _build_group(r_srcs, r_hdrs, RUNTIME_FLAGS, LIBDIR / "libdli_runtime.so",
                                       jobs, extra=("-lpthread",), kind="runtime")

@@ -121,6 +121,21 @@ def test_stage_death_redispatch_and_ring_reform(tmp_path):
                               data={"model_name": "llama-tiny", "prompt": f"recover {i} " * 3},
                               timeout=10)
             rids.append(r.json()["request_id"])
+        death = {}
+
+        def watch():                       # stage 2's exit -> the head answering 503
+            while procs[2].poll() is None:
+                time.sleep(0.02)
+            death["exit"] = time.time()
+            while time.time() - death["exit"] < 60:
+                try:
+                    if requests.get(f"{urls[0]}/health", timeout=2).status_code == 503:
+                        death["503"] = time.time()
+                        return
+                except Exception:  # noqa: BLE001
+                    pass
+                time.sleep(0.05)
+        threading.Thread(target=watch, daemon=True).start()
         t0 = time.time()
         while True:
             rows = [st.store.get_request(r) for r in rids]
@@ -130,6 +145,12 @@ def test_stage_death_redispatch_and_ring_reform(tmp_path):
             time.sleep(0.5)
         assert [x["status"] for x in rows] == ["completed"] * 12, rows
         assert procs[2].wait(timeout=60) == 17            # the injected stage death
+        # the ring watchdog (stage pid liveness on the control ring) fails the session within
+        # ~0.2 s of the death; /health answers 503 well inside the reference's 5 s probe
+        t1 = time.time()
+        while "503" not in death and time.time() - t1 < 30:
+            time.sleep(0.1)
+        assert "503" in death and death["503"] - death["exit"] < 5.0, death
         # some requests were retried: their first node was the broken ring
         assert any(int(x.get("attempts") or 1) > 1 for x in rows), rows
         h = requests.get(f"{urls[0]}/health", timeout=10)
