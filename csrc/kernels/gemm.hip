@@ -1198,6 +1198,14 @@ __device__ __forceinline__ void buf_lds16(const void* base, int nbytes, char* ld
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds, 16, voff, soff, 0, 0);
 }
 
+// 16-B buffer load of `base` into registers (same range-checked descriptor as buf_lds16)
+__device__ __forceinline__ uint4 buf_ld16(const void* base, int nbytes, int voff, int soff) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, nbytes, 0x00020000);
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+  return uint4{v[0], v[1], v[2], v[3]};
+}
+
 // ---------------------------------------------------------------------------------------
 // 256x256 GEMM with ONE wave per SIMD and 128x128 wave tiles ("4-wave"): the structure of
 // the library kernels the prefill projections used to fall back to (hipBLASLt's
@@ -1313,6 +1321,22 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(
 #pragma unroll
     for (int f = 0; f < 16; ++f) stage_piece(ka, kw, ws, f);
   };
+  // VAR 1024 (register staging): piece f of K-tile k is loaded into stg[f] (buffer_load to
+  // VGPRs, 64 per lane for a K-tile) and later written to LDS with one ds_write_b128 — the
+  // load / write pair issues in a fraction of an LDS-DMA's cost among MFMAs with ONE wave
+  // per SIMD (no partner wave hides the DMA issue, as the 8-wave ping-pong does)
+  constexpr bool RS = (VAR & 1024) != 0;
+  uint4 stg[16];
+  auto rs_load = [&](int k, int f) {
+    const int i = f & 7;
+    if (f < 8) stg[f] = buf_ld16(a_base, a_bytes, a_off[i & 1], i * 16 * lda + kpos(k) * (BK * 2));
+    else stg[f] = buf_ld16(w_base, w_bytes, w_off[i & 1], i * 16 * ldw + kpos(k) * (BK * 2));
+  };
+  auto rs_write = [&](int k, int f) {
+    const int i = f & 7;
+    char* dst = (f < 8 ? abase(k) : wbase(k, 0)) + (64 * wid + 8 * i) * 128 + lane * 16;
+    *reinterpret_cast<uint4*>(dst) = stg[f];
+  };
 
   const int fr = lane & 15, fq = lane >> 4;
   auto read_frag = [&](const char* part, int row, int kk) -> bf16x8 {
@@ -1346,7 +1370,8 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(
   // cycles: an LDS-DMA issue costs ~60 cycles among MFMAs, MI355X_MICROARCH.md constants).
   auto half = [&](const bf16x8 (&acur)[8], const bf16x8 (&bcur)[8], bf16x8 (&anext)[8],
                   bf16x8 (&bnext)[8], const char* na, const char* nw, int nkk, bool more,
-                  int ka, int kw, int ws) __attribute__((always_inline)) {
+                  int ka, int kw, int ws, int rw = -1, int rl = -1)
+      __attribute__((always_inline)) {
     if ((VAR & 2) && more) {                       // A/B: all 16 reads up front
 #pragma unroll
       for (int i = 0; i < 8; ++i) anext[i] = read_frag(na, arow + 16 * i, nkk);
@@ -1365,6 +1390,11 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(
           stage_piece(ka, kw, ws, q >> 2);
           __builtin_amdgcn_sched_barrier(0);
         }
+        if (RS && rw >= 0 && (q & 3) == 1) {        // write piece of rw, reload it with rl
+          rs_write(rw, q >> 2);
+          if (rl >= 0) rs_load(rl, q >> 2);
+          __builtin_amdgcn_sched_barrier(0);
+        }
         // one next-half fragment read after every 4th MFMA, pinned in place (the scheduler
         // hoisted all 16 above the first MFMA, whose lgkmcnt then waited on 2 of them), in
         // the order the next half consumes them: A0, B0..B7, A1..A7
@@ -1379,13 +1409,31 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(
 
   // ---- prologue. Plain: K-tiles 0 and 1 in flight. DEEP: A 0-1 and W 0-2 (issue order A0 W0
   // A1 W1 W2). Then the kk=0 fragments of K-tile 0 in registers.
-  if (nk > 0) stage(0, 0, 0);
-  if (nk > 1) stage(1, 1, 1);
-  if (DEEP && nk > 2) stage(-1, 2, 2);
-  if (DEEP && nk > 2) wait_vmcnt<24>();
-  else if (nk > 1) wait_vmcnt<16>();
-  else wait_vmcnt<0>();
-  barrier();
+  if (RS) {                                        // K-tiles 0, 1 into LDS, 2 in registers
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      if (k < nk) {
+#pragma unroll
+        for (int f = 0; f < 16; ++f) rs_load(k, f);
+#pragma unroll
+        for (int f = 0; f < 16; ++f) rs_write(k, f);
+      }
+    }
+    if (nk > 2) {
+#pragma unroll
+      for (int f = 0; f < 16; ++f) rs_load(2, f);
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);            // lgkmcnt(0): the writes landed
+    barrier();
+  } else {
+    if (nk > 0) stage(0, 0, 0);
+    if (nk > 1) stage(1, 1, 1);
+    if (DEEP && nk > 2) stage(-1, 2, 2);
+    if (DEEP && nk > 2) wait_vmcnt<24>();
+    else if (nk > 1) wait_vmcnt<16>();
+    else wait_vmcnt<0>();
+    barrier();
+  }
   bf16x8 a0[8], b0[8], a1[8], b1[8];
   if (nk > 0) {
     a0[0] = read_frag(abase(0), arow, 0);
@@ -1409,22 +1457,32 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(
     // only younger DMAs may be DEEP's W of kt+2 (issued last in the previous K-tile)
     if (!(VAR & 128)) {
       __builtin_amdgcn_s_waitcnt(0xC07F);          // lgkmcnt(0), seen by hipcc's counters
-      if (DEEP && kt + 2 < nk) wait_vmcnt<8>();
-      else wait_vmcnt<0>();
+      if (RS) {
+      } else if (DEEP && kt + 2 < nk) {
+        wait_vmcnt<8>();
+      } else {
+        wait_vmcnt<0>();
+      }
       barrier();
     }
-    // half 1: MFMAs on kk=1 of kt, reading kk=0 of kt+1; restage kt's buffers
+    // half 1: MFMAs on kk=1 of kt, reading kk=0 of kt+1; restage kt's buffers (register
+    // staging: write K-tile kt+2 from the registers, reload them with kt+3)
     const int ka = (sa && !(VAR & 64)) ? kt + 2 : -1;
     const int kw = (sw && !(VAR & 64)) ? kt + (DEEP ? 3 : 2) : -1;
-    if ((VAR & 4) && (ka >= 0 || kw >= 0)) stage(ka, kw, wsl);
-    half(a1, b1, a0, b0, abase(kt + 1), wbase(kt + 1, ws1), 0, true,
-         (VAR & 4) ? -1 : ka, (VAR & 4) ? -1 : kw, wsl);
+    if (RS) {
+      half(a1, b1, a0, b0, abase(kt + 1), wbase(kt + 1, ws1), 0, true, -1, -1, 0,
+           sa ? kt + 2 : -1, sw ? kt + 3 : -1);
+    } else {
+      if ((VAR & 4) && (ka >= 0 || kw >= 0)) stage(ka, kw, wsl);
+      half(a1, b1, a0, b0, abase(kt + 1), wbase(kt + 1, ws1), 0, true,
+           (VAR & 4) ? -1 : ka, (VAR & 4) ? -1 : kw, wsl);
+    }
     wsl = ws1;
   };
   using T_ = std::integral_constant<bool, true>;
   using F_ = std::integral_constant<bool, false>;
   int kt = 0;
-  if (DEEP) {
+  if (DEEP || RS) {                                // RS: SA = write kt+2, SW = load kt+3
     for (; kt + 3 < nk; ++kt) ktile(T_{}, T_{}, kt);
     if (kt + 2 < nk) { ktile(T_{}, F_{}, kt); ++kt; }
   } else {
@@ -1891,6 +1949,9 @@ static int dispatch_tile(int tile_cfg, const void* A, int lda, const void* W, in
     case 37: return launch_4w<EPI, 8 | 3>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
     // 41: 34 with the deep weight ring (3 W stages, 160 KiB LDS), 42: 41 + stagger-U
     case 41: return launch_4w<EPI, 8 | 32>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
+    // 43: 34 with register staging (buffer_load -> VGPRs -> ds_write), 44: 43 + stagger-U
+    case 43: return launch_4w<EPI, 8 | 1024>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
+    case 44: return launch_4w<EPI, 8 | 1024 | 1>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
     case 42: return launch_4w<EPI, 8 | 32 | 1>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
     // 40: 34 with the K-tile's LDS-DMA issued in one burst (the first schedule, for A/B)
     case 40: return launch_4w<EPI, 8 | 4>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);

@@ -53,7 +53,10 @@ TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256), 4: (256, 128),
          34: (256, 256), 35: (256, 256), 36: (256, 256), 37: (256, 256),
          # 34 with a 3-stage weight ring (160 KiB LDS: W fetched a K-tile further ahead for
          # decode-sized GEMMs that stream their weights from HBM), 42 = 41 + stagger-U
-         41: (256, 256), 42: (256, 256)}
+         41: (256, 256), 42: (256, 256),
+         # 34 with register staging (buffer_load -> VGPRs -> ds_write_b128 instead of LDS-DMA),
+         # 44 = 43 + stagger-U
+         43: (256, 256), 44: (256, 256)}
 # weight-streaming skinny GEMM (gemm.hip gemv_kernel) for M <= GEMV_MAX_M rows: 16 / 32 output
 # rows per workgroup (31 for the SiLU*up gate/up pairing); not an MFMA tile, so kept apart
 GEMV_TILES = {30: 16, 31: 32, 32: 16, 33: 32}   # 32 / 33: 4 K-steps in flight per lane, M = 1
@@ -409,6 +412,13 @@ def prefill_candidates(M: int, N: int, K: int, epi: str):
     (profiles/r3/prefill_gemm/); ``DLI_GEMM_NO_BLAS=1`` or ``DLI_TUNE_PREFILL_BLAS=0`` keeps
     every prefill GEMM on our kernels."""
     out = [_heuristic(M, N, K, epi)]
+    # the one-wave-per-SIMD 256x256 kernel with the deep weight ring (tile 41) at the same
+    # split: 1.0-2.5 % faster than the 8-phase tile on QKV / gate-up / square prefill shapes,
+    # ~5 % slower on the long-K down projection (profiles/r4/gemm4w/), so measured per shape
+    base = out[0]
+    if base.backend == "dli" and base.tile == 22 and \
+            "41" not in os.environ.get("DLI_GEMM_PREFILL_EXCLUDE", "").split(","):
+        out.append(GemmPlan("dli", 41, base.splits))
     if (epi in ("none", "splitk", "silu_mul", "f32")
             and os.environ.get("DLI_GEMM_NO_BLAS", "0") != "1"
             and os.environ.get("DLI_TUNE_PREFILL_BLAS", "1") == "1"
@@ -425,7 +435,7 @@ def candidate_plans(M: int, N: int, K: int, epi: str):
     # the bench 0.3-0.7 % lower in three same-box A/B runs (profiles/r2_s2/README.md)
     # 27 is tile 22 with the round-1 wait schedule (A/B reference only)
     excl_env = os.environ.get("DLI_GEMM_EXCLUDE")
-    excl = {int(t) for t in (excl_env if excl_env is not None else "26,27,35,36,37,41,42").split(",")
+    excl = {int(t) for t in (excl_env if excl_env is not None else "26,27,35,36,37,41,42,43,44").split(",")
             if t.strip()}
     # ... except where 256x256 tiles take more than one wave of the chip and 256x224 tiles
     # land on a whole number of waves (Llama-3-70B gate/up at M = 512: N = 57344 is 448

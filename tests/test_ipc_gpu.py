@@ -79,7 +79,8 @@ def _ep_worker(rank, world, port, q):
         ep.exchange([(x, nxt)], [(buf, prv)], st)           # flight: the mailbox holds one)
         ep.exchange([(odd, nxt)], [(obuf, prv)], st)
     torch.cuda.synchronize()
-    out["data"] = bool(torch.equal(buf.float(), torch.arange(4096, device=dev).float() + 7 * prv)
+    want = (torch.arange(4096, dtype=torch.float32, device=dev) + 7 * prv).to(torch.bfloat16)
+    out["data"] = bool(torch.equal(buf, want)
                        and torch.equal(obuf, torch.arange(13, dtype=torch.int32,
                                                           device=dev)[1:] + prv))
     out["err0"] = ep.error()
