@@ -31,8 +31,13 @@ typedef __attribute__((address_space(3))) void lds_void;
 typedef const __attribute__((address_space(1))) void gbl_void;
 
 __device__ __forceinline__ float silu_f(float x) { return x / (1.f + __expf(-x)); }
+// tanh-approximate GELU, branch-free: 0.5 (1 + tanh(y)) = sigmoid(2 y). tanhf's range
+// branches made a 256-accumulator epilogue too large to unroll, and the rolled loop indexed
+// the accumulators dynamically: hipcc demoted them to scratch and copied them out of the
+// AGPRs inside the K loop, where no hazard padding follows an inline-asm MFMA
 __device__ __forceinline__ float gelu_f(float x) {
-  return 0.5f * x * (1.f + tanhf(0.7978845608028654f * (x + 0.044715f * x * x * x)));
+  const float y2 = 1.5957691216057308f * (x + 0.044715f * x * x * x);
+  return x / (1.f + __expf(-y2));
 }
 
 template <int EPI>

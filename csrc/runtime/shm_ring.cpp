@@ -24,6 +24,7 @@
 
 #include <atomic>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <string>
 
@@ -84,9 +85,20 @@ inline double now_s() {
   return ts.tv_sec + 1e-9 * ts.tv_nsec;
 }
 
+// A process that exited but was not reaped yet (a zombie: its parent — a launcher blocked
+// elsewhere — has not waited for it) still answers kill(pid, 0): read its state too.
 inline bool pid_alive(int64_t pid) {
   if (pid <= 0) return true;
-  return kill((pid_t)pid, 0) == 0 || errno == EPERM;
+  if (!(kill((pid_t)pid, 0) == 0 || errno == EPERM)) return false;
+  char path[64], buf[512];
+  snprintf(path, sizeof path, "/proc/%lld/stat", (long long)pid);
+  FILE* f = fopen(path, "r");
+  if (!f) return true;                             // no procfs: trust kill()
+  const size_t n = fread(buf, 1, sizeof buf - 1, f);
+  fclose(f);
+  buf[n] = 0;
+  const char* rp = strrchr(buf, ')');              // "pid (comm) S ..." — comm may hold ')'
+  return !(rp && rp[1] == ' ' && (rp[2] == 'Z' || rp[2] == 'X'));
 }
 
 // Adaptive wait: spin briefly (the common case: the message is already there), then yield,

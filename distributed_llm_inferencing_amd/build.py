@@ -64,17 +64,45 @@ def _digest(paths, flags) -> str:
     return h.hexdigest()
 
 
+# Kernels whose MFMAs are inline asm: hipcc pads no hazard after an asm statement, so any
+# compiler-made copy of their accumulators inside the K loop (a scratch spill, a rolled
+# epilogue indexing them dynamically) reads AGPRs an MFMA may still be writing. Such a
+# kernel must keep its accumulators in registers: a nonzero scratch size fails the build.
+ASM_MFMA_KERNELS = ("gemm4w_kernel",)
+_REMARKS = "-Rpass-analysis=kernel-resource-usage"
+
+
+def check_scratch(stderr: str, src: str) -> None:
+    """Raise if a kernel named in ASM_MFMA_KERNELS reports scratch (hipcc resource remarks)."""
+    fn = None
+    for line in stderr.splitlines():
+        if "remark:" not in line:
+            continue
+        body = line.split("remark:", 1)[1].strip()
+        if body.startswith("Function Name:"):
+            fn = body.split(":", 1)[1].strip()
+        elif body.startswith("ScratchSize") and fn and any(k in fn for k in ASM_MFMA_KERNELS):
+            size = int(body.split(":")[-1].split()[0])
+            if size:
+                raise RuntimeError(f"{src}: {fn} uses {size} B/lane of scratch: its inline-asm "
+                                   "MFMA accumulators would be copied without hazard padding")
+
+
 def _compile(src: Path, obj: Path, flags, headers) -> Path:
     stamp = obj.with_suffix(".sha1")
     dig = _digest([src, *headers], flags)
     if obj.exists() and stamp.exists() and stamp.read_text() == dig:
         return obj
     obj.parent.mkdir(parents=True, exist_ok=True)
-    cmd = [_hipcc(), *flags, "-I", str(CSRC / "kernels"), "-I", str(CSRC / "runtime"),
-           "-c", str(src), "-o", str(obj)]
+    remarks = src.suffix == ".hip" and any(k.split("_")[0] in src.read_text()
+                                           for k in ASM_MFMA_KERNELS)
+    cmd = [_hipcc(), *flags, *([_REMARKS] if remarks else []), "-I", str(CSRC / "kernels"),
+           "-I", str(CSRC / "runtime"), "-c", str(src), "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src.name}:\n{' '.join(cmd)}\n{r.stderr[-6000:]}")
+    if remarks:
+        check_scratch(r.stderr, src.name)
     stamp.write_text(dig)
     return obj
 

@@ -8,10 +8,11 @@ The projection GEMMs of a decode step are skinny (M = batch) and of a prefill st
   GEMM at M = 256': choose SPLITK so that tiles * SPLITK ~ 0.5-1x the CU count),
 * the backend: decode GEMMs (the hipGraph steps) always on our MFMA kernels, tiles
   autotuned at graph capture (on by default; ``DLI_GEMM_AUTOTUNE=0`` disables it). Prefill
-  GEMMs: our 8-phase 256x256 kernel or hipBLASLt (torch.matmul + our epilogue pass),
-  whichever the warmup measures faster per token bucket (``prefill_candidates``;
-  ``DLI_GEMM_NO_BLAS=1`` keeps everything on our kernels). ``DLI_GEMM_BACKEND=hipblaslt``,
-  ``DLI_GEMM_PREFILL_BLAS=1`` and ``DLI_GEMM_DECODE_BLAS=1`` remain as ablations.
+  GEMMs: our 8-phase 256x256 kernel or the one-wave-per-SIMD 256x256 kernel (tile 41),
+  whichever the warmup measures faster per token bucket (``prefill_candidates``). hipBLASLt
+  is off the hot path: ``DLI_TUNE_PREFILL_BLAS=1`` lets it compete in the prefill autotune,
+  ``DLI_GEMM_BACKEND=hipblaslt``, ``DLI_GEMM_PREFILL_BLAS=1`` and ``DLI_GEMM_DECODE_BLAS=1``
+  force it (ablations; ``DLI_GEMM_NO_BLAS=1`` vetoes all of them).
 
 Split-K partial slabs live in a grow-only per-device workspace; engines warm every shape
 up before hipGraph capture so no allocation happens inside a capture.
@@ -409,8 +410,9 @@ def prefill_candidates(M: int, N: int, K: int, epi: str):
     and RoPE/cache consumers run as their own kernels after either). At these sizes the GEMM
     is MFMA-bound, so the autotuner times them warm (``cold_bytes`` 1). Measured at
     M = 16384 on MI355X: ours 1.37-1.46 PF, hipBLASLt 1.57-1.62 PF on the plain projections
-    (profiles/r3/prefill_gemm/); ``DLI_GEMM_NO_BLAS=1`` or ``DLI_TUNE_PREFILL_BLAS=0`` keeps
-    every prefill GEMM on our kernels."""
+    (profiles/r3/prefill_gemm/). Not a candidate by default since round 4: with tile 41 in
+    the autotune the whole b512 bench lost 0.35 % without it (43,820 -> 43,665 tok/s, same
+    box, profiles/r4/README.md); ``DLI_TUNE_PREFILL_BLAS=1`` restores it."""
     out = [_heuristic(M, N, K, epi)]
     # the one-wave-per-SIMD 256x256 kernel with the deep weight ring (tile 41) at the same
     # split: 1.0-2.5 % faster than the 8-phase tile on QKV / gate-up / square prefill shapes,
@@ -421,7 +423,7 @@ def prefill_candidates(M: int, N: int, K: int, epi: str):
         out.append(GemmPlan("dli", 41, base.splits))
     if (epi in ("none", "splitk", "silu_mul", "f32")
             and os.environ.get("DLI_GEMM_NO_BLAS", "0") != "1"
-            and os.environ.get("DLI_TUNE_PREFILL_BLAS", "1") == "1"
+            and os.environ.get("DLI_TUNE_PREFILL_BLAS", "0") == "1"
             and out[0].backend != "hipblaslt"):
         out.append(GemmPlan("hipblaslt", 0, 1))
     return out
@@ -433,9 +435,11 @@ def candidate_plans(M: int, N: int, K: int, epi: str):
     # Default: 26 (256x224). It fills all 256 CUs on the gate/up GEMM and wins the isolated
     # autotune (98.8 vs ~106 us), but in the decode step it ran 97.9 vs 99.0 us per call and
     # the bench 0.3-0.7 % lower in three same-box A/B runs (profiles/r2_s2/README.md)
-    # 27 is tile 22 with the round-1 wait schedule (A/B reference only)
+    # 27 is tile 22 with the round-1 wait schedule (A/B reference only); 35-37, 42-44 are
+    # 4-wave variants measured slower everywhere (profiles/r4/gemm4w/); 41 competes (its deep
+    # weight ring streamed the M = 512 LM head 4-7 % faster than tile 22)
     excl_env = os.environ.get("DLI_GEMM_EXCLUDE")
-    excl = {int(t) for t in (excl_env if excl_env is not None else "26,27,35,36,37,41,42,43,44").split(",")
+    excl = {int(t) for t in (excl_env if excl_env is not None else "26,27,35,36,37,42,43,44").split(",")
             if t.strip()}
     # ... except where 256x256 tiles take more than one wave of the chip and 256x224 tiles
     # land on a whole number of waves (Llama-3-70B gate/up at M = 512: N = 57344 is 448

@@ -114,7 +114,9 @@ def test_ipc_mailboxes_uncached_sequenced_and_sticky(gpu):
     assert res[1]["err1"] & 2, res[1]                 # the corrupted message was flagged
     # the flagged rank stops signalling; its peer's next wait runs out of budget (5 s) or
     # the queue is released, never a hang
-    assert res[0]["err1"] in (0, 1), res[0]
+    # (its first message still landed; its next waits run out of budget: bit 0, and the
+    # stale mailbox it then reads is flagged too: bit 1)
+    assert res[0]["err1"] in (0, 1, 3), res[0]
     assert res[1]["drain_s"] < 10 and res[0]["drain_s"] < 10, res
 
 

@@ -123,8 +123,14 @@ def test_gemm_4wave_256(gpu, M, N, K, epi, tile):
     for splits in (1, 2, 4):
         if K % (64 * splits) or (splits > 1 and M * N > (1 << 27)):
             continue
-        out = ops._gemm_native(x, w, epi, plan=G.GemmPlan("dli", tile, splits), bias=bias)
-        close(out, ref, rtol=2e-2, atol=2e-2)
+        for rep in range(3):              # a schedule race shows up as an intermittent tile
+            out = ops._gemm_native(x, w, epi, plan=G.GemmPlan("dli", tile, splits), bias=bias)
+            err = (out.float() - ref.float()).abs()
+            bad = err > 2e-2 + 2e-2 * ref.float().abs().max()
+            assert not bool(bad.any()), (
+                f"tile {tile} split {splits} rep {rep}: {int(bad.sum())} bad elements, rows "
+                f"{torch.unique(torch.nonzero(bad)[:, 0])[:16].tolist()}, cols "
+                f"{torch.unique(torch.nonzero(bad)[:, 1])[:16].tolist()}, max {float(err.max())}")
 
 
 @pytest.mark.parametrize("M", [1, 2, 3, 4])

@@ -205,6 +205,34 @@ def test_shm_ring_broadcast_order_backpressure_and_dead_producer():
         x.destroy()
 
 
+def _open_ring_and_exit(name):
+    from distributed_llm_inferencing_amd.runtime import ShmRing
+    ShmRing.open(name, 0)
+    os._exit(0)
+
+
+def test_shm_ring_reports_an_unreaped_consumer_as_dead():
+    """A stage that exited while its launcher is blocked elsewhere stays a zombie (kill(pid,
+    0) still succeeds): the ring's liveness check reads its state and reports it dead."""
+    import multiprocessing as mproc
+    import time
+    from distributed_llm_inferencing_amd.runtime import ShmRing
+    name = f"/dli_ztest_{os.getpid()}"
+    r = ShmRing.create(name, 4, 256, 1)
+    assert r.dead() == -1                          # never opened: counts as alive
+    p = mproc.get_context("fork").Process(target=_open_ring_and_exit, args=(name,))
+    p.start()
+    t0 = time.monotonic()
+    while r.dead() != 0 and time.monotonic() - t0 < 10:
+        time.sleep(0.05)
+    try:
+        assert r.dead() == 0                       # the child is a zombie: not reaped yet
+    finally:
+        p.join()
+        r.unlink()
+        r.destroy()
+
+
 def test_decode_core_matches_python_scheduler():
     """The C++ decode fast path (DecodeCore) builds the same step metadata and applies
     tokens exactly like the numpy path, including finishing rows and preemption."""
@@ -275,14 +303,22 @@ def test_prefill_gemm_plan_is_own_kernel(monkeypatch):
     assert G.plan(16384, 28672, 4096, "silu_mul").backend == "dli"
     G.clear_plans()
     monkeypatch.delenv("DLI_GEMM_PREFILL_BLAS")
-    # prefill autotune (StageRunner.autotune_prefill): our 8-phase plan vs hipBLASLt
+    # prefill autotune (StageRunner.autotune_prefill): our 8-phase plan vs our 4-wave deep-W
+    # plan at the same split; hipBLASLt only when DLI_TUNE_PREFILL_BLAS=1 asks for it
     c = G.prefill_candidates(16384, 28672, 4096, "silu_mul")
-    assert c[0] == G.GemmPlan("dli", 22, 1) and c[1].backend == "hipblaslt"
-    assert [p.backend for p in G.prefill_candidates(2048, 4096, 4096, "splitk")] == \
-        ["dli", "hipblaslt"]
-    assert [p.backend for p in G.prefill_candidates(4096, 4096, 4096, "bias_gelu")] == ["dli"]
+    assert c == [G.GemmPlan("dli", 22, 1), G.GemmPlan("dli", 41, 1)]
+    assert G.prefill_candidates(2048, 4096, 4096, "splitk") == \
+        [G.GemmPlan("dli", 22, 2), G.GemmPlan("dli", 41, 2)]
+    assert all(p.backend == "dli" for p in G.prefill_candidates(4096, 4096, 4096, "bias_gelu"))
+    monkeypatch.setenv("DLI_TUNE_PREFILL_BLAS", "1")
+    assert [p.backend for p in G.prefill_candidates(16384, 6144, 4096, "none")] == \
+        ["dli", "dli", "hipblaslt"]
     monkeypatch.setenv("DLI_GEMM_NO_BLAS", "1")
-    assert [p.backend for p in G.prefill_candidates(16384, 6144, 4096, "none")] == ["dli"]
+    assert [p.backend for p in G.prefill_candidates(16384, 6144, 4096, "none")] == ["dli", "dli"]
+    monkeypatch.delenv("DLI_TUNE_PREFILL_BLAS")
+    # the 4-wave deep-W tile competes in the decode autotune too; its slower variants do not
+    tiles = {p.tile for p in G.candidate_plans(512, 4096, 4096, "none")}
+    assert 41 in tiles and not tiles & {35, 36, 37, 42, 43, 44}
     # decode QKV timing pins the candidate for the fused attention path, then restores
     p1, p4 = G.GemmPlan("dli", 30, 1), G.GemmPlan("dli", 32, 4)
     G.set_plan(1, 6144, 4096, "none", p4)
@@ -304,3 +340,20 @@ def test_slice_experts_releases_other_experts():
     assert s.shape[0] == 2 and torch.equal(s, t[2:4])
     assert s.untyped_storage().nbytes() == 2 * 16 * 4 * 4
     assert W.slice_experts("layers.0.attn_norm", t, (2, 4)) is t
+
+
+def test_build_refuses_scratch_in_asm_mfma_kernels():
+    """build.check_scratch: an inline-asm-MFMA kernel (gemm4w) that spills its accumulators
+    to scratch fails the build (hipcc pads no hazard after the asm; a rolled bias-GELU
+    epilogue did exactly this and returned intermittently wrong tiles); other kernels and a
+    zero scratch size pass."""
+    from distributed_llm_inferencing_amd import build
+    ok = ("gemm.hip:1:1: remark: Function Name: _Z13gemm4w_kernelILi3ELi9EEvPKti\n"
+          "gemm.hip:1:1: remark:     ScratchSize [bytes/lane]: 0\n"
+          "gemm.hip:1:1: remark: Function Name: _Z9other_kernelv\n"
+          "gemm.hip:1:1: remark:     ScratchSize [bytes/lane]: 64\n")
+    build.check_scratch(ok, "gemm.hip")
+    bad = ok + ("gemm.hip:1:1: remark: Function Name: _Z13gemm4w_kernelILi3ELi8EEvPKti\n"
+                "gemm.hip:1:1: remark:     ScratchSize [bytes/lane]: 1040\n")
+    with pytest.raises(RuntimeError, match="1040 B/lane"):
+        build.check_scratch(bad, "gemm.hip")
