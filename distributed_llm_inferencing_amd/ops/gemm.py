@@ -436,10 +436,11 @@ def candidate_plans(M: int, N: int, K: int, epi: str):
     # autotune (98.8 vs ~106 us), but in the decode step it ran 97.9 vs 99.0 us per call and
     # the bench 0.3-0.7 % lower in three same-box A/B runs (profiles/r2_s2/README.md)
     # 27 is tile 22 with the round-1 wait schedule (A/B reference only); 35-37, 42-44 are
-    # 4-wave variants measured slower everywhere (profiles/r4/gemm4w/); 41 competes (its deep
-    # weight ring streamed the M = 512 LM head 4-7 % faster than tile 22)
+    # 4-wave variants measured slower everywhere (profiles/r4/gemm4w/); 41 (prefill-only) won
+    # isolated decode timings (M = 512 LM head 4-7 %) but cost the step 1.8 % in a same-box
+    # bench A/B (42,548 without vs 41,790 / 41,653 tok/s with, profiles/r4/bench/)
     excl_env = os.environ.get("DLI_GEMM_EXCLUDE")
-    excl = {int(t) for t in (excl_env if excl_env is not None else "26,27,35,36,37,42,43,44").split(",")
+    excl = {int(t) for t in (excl_env if excl_env is not None else "26,27,35,36,37,41,42,43,44").split(",")
             if t.strip()}
     # ... except where 256x256 tiles take more than one wave of the chip and 256x224 tiles
     # land on a whole number of waves (Llama-3-70B gate/up at M = 512: N = 57344 is 448

@@ -155,7 +155,10 @@ def _pp_worker(rank, world, port, q, vp, mixed, chunk, schedule="piped"):
     # grouped exchange per tick), through the same tag-blind FIFO model
     (2, "0", "1", 16384, "grouped"), (3, "1", "1", 16, "grouped"),
     (4, "auto", "1", 16, "grouped"), (8, "auto", "0", 16384, "grouped"),
-    (8, "0", "1", 16, "grouped")])
+    (8, "0", "1", 16, "grouped"),
+    # every ring size up to a full node: odd sizes, the vocab-parallel head at 5-7 ranks
+    (5, "auto", "1", 16, "piped"), (6, "0", "1", 16384, "grouped"), (7, "auto", "0", 16, "piped"),
+    (5, "0", "0", 16, "grouped"), (6, "auto", "1", 16, "piped"), (7, "1", "1", 16384, "grouped")])
 def test_pipeline_over_fifo_mailboxes_matches_single_stage(world, vp, mixed, chunk, schedule):
     (res,) = _spawn(_pp_worker, world, vp, mixed, chunk, schedule)
     eng = LLMEngine("llama-tiny", device="cpu", dtype=torch.float32, max_batch=8,
