@@ -201,7 +201,35 @@ class StageRunner:
             add(m.params.get("head_slice"), "f32")
         return shapes, weights
 
+    def tune_lock(self):
+        """Ranks that share one GPU (same-device rehearsals: DLI_SAME_DEVICE=1) time their
+        GEMM candidates one process at a time: tuned concurrently, each plan was measured
+        under the other ranks' load and the pins came out at random (an expert-parallel rank
+        ran 947 us grouped GEMMs that take ~120 us alone). Engines that exchange data during
+        capture tune every bucket first, then barrier, then capture (no peer waits on a
+        tuning rank inside a bounded device wait)."""
+        import contextlib
+        if os.environ.get("DLI_SAME_DEVICE", "0") != "1" or self.device.type != "cuda":
+            return contextlib.nullcontext()
+
+        @contextlib.contextmanager
+        def held():
+            import fcntl
+            path = f"/tmp/dli_tune_{os.getuid()}_{self.device.index or 0}.lock"
+            with open(path, "w") as f:
+                fcntl.flock(f, fcntl.LOCK_EX)
+                try:
+                    torch.cuda.synchronize(self.device)
+                    yield
+                finally:
+                    fcntl.flock(f, fcntl.LOCK_UN)
+        return held()
+
     def autotune(self, buckets=None):
+        with self.tune_lock():
+            self._autotune(buckets)
+
+    def _autotune(self, buckets=None):
         from ..ops import gemm as G
         log = None
         if os.environ.get("DLI_GEMM_AUTOTUNE_LOG", "0") == "1":
@@ -238,12 +266,13 @@ class StageRunner:
         c = self.model.cfg
         qkv = (c.num_heads, c.num_kv_heads, c.head_dim) if c.arch != "gpt2" else None
         b = 2048
-        while b <= top:
-            shapes, weights = self.gemm_shapes(b)
-            shapes = [s for s in shapes if s[3] != "f32"]     # prefill's LM head: last rows
-            G.autotune(shapes, weights, self.device, iters=3, log=log, cold_bytes=1,
-                       qkv_heads=qkv, candidates=G.prefill_candidates)
-            b *= 2
+        with self.tune_lock():
+            while b <= top:
+                shapes, weights = self.gemm_shapes(b)
+                shapes = [s for s in shapes if s[3] != "f32"]     # prefill's LM head: last rows
+                G.autotune(shapes, weights, self.device, iters=3, log=log, cold_bytes=1,
+                           qkv_heads=qkv, candidates=G.prefill_candidates)
+                b *= 2
 
     def autotune_mixed(self, max_rows: int) -> None:
         """GEMM plans for mixed prefill+decode steps (a running batch's decode rows plus the

@@ -488,9 +488,15 @@ def moe_route(router_logits, k: int):
     return w, ids
 
 
-def moe_mlp(x, w_gu, w_down, topk_w, topk_ids, expert_offset: int = 0):
+def moe_mlp(x, w_gu, w_down, topk_w, topk_ids, expert_offset: int = 0,
+            plan_rows: Optional[int] = None):
     """Experts [expert_offset, expert_offset+E_local) of one MoE layer; returns the weighted
-    sum over the token's selected local experts (zeros for tokens routed elsewhere)."""
+    sum over the token's selected local experts (zeros for tokens routed elsewhere).
+    ``plan_rows``: the routed rows these experts typically receive, when ``x`` is a region
+    sized for the worst case (the expert-parallel receive region: every peer's bucket at
+    min(k, E/N) rows per token). The grouped-GEMM plan is looked up for it — the autotuned
+    key — instead of for the capacity, whose 4-8x larger row count mapped to 256-row tiles
+    (1 workgroup per CU) that streamed the experts at ~2 TB/s."""
     if not _use_native(x):
         return R.moe_mlp(x, w_gu, w_down, topk_w, topk_ids, expert_offset)
     T, D = x.shape
@@ -525,11 +531,15 @@ def moe_mlp(x, w_gu, w_down, topk_w, topk_ids, expert_offset: int = 0):
         out = torch.empty_like(x)
         _native_call("dli_moe_combine", _p(out), _p(y), _p(topk_w), _p(pos), T, k, D, _st())
         return out
+    p_gu = p_dn = None
+    if plan_rows is not None:
+        p_gu = G.grouped_plan(plan_rows, F2, D, "silu_mul", E_local)
+        p_dn = G.grouped_plan(plan_rows, D, F2 // 2, "none", E_local)
     _gemm_native(xp, w_gu, "silu_mul", out=act, groups=E_local, group_off=offsets,
-                 rows_per_group=n)
+                 rows_per_group=n, plan=p_gu)
     y = torch.empty(max(n, 1), D, dtype=x.dtype, device=dev)
     _gemm_native(act, w_down, "none", out=y, groups=E_local, group_off=offsets,
-                 rows_per_group=n)
+                 rows_per_group=n, plan=p_dn)
     out = torch.empty_like(x)
     _native_call("dli_moe_combine", _p(out), _p(y), _p(topk_w), _p(pos), T, k, D, _st())
     return out

@@ -155,7 +155,7 @@ class ExpertParallelMoE:
         if R > 0:
             y = ops.moe_mlp(recv_x[:R], lp["w_gu"], lp["w_down"],
                             torch.ones(R, 1, dtype=torch.float32, device=dev),
-                            recv_e[:R].view(R, 1), self.e0)
+                            recv_e[:R].view(R, 1), self.e0, plan_rows=self._plan_rows())
         else:
             y = recv_x
         self.ep.ep(st, True, self.row_bytes, send_x, send_e, send_base, cnt, y, None,
@@ -167,6 +167,13 @@ class ExpertParallelMoE:
         if T == 0:
             return h.new_zeros(0, D)
         return ops.moe_combine(send_x, topk_w, pos)
+
+    def _plan_rows(self) -> int:
+        """Routed rows this rank's experts receive on average for the step's token counts:
+        every rank's tokens x top-k, spread over the N ranks' experts. The receive region is
+        sized for the worst case; the grouped-GEMM plan is the one autotuned for this
+        (``StageRunner.autotune``: bucket x top-k rows over the local experts)."""
+        return max(1, sum(self.peer_tokens) * self.k // self.world)
 
     def begin_step(self, peer_tokens: List[int]) -> None:
         """Every rank's token count for the forward about to run (same list everywhere)."""
@@ -234,7 +241,7 @@ class ExpertParallelMoE:
         if recv_rows > 0:
             y = ops.moe_mlp(recv_x, lp["w_gu"], lp["w_down"],
                             torch.ones(recv_rows, 1, dtype=torch.float32, device=dev),
-                            recv_e.view(recv_rows, 1), self.e0)
+                            recv_e.view(recv_rows, 1), self.e0, plan_rows=self._plan_rows())
         else:
             y = recv_x.new_zeros(0, D)
         back = torch.empty(send_rows, D, dtype=h.dtype, device=cd)
@@ -313,6 +320,11 @@ class ExpertParallelEngine:
         run = self.engine.runner
         if not run.use_graphs:
             return
+        if os.environ.get("DLI_GEMM_AUTOTUNE", "1") == "1":
+            # every bucket tuned before the first captured exchange (ranks sharing a GPU tune
+            # one at a time: StageRunner.tune_lock), then all ranks start capturing together
+            run.autotune(run.buckets)
+            dist.barrier(group=self.ctrl_group)
         self.moe.static = True
         try:
             for b in run.buckets:

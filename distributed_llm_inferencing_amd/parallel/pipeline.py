@@ -775,7 +775,15 @@ class DistributedPipelineEngine:
 
     def warmup(self):
         install_piped(self.stage, self.channel)
-        self.stage.runner.capture()
+        run = self.stage.runner
+        if (run.use_graphs and os.environ.get("DLI_GEMM_AUTOTUNE", "1") == "1"
+                and getattr(self.channel, "ctrl_group", None) is not None):
+            # tune every bucket, then barrier, then capture: a stage's captured exchange
+            # never waits on a peer that is still tuning (ranks sharing a GPU tune one at a
+            # time, StageRunner.tune_lock)
+            run.autotune(run.buckets)
+            dist.barrier(group=self.channel.ctrl_group)
+        run.capture()
         self.channel.start_watchdog()
 
     def add_request(self, prompt, params: Optional[SamplingParams] = None, request_id=None):
