@@ -1947,22 +1947,25 @@ static int dispatch_tile(int tile_cfg, const void* A, int lda, const void* W, in
     // M = 512 (64 tiles x split 4)
     case 28: return launch_8p128<EPI>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
     // 256x256, one wave per SIMD, 128x128 wave tiles (gemm4w_kernel): 34 grouped order,
-    // 35 + stagger-U, 36 + explicit MFMA/ds_read interleave, 37 both
+    // 41 = 34 with the deep weight ring (3 W stages, 160 KiB LDS)
     case 34: return launch_4w<EPI, 8>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
+    case 41: return launch_4w<EPI, 8 | 32>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
+#if DLI_GEMM_AB_VARIANTS
+    // A/B variants measured slower everywhere (profiles/r4/gemm4w/; built only with
+    // DLI_GEMM_AB=1, each is 5 more heavy instantiations): 35 stagger-U, 36 all next-half
+    // reads up front, 37 both, 42 = 41 + stagger-U, 43 register staging, 44 = 43 +
+    // stagger-U, 40 the K-tile's LDS-DMA in one burst; diagnostics (wrong results): 38 no
+    // LDS-DMA in the K loop, 39 also no barrier
     case 35: return launch_4w<EPI, 8 | 1>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
     case 36: return launch_4w<EPI, 8 | 2>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
     case 37: return launch_4w<EPI, 8 | 3>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
-    // 41: 34 with the deep weight ring (3 W stages, 160 KiB LDS), 42: 41 + stagger-U
-    case 41: return launch_4w<EPI, 8 | 32>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
-    // 43: 34 with register staging (buffer_load -> VGPRs -> ds_write), 44: 43 + stagger-U
+    case 42: return launch_4w<EPI, 8 | 32 | 1>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
     case 43: return launch_4w<EPI, 8 | 1024>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
     case 44: return launch_4w<EPI, 8 | 1024 | 1>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
-    case 42: return launch_4w<EPI, 8 | 32 | 1>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
-    // 40: 34 with the K-tile's LDS-DMA issued in one burst (the first schedule, for A/B)
     case 40: return launch_4w<EPI, 8 | 4>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
-    // diagnostics (wrong results): 38 = 34 without the K loop's LDS-DMA, 39 = also no barrier
     case 38: return launch_4w<EPI, 8 | 64>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
     case 39: return launch_4w<EPI, 8 | 64 | 128>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
+#endif
     // skinny weight-streaming GEMM for M <= 4 (no grouped mode)
     case 30: case 31: case 32: case 33:
       if (go != nullptr) return (int)hipErrorInvalidValue;

@@ -51,6 +51,9 @@ def _hipcc() -> str:
 # -inf as the masked-score / running-max sentinel (poison under ninf -> NaNs).
 KERNEL_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-fno-gpu-rdc",
                 "-munsafe-fp-atomics", "-Wno-unused-result"]
+# DLI_GEMM_AB=1: also build the 4-wave GEMM's A/B variants (tiles 35-40, 42-44)
+if os.environ.get("DLI_GEMM_AB", "0") == "1":
+    KERNEL_FLAGS.append("-DDLI_GEMM_AB_VARIANTS=1")
 RUNTIME_FLAGS = ["-O2", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",
                  "-Wno-unused-result"]
 

@@ -50,14 +50,10 @@ TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256), 4: (256, 128),
          # N = 4096 at M = 512 with split-K 4
          28: (256, 128),
          # 256x256, 4 waves (one per SIMD), 128x128 wave tiles, accumulators pinned in the AGPR
-         # file (gemm4w_kernel); 35-37 are its stagger-U / bulk-read variants for A/B runs
-         34: (256, 256), 35: (256, 256), 36: (256, 256), 37: (256, 256),
-         # 34 with a 3-stage weight ring (160 KiB LDS: W fetched a K-tile further ahead for
-         # decode-sized GEMMs that stream their weights from HBM), 42 = 41 + stagger-U
-         41: (256, 256), 42: (256, 256),
-         # 34 with register staging (buffer_load -> VGPRs -> ds_write_b128 instead of LDS-DMA),
-         # 44 = 43 + stagger-U
-         43: (256, 256), 44: (256, 256)}
+         # file (gemm4w_kernel); 41 = 34 with a 3-stage weight ring (160 KiB LDS: W fetched a
+         # K-tile further ahead). Its A/B variants 35-40 / 42-44 are built only with
+         # DLI_GEMM_AB=1 (build.py) and never planned (profiles/r4/gemm4w/)
+         34: (256, 256), 41: (256, 256)}
 # weight-streaming skinny GEMM (gemm.hip gemv_kernel) for M <= GEMV_MAX_M rows: 16 / 32 output
 # rows per workgroup (31 for the SiLU*up gate/up pairing); not an MFMA tile, so kept apart
 GEMV_TILES = {30: 16, 31: 32, 32: 16, 33: 32}   # 32 / 33: 4 K-steps in flight per lane, M = 1
@@ -435,12 +431,11 @@ def candidate_plans(M: int, N: int, K: int, epi: str):
     # Default: 26 (256x224). It fills all 256 CUs on the gate/up GEMM and wins the isolated
     # autotune (98.8 vs ~106 us), but in the decode step it ran 97.9 vs 99.0 us per call and
     # the bench 0.3-0.7 % lower in three same-box A/B runs (profiles/r2_s2/README.md)
-    # 27 is tile 22 with the round-1 wait schedule (A/B reference only); 35-37, 42-44 are
-    # 4-wave variants measured slower everywhere (profiles/r4/gemm4w/); 41 (prefill-only) won
+    # 27 is tile 22 with the round-1 wait schedule (A/B reference only); 41 (prefill-only) won
     # isolated decode timings (M = 512 LM head 4-7 %) but cost the step 1.8 % in a same-box
     # bench A/B (42,548 without vs 41,790 / 41,653 tok/s with, profiles/r4/bench/)
     excl_env = os.environ.get("DLI_GEMM_EXCLUDE")
-    excl = {int(t) for t in (excl_env if excl_env is not None else "26,27,35,36,37,41,42,43,44").split(",")
+    excl = {int(t) for t in (excl_env if excl_env is not None else "26,27,41").split(",")
             if t.strip()}
     # ... except where 256x256 tiles take more than one wave of the chip and 256x224 tiles
     # land on a whole number of waves (Llama-3-70B gate/up at M = 512: N = 57344 is 448
