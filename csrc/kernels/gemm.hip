@@ -1196,11 +1196,14 @@ __global__ void __launch_bounds__(512) gemm8p128_kernel(
 
 // 16-B buffer load of `base` (a range-checked descriptor over `nbytes`: lanes past it read
 // zeros) straight into LDS at the wave-uniform `lds` + 16 * lane; voff per lane, soff uniform
+// CPOL: the load's cache-policy bits (0 default; 16 = sc1, device scope: the line is not
+// allocated in the CU's vector L1, which an LDS-DMA stream never re-reads)
+template <int CPOL = 0>
 __device__ __forceinline__ void buf_lds16(const void* base, int nbytes, char* lds, int voff,
                                           int soff) {
   const __amdgpu_buffer_rsrc_t r =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, nbytes, 0x00020000);
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds, 16, voff, soff, 0, 0);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds, 16, voff, soff, 0, CPOL);
 }
 
 // 16-B buffer load of `base` into registers (same range-checked descriptor as buf_lds16)
@@ -1311,15 +1314,16 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(
   };
   // one 1-KiB piece f (0..15: A pieces 0-7 of K-tile ka, W pieces 8-15 of K-tile kw into W
   // slot ws); a negative K-tile skips its pieces
+  constexpr int CPOL = (VAR & 2048) ? 16 : 0;
   auto stage_piece = [&](int ka, int kw, int ws, int f) {
     const int i = f & 7;
     if (f < 8) {
       if (ka >= 0)
-        buf_lds16(a_base, a_bytes, abase(ka) + (64 * wid + 8 * i) * 128, a_off[i & 1],
-                  i * 16 * lda + kpos(ka) * (BK * 2));
+        buf_lds16<CPOL>(a_base, a_bytes, abase(ka) + (64 * wid + 8 * i) * 128, a_off[i & 1],
+                        i * 16 * lda + kpos(ka) * (BK * 2));
     } else if (kw >= 0) {
-      buf_lds16(w_base, w_bytes, wbase(kw, ws) + (64 * wid + 8 * i) * 128, w_off[i & 1],
-                i * 16 * ldw + kpos(kw) * (BK * 2));
+      buf_lds16<CPOL>(w_base, w_bytes, wbase(kw, ws) + (64 * wid + 8 * i) * 128, w_off[i & 1],
+                      i * 16 * ldw + kpos(kw) * (BK * 2));
     }
   };
   auto stage = [&](int ka, int kw, int ws) {
@@ -1484,19 +1488,99 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(
     }
     wsl = ws1;
   };
+  // VAR 4096 ("two barriers", the buffer-release point moved forward): one K-tile = 128
+  // MFMAs, 64 on F0 (kk=0, read during the previous K-tile) then 64 on F1:
+  //   MFMAs 0-15: one F1(kt) fragment read after each        | frees buffer kt early
+  //   after MFMA 19: lgkmcnt(0) + s_barrier (B1: every wave has read buffer kt)
+  //   MFMAs 20-95: LDS-DMA of K-tile kt+2 into buffer kt, one piece per 5 MFMAs
+  //   after MFMA 103: vmcnt(16) (K-tile kt+1 landed; kt+2 may fly) + s_barrier (B2)
+  //   MFMAs 104-119: one F0(kt+1) fragment read after each
+  // The DMA of kt+2 starts ~45 MFMAs earlier than in the one-barrier schedule and is waited
+  // for ~1.5 K-tiles later (hides ~2,400 cycles of HBM latency instead of ~1,000-2,000),
+  // and 16 DMAs spread over 80 MFMAs instead of 64. Plain (2-stage) ring only.
+  constexpr bool TWO_B = (VAR & 4096) != 0;
+  static_assert(!(TWO_B && (DEEP || RS)), "two-barrier schedule: 2-stage ring only");
+  auto ktile2 = [&](auto SD, bool more, int kt) __attribute__((always_inline)) {
+    constexpr bool sd = decltype(SD)::value;       // stage K-tile kt + 2
+    const char* ab = abase(kt);
+    const char* wb = wbase(kt, 0);
+    const char* nab = abase(kt + 1);
+    const char* nwb = wbase(kt + 1, 0);
+    // B1 / B2 positions: default 19 / 103; VAR 8192: 25 / 111; VAR 16384: 25 / after the
+    // last MFMA with the 16 F0(kt+1) reads in one burst (the library kernel's placement)
+    constexpr int QB1 = (VAR & (8192 | 16384)) ? 25 : 19;
+    constexpr int QB2 = (VAR & 8192) ? 111 : (VAR & 16384) ? 127 : 103;
+    auto read_f0 = [&](int f) __attribute__((always_inline)) {
+      if (f >= 1 && f <= 8) b0[f - 1] = read_frag(nwb, wrow + 16 * (f - 1), 0);
+      else { const int ia = f == 0 ? 0 : f - 8; a0[ia] = read_frag(nab, arow + 16 * ia, 0); }
+    };
+    auto step = [&](int q) __attribute__((always_inline)) {
+      if (q < 16) {                                // F1(kt): A0, B0..B7, A1..A7
+        if (q >= 1 && q <= 8) b1[q - 1] = read_frag(wb, wrow + 16 * (q - 1), 1);
+        else { const int ia = q == 0 ? 0 : q - 8; a1[ia] = read_frag(ab, arow + 16 * ia, 1); }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (q == QB1 && !(VAR & 128)) {
+        __builtin_amdgcn_s_waitcnt(0xC07F);        // lgkmcnt(0)
+        barrier();
+      }
+      if (sd && !(VAR & 64) && q > QB1 && q <= QB1 + 80 && (q - QB1 - 1) % 5 == 0) {
+        stage_piece(kt + 2, kt + 2, 0, (q - QB1 - 1) / 5);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (q == QB2 && more && !(VAR & 128)) {
+        if (sd && !(VAR & 64)) wait_vmcnt<16>(); else wait_vmcnt<0>();
+        barrier();
+      }
+      if (more) {                                  // F0(kt+1)
+        if (QB2 == 127) {
+          if (q == 127) {
+#pragma unroll
+            for (int f = 0; f < 16; ++f) read_f0(f);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        } else if (q > QB2 && q <= QB2 + 16) {
+          read_f0(q - QB2 - 1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    };
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
+                     : "+a"(acc[i][j]) : "v"(b0[j]), "v"(a0[i]));
+        step(8 * i + j);
+      }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
+                     : "+a"(acc[i][j]) : "v"(b1[j]), "v"(a1[i]));
+        step(64 + 8 * i + j);
+      }
+  };
+
   using T_ = std::integral_constant<bool, true>;
   using F_ = std::integral_constant<bool, false>;
   int kt = 0;
-  if (DEEP || RS) {                                // RS: SA = write kt+2, SW = load kt+3
+  if (TWO_B) {
+    for (; kt + 2 < nk; ++kt) ktile2(T_{}, true, kt);
+    for (; kt < nk; ++kt) ktile2(F_{}, kt + 1 < nk, kt);
+  } else if (DEEP || RS) {                         // RS: SA = write kt+2, SW = load kt+3
     for (; kt + 3 < nk; ++kt) ktile(T_{}, T_{}, kt);
     if (kt + 2 < nk) { ktile(T_{}, F_{}, kt); ++kt; }
   } else {
     for (; kt + 2 < nk; ++kt) ktile(T_{}, T_{}, kt);
   }
-  if (kt + 1 < nk) { ktile(F_{}, F_{}, kt); ++kt; }
-  if (nk > 0) {
-    half(a0, b0, a1, b1, abase(kt), wbase(kt, wsl), 1, true, -1, -1, 0);
-    half(a1, b1, a0, b0, smem, smem, 0, false, -1, -1, 0);
+  if (!TWO_B) {
+    if (kt + 1 < nk) { ktile(F_{}, F_{}, kt); ++kt; }
+    if (nk > 0) {
+      half(a0, b0, a1, b1, abase(kt), wbase(kt, wsl), 1, true, -1, -1, 0);
+      half(a1, b1, a0, b0, smem, smem, 0, false, -1, -1, 0);
+    }
   }
   // MFMA results -> any other reader: the XDL write-back wait states (§5.7 item 2), tied to
   // the last row of accumulators written so that no copy of them is hoisted above the pad
@@ -1950,6 +2034,12 @@ static int dispatch_tile(int tile_cfg, const void* A, int lda, const void* W, in
     // 41 = 34 with the deep weight ring (3 W stages, 160 KiB LDS)
     case 34: return launch_4w<EPI, 8>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
     case 41: return launch_4w<EPI, 8 | 32>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
+    // experimental (round 4): 45 = 34 with the two-barrier schedule (sc1 loads, VAR 2048,
+    // measured neutral: profiles/r4/gemm4w/s17_*)
+    case 45: return launch_4w<EPI, 8 | 4096>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
+    // 49 / 50: 45 with the barriers at MFMA 25 / 111, and at 25 / after the last MFMA
+    case 49: return launch_4w<EPI, 8 | 4096 | 8192>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
+    case 50: return launch_4w<EPI, 8 | 4096 | 16384>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
 #if DLI_GEMM_AB_VARIANTS
     // A/B variants measured slower everywhere (profiles/r4/gemm4w/; built only with
     // DLI_GEMM_AB=1, each is 5 more heavy instantiations): 35 stagger-U, 36 all next-half

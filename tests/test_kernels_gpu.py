@@ -99,7 +99,8 @@ def test_gemm_256x224_pingpong(gpu, M, N, K, epi, tile):
         close(out, ref, rtol=2e-2, atol=2e-2)
 
 
-@pytest.mark.parametrize("tile", [34, 41])   # A/B variants: DLI_GEMM_AB=1 builds
+@pytest.mark.parametrize("tile", [int(t) for t in os.environ.get("DLI_TEST_4W_TILES",
+                                                                  "34,41").split(",")])
 @pytest.mark.parametrize("M,N,K,epi", [(2048, 6144, 4096, "none"), (4096, 4096, 4096, "none"),
                                        (8192, 28672, 4096, "silu_mul"),
                                        (16384, 4096, 14336, "none"), (512, 28672, 4096, "silu_mul"),
