@@ -1499,13 +1499,21 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(
   // for ~1.5 K-tiles later (hides ~2,400 cycles of HBM latency instead of ~1,000-2,000),
   // and 16 DMAs spread over 80 MFMAs instead of 64. Plain (2-stage) ring only.
   constexpr bool TWO_B = (VAR & 4096) != 0;
-  static_assert(!(TWO_B && (DEEP || RS)), "two-barrier schedule: 2-stage ring only");
-  auto ktile2 = [&](auto SD, bool more, int kt) __attribute__((always_inline)) {
-    constexpr bool sd = decltype(SD)::value;       // stage K-tile kt + 2
+  // With DEEP (3 W stages) the DMA of this K-tile is A(kt+2) and W(kt+3), both into kt's
+  // slots; B2 may leave the previous tile's W pieces in flight too (vmcnt 24).
+  static_assert(!(TWO_B && RS), "two-barrier schedule: LDS-DMA staging only");
+  // SA / SW: this K-tile stages A(kt+2) / W(kt+2, DEEP: kt+3); PW: the previous K-tile
+  // staged W (DEEP: its pieces may still fly at B2)
+  auto ktile2 = [&](auto SA, auto SW, auto PW, bool more, int kt)
+      __attribute__((always_inline)) {
+    constexpr bool sa = decltype(SA)::value, sw = decltype(SW)::value;
+    constexpr bool pw = DEEP && decltype(PW)::value;
+    constexpr bool sd = sa || sw;
+    const int ws1 = wsl == 2 ? 0 : wsl + 1;
     const char* ab = abase(kt);
-    const char* wb = wbase(kt, 0);
+    const char* wb = wbase(kt, wsl);
     const char* nab = abase(kt + 1);
-    const char* nwb = wbase(kt + 1, 0);
+    const char* nwb = wbase(kt + 1, ws1);
     // B1 / B2 positions: default 19 / 103; VAR 8192: 25 / 111; VAR 16384: 25 / after the
     // last MFMA with the 16 F0(kt+1) reads in one burst (the library kernel's placement)
     constexpr int QB1 = (VAR & (8192 | 16384)) ? 25 : 19;
@@ -1525,11 +1533,12 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(
         barrier();
       }
       if (sd && !(VAR & 64) && q > QB1 && q <= QB1 + 80 && (q - QB1 - 1) % 5 == 0) {
-        stage_piece(kt + 2, kt + 2, 0, (q - QB1 - 1) / 5);
+        stage_piece(sa ? kt + 2 : -1, sw ? kt + (DEEP ? 3 : 2) : -1, wsl, (q - QB1 - 1) / 5);
         __builtin_amdgcn_sched_barrier(0);
       }
       if (q == QB2 && more && !(VAR & 128)) {
-        if (sd && !(VAR & 64)) wait_vmcnt<16>(); else wait_vmcnt<0>();
+        constexpr int fly = (VAR & 64) ? 0 : 8 * ((sa ? 1 : 0) + (sw ? 1 : 0) + (pw ? 1 : 0));
+        wait_vmcnt<fly>();
         barrier();
       }
       if (more) {                                  // F0(kt+1)
@@ -1566,9 +1575,13 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(
   using T_ = std::integral_constant<bool, true>;
   using F_ = std::integral_constant<bool, false>;
   int kt = 0;
-  if (TWO_B) {
-    for (; kt + 2 < nk; ++kt) ktile2(T_{}, true, kt);
-    for (; kt < nk; ++kt) ktile2(F_{}, kt + 1 < nk, kt);
+  if (TWO_B && DEEP) {
+    for (; kt + 3 < nk; ++kt) { ktile2(T_{}, T_{}, T_{}, true, kt); wsl = wsl == 2 ? 0 : wsl + 1; }
+    if (kt + 2 < nk) { ktile2(T_{}, F_{}, T_{}, true, kt); wsl = wsl == 2 ? 0 : wsl + 1; ++kt; }
+    for (; kt < nk; ++kt) { ktile2(F_{}, F_{}, F_{}, kt + 1 < nk, kt); wsl = wsl == 2 ? 0 : wsl + 1; }
+  } else if (TWO_B) {
+    for (; kt + 2 < nk; ++kt) ktile2(T_{}, T_{}, F_{}, true, kt);
+    for (; kt < nk; ++kt) ktile2(F_{}, F_{}, F_{}, kt + 1 < nk, kt);
   } else if (DEEP || RS) {                         // RS: SA = write kt+2, SW = load kt+3
     for (; kt + 3 < nk; ++kt) ktile(T_{}, T_{}, kt);
     if (kt + 2 < nk) { ktile(T_{}, F_{}, kt); ++kt; }
@@ -2040,6 +2053,8 @@ static int dispatch_tile(int tile_cfg, const void* A, int lda, const void* W, in
     // 49 / 50: 45 with the barriers at MFMA 25 / 111, and at 25 / after the last MFMA
     case 49: return launch_4w<EPI, 8 | 4096 | 8192>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
     case 50: return launch_4w<EPI, 8 | 4096 | 16384>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
+    // 51: 45 with the deep weight ring of 41 (W of K-tile kt+3 staged during kt)
+    case 51: return launch_4w<EPI, 8 | 4096 | 32>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
 #if DLI_GEMM_AB_VARIANTS
     // A/B variants measured slower everywhere (profiles/r4/gemm4w/; built only with
     // DLI_GEMM_AB=1, each is 5 more heavy instantiations): 35 stagger-U, 36 all next-half

@@ -8,7 +8,7 @@ The projection GEMMs of a decode step are skinny (M = batch) and of a prefill st
   GEMM at M = 256': choose SPLITK so that tiles * SPLITK ~ 0.5-1x the CU count),
 * the backend: decode GEMMs (the hipGraph steps) always on our MFMA kernels, tiles
   autotuned at graph capture (on by default; ``DLI_GEMM_AUTOTUNE=0`` disables it). Prefill
-  GEMMs: our 8-phase 256x256 kernel or the one-wave-per-SIMD 256x256 kernel (tile 41),
+  GEMMs: our 8-phase 256x256 kernel or the one-wave-per-SIMD 256x256 kernel (tile 45),
   whichever the warmup measures faster per token bucket (``prefill_candidates``). hipBLASLt
   is off the hot path: ``DLI_TUNE_PREFILL_BLAS=1`` lets it compete in the prefill autotune,
   ``DLI_GEMM_BACKEND=hipblaslt``, ``DLI_GEMM_PREFILL_BLAS=1`` and ``DLI_GEMM_DECODE_BLAS=1``
@@ -51,9 +51,14 @@ TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256), 4: (256, 128),
          28: (256, 128),
          # 256x256, 4 waves (one per SIMD), 128x128 wave tiles, accumulators pinned in the AGPR
          # file (gemm4w_kernel); 41 = 34 with a 3-stage weight ring (160 KiB LDS: W fetched a
-         # K-tile further ahead). Its A/B variants 35-40 / 42-44 are built only with
-         # DLI_GEMM_AB=1 (build.py) and never planned (profiles/r4/gemm4w/)
-         34: (256, 256), 41: (256, 256)}
+         # K-tile further ahead); 45 = 34 with two barriers per K-tile (the buffer released
+         # after 20 MFMAs, the next-next K-tile's DMA over 80 MFMAs); 49 / 50 = 45 with other
+         # barrier placements, 51 = 45 with the weight ring of 41. A/B variants 35-40 / 42-44
+         # are built only with DLI_GEMM_AB=1 (build.py) and never planned (profiles/r4/gemm4w/)
+         34: (256, 256), 41: (256, 256), 45: (256, 256), 49: (256, 256), 50: (256, 256),
+         51: (256, 256)}
+# the 4-wave plan raced against the 8-phase one in the prefill autotune
+PREFILL_4W_TILE = int(os.environ.get("DLI_GEMM_PREFILL_4W", "45"))
 # weight-streaming skinny GEMM (gemm.hip gemv_kernel) for M <= GEMV_MAX_M rows: 16 / 32 output
 # rows per workgroup (31 for the SiLU*up gate/up pairing); not an MFMA tile, so kept apart
 GEMV_TILES = {30: 16, 31: 32, 32: 16, 33: 32}   # 32 / 33: 4 K-steps in flight per lane, M = 1
@@ -410,13 +415,12 @@ def prefill_candidates(M: int, N: int, K: int, epi: str):
     the autotune the whole b512 bench lost 0.35 % without it (43,820 -> 43,665 tok/s, same
     box, profiles/r4/README.md); ``DLI_TUNE_PREFILL_BLAS=1`` restores it."""
     out = [_heuristic(M, N, K, epi)]
-    # the one-wave-per-SIMD 256x256 kernel with the deep weight ring (tile 41) at the same
-    # split: 1.0-2.5 % faster than the 8-phase tile on QKV / gate-up / square prefill shapes,
-    # ~5 % slower on the long-K down projection (profiles/r4/gemm4w/), so measured per shape
+    # the one-wave-per-SIMD 256x256 kernel (PREFILL_4W_TILE: the two-barrier schedule) at
+    # the same split: 1-4 % faster than the 8-phase tile on the square / QKV / gate-up /
+    # down prefill shapes (profiles/r4/gemm4w/), measured per shape and bucket
     base = out[0]
-    if base.backend == "dli" and base.tile == 22 and \
-            "41" not in os.environ.get("DLI_GEMM_PREFILL_EXCLUDE", "").split(","):
-        out.append(GemmPlan("dli", 41, base.splits))
+    if base.backend == "dli" and base.tile == 22 and PREFILL_4W_TILE > 0:
+        out.append(GemmPlan("dli", PREFILL_4W_TILE, base.splits))
     if (epi in ("none", "splitk", "silu_mul", "f32")
             and os.environ.get("DLI_GEMM_NO_BLAS", "0") != "1"
             and os.environ.get("DLI_TUNE_PREFILL_BLAS", "0") == "1"
@@ -435,7 +439,7 @@ def candidate_plans(M: int, N: int, K: int, epi: str):
     # isolated decode timings (M = 512 LM head 4-7 %) but cost the step 1.8 % in a same-box
     # bench A/B (42,548 without vs 41,790 / 41,653 tok/s with, profiles/r4/bench/)
     excl_env = os.environ.get("DLI_GEMM_EXCLUDE")
-    excl = {int(t) for t in (excl_env if excl_env is not None else "26,27,41").split(",")
+    excl = {int(t) for t in (excl_env if excl_env is not None else "26,27,41,45,49,50,51").split(",")
             if t.strip()}
     # ... except where 256x256 tiles take more than one wave of the chip and 256x224 tiles
     # land on a whole number of waves (Llama-3-70B gate/up at M = 512: N = 57344 is 448

@@ -100,7 +100,7 @@ def test_gemm_256x224_pingpong(gpu, M, N, K, epi, tile):
 
 
 @pytest.mark.parametrize("tile", [int(t) for t in os.environ.get("DLI_TEST_4W_TILES",
-                                                                  "34,41").split(",")])
+                                                                  "34,41,45").split(",")])
 @pytest.mark.parametrize("M,N,K,epi", [(2048, 6144, 4096, "none"), (4096, 4096, 4096, "none"),
                                        (8192, 28672, 4096, "silu_mul"),
                                        (16384, 4096, 14336, "none"), (512, 28672, 4096, "silu_mul"),

@@ -306,9 +306,10 @@ def test_prefill_gemm_plan_is_own_kernel(monkeypatch):
     # prefill autotune (StageRunner.autotune_prefill): our 8-phase plan vs our 4-wave deep-W
     # plan at the same split; hipBLASLt only when DLI_TUNE_PREFILL_BLAS=1 asks for it
     c = G.prefill_candidates(16384, 28672, 4096, "silu_mul")
-    assert c == [G.GemmPlan("dli", 22, 1), G.GemmPlan("dli", 41, 1)]
+    t4 = G.PREFILL_4W_TILE
+    assert c == [G.GemmPlan("dli", 22, 1), G.GemmPlan("dli", t4, 1)]
     assert G.prefill_candidates(2048, 4096, 4096, "splitk") == \
-        [G.GemmPlan("dli", 22, 2), G.GemmPlan("dli", 41, 2)]
+        [G.GemmPlan("dli", 22, 2), G.GemmPlan("dli", t4, 2)]
     assert all(p.backend == "dli" for p in G.prefill_candidates(4096, 4096, 4096, "bias_gelu"))
     monkeypatch.setenv("DLI_TUNE_PREFILL_BLAS", "1")
     assert [p.backend for p in G.prefill_candidates(16384, 6144, 4096, "none")] == \
@@ -318,7 +319,7 @@ def test_prefill_gemm_plan_is_own_kernel(monkeypatch):
     monkeypatch.delenv("DLI_TUNE_PREFILL_BLAS")
     # the 4-wave tiles stay out of the decode autotune (tile 41 cost the step 1.8 %)
     tiles = {p.tile for p in G.candidate_plans(512, 4096, 4096, "none")}
-    assert 41 not in tiles and 34 in tiles
+    assert not tiles & {41, 45, 49, 50, 51} and 34 in tiles
     # decode QKV timing pins the candidate for the fused attention path, then restores
     p1, p4 = G.GemmPlan("dli", 30, 1), G.GemmPlan("dli", 32, 4)
     G.set_plan(1, 6144, 4096, "none", p4)
