@@ -2047,15 +2047,19 @@ static int dispatch_tile(int tile_cfg, const void* A, int lda, const void* W, in
     // 41 = 34 with the deep weight ring (3 W stages, 160 KiB LDS)
     case 34: return launch_4w<EPI, 8>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
     case 41: return launch_4w<EPI, 8 | 32>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
-    // experimental (round 4): 45 = 34 with the two-barrier schedule (sc1 loads, VAR 2048,
-    // measured neutral: profiles/r4/gemm4w/s17_*)
+    // 45 = 34 with the two-barrier schedule: the prefill autotune's 4-wave candidate
+    // (sc1 loads, VAR 2048, measured neutral: profiles/r4/gemm4w/s17_*)
     case 45: return launch_4w<EPI, 8 | 4096>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
+#if DLI_GEMM_AB_VARIANTS
+    // two-barrier variants measured no faster than 45 (profiles/r4/gemm4w/s18_*):
     // 49 / 50: 45 with the barriers at MFMA 25 / 111, and at 25 / after the last MFMA
     case 49: return launch_4w<EPI, 8 | 4096 | 8192>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
     case 50: return launch_4w<EPI, 8 | 4096 | 16384>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
+    // 52 / 53: 45 with 8-row-tile groups / no grouping (tile order A/B)
+    case 52: return launch_4w<EPI, 16 | 4096>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
+    case 53: return launch_4w<EPI, 4096>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
     // 51: 45 with the deep weight ring of 41 (W of K-tile kt+3 staged during kt)
     case 51: return launch_4w<EPI, 8 | 4096 | 32>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
-#if DLI_GEMM_AB_VARIANTS
     // A/B variants measured slower everywhere (profiles/r4/gemm4w/; built only with
     // DLI_GEMM_AB=1, each is 5 more heavy instantiations): 35 stagger-U, 36 all next-half
     // reads up front, 37 both, 42 = 41 + stagger-U, 43 register staging, 44 = 43 +

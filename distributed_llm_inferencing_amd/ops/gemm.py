@@ -52,11 +52,10 @@ TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256), 4: (256, 128),
          # 256x256, 4 waves (one per SIMD), 128x128 wave tiles, accumulators pinned in the AGPR
          # file (gemm4w_kernel); 41 = 34 with a 3-stage weight ring (160 KiB LDS: W fetched a
          # K-tile further ahead); 45 = 34 with two barriers per K-tile (the buffer released
-         # after 20 MFMAs, the next-next K-tile's DMA over 80 MFMAs); 49 / 50 = 45 with other
-         # barrier placements, 51 = 45 with the weight ring of 41. A/B variants 35-40 / 42-44
-         # are built only with DLI_GEMM_AB=1 (build.py) and never planned (profiles/r4/gemm4w/)
-         34: (256, 256), 41: (256, 256), 45: (256, 256), 49: (256, 256), 50: (256, 256),
-         51: (256, 256)}
+         # after 20 MFMAs, the next-next K-tile's DMA over 80 MFMAs). A/B variants 35-40 and
+         # 42-44 / 49-53 are built only with DLI_GEMM_AB=1 (build.py) and never planned
+         # (profiles/r4/gemm4w/)
+         34: (256, 256), 41: (256, 256), 45: (256, 256)}
 # the 4-wave plan raced against the 8-phase one in the prefill autotune
 PREFILL_4W_TILE = int(os.environ.get("DLI_GEMM_PREFILL_4W", "45"))
 # weight-streaming skinny GEMM (gemm.hip gemv_kernel) for M <= GEMV_MAX_M rows: 16 / 32 output
@@ -435,11 +434,12 @@ def candidate_plans(M: int, N: int, K: int, epi: str):
     # Default: 26 (256x224). It fills all 256 CUs on the gate/up GEMM and wins the isolated
     # autotune (98.8 vs ~106 us), but in the decode step it ran 97.9 vs 99.0 us per call and
     # the bench 0.3-0.7 % lower in three same-box A/B runs (profiles/r2_s2/README.md)
-    # 27 is tile 22 with the round-1 wait schedule (A/B reference only); 41 (prefill-only) won
+    # 27 is tile 22 with the round-1 wait schedule (A/B reference only); 45 stays
+    # prefill-only too (no gain in a same-box bench A/B, profiles/r4/bench/s18_*); 41 won
     # isolated decode timings (M = 512 LM head 4-7 %) but cost the step 1.8 % in a same-box
     # bench A/B (42,548 without vs 41,790 / 41,653 tok/s with, profiles/r4/bench/)
     excl_env = os.environ.get("DLI_GEMM_EXCLUDE")
-    excl = {int(t) for t in (excl_env if excl_env is not None else "26,27,41,45,49,50,51").split(",")
+    excl = {int(t) for t in (excl_env if excl_env is not None else "26,27,41,45").split(",")
             if t.strip()}
     # ... except where 256x256 tiles take more than one wave of the chip and 256x224 tiles
     # land on a whole number of waves (Llama-3-70B gate/up at M = 512: N = 57344 is 448

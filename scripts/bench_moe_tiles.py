@@ -6,6 +6,10 @@ the Infinity Cache, so each call streams them from HBM). Prints one JSON line pe
 sorted by time, with the achieved weight-streaming bandwidth.
 
     python scripts/bench_moe_tiles.py [--batch 512] [--which down,gate_up]
+    python scripts/bench_moe_tiles.py --batch 16384 --tiles 22,45   # prefill-sized experts
+
+With ``--tiles`` only those tiles run, and the grid is bounded by the largest expert's rows
+(the eager prefill path of ``ops.moe_mlp``) instead of all rows.
 """
 import argparse
 import itertools
@@ -24,7 +28,9 @@ def main():
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--which", default="down,gate_up")
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--tiles", default="")
     a = ap.parse_args()
+    only = [int(t) for t in a.tiles.split(",") if t]
     from distributed_llm_inferencing_amd import ops
     from distributed_llm_inferencing_amd.ops import gemm as G
     dev = torch.device("cuda")
@@ -37,8 +43,10 @@ def main():
         w = (torch.randn(E, N, K, device=dev) * 0.02).to(torch.bfloat16)
         x = (torch.randn(rows, K, device=dev) * 0.5).to(torch.bfloat16)
         out = []
-        for tile in sorted(G.TILES):
-            if G.TILES[tile][0] > 2 * max(64, rows // E + 32) or not G.tile_ok(tile, epi):
+        rpg = max(counts) if only else rows
+        for tile in (only or sorted(G.TILES)):
+            if not only and (G.TILES[tile][0] > 2 * max(64, rows // E + 32)
+                             or not G.tile_ok(tile, epi)):
                 continue
             for splits in (1, 2, 4):
                 if splits > 1 and not (K % (64 * splits) == 0 and K // splits >= 2048):
@@ -46,14 +54,16 @@ def main():
                 p = G.GemmPlan("dli", tile, splits)
                 try:
                     ms = ops.benchmark(lambda p=p: ops._gemm_native(
-                        x, w, epi, plan=p, groups=E, group_off=off, rows_per_group=rows),
+                        x, w, epi, plan=p, groups=E, group_off=off, rows_per_group=rpg),
                         iters=a.iters, warmup=1)
                 except Exception as e:  # noqa: BLE001
                     out.append({"which": which, "tile": tile, "splits": splits,
                                 "error": str(e)[:60]})
                     continue
                 out.append({"which": which, "rows": rows, "tile": tile,
-                            "bm_bn": G.TILES[tile], "splits": splits, "us": round(ms * 1e3, 1),
+                            "bm_bn": G.TILES.get(tile), "splits": splits,
+                            "us": round(ms * 1e3, 1),
+                            "tflops": round(2.0 * rows * N * K / (ms * 1e-3) / 1e12, 1),
                             "weight_TBps": round(w.numel() * 2 / (ms * 1e-3) / 1e12, 2)})
         for r in sorted(out, key=lambda r: r.get("us", 1e9)):
             print(json.dumps(r), flush=True)
