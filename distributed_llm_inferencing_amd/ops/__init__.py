@@ -514,16 +514,16 @@ def moe_mlp(x, w_gu, w_down, topk_w, topk_ids, expert_offset: int = 0,
     _native_call("dli_moe_gather", _p(xp), _p(x), _p(src), n, D, _p(offsets[E_local:]), _st())
     act = torch.empty(max(n, 1), F2 // 2, dtype=x.dtype, device=dev)
     if n >= _MOE_PREFILL_ROWS * E_local and not torch.cuda.is_current_stream_capturing():
-        # prefill-sized expert GEMMs (thousands of rows per expert) are compute-bound: the
-        # grouped 8-phase 256x256 kernel (tile 22, grid.z = expert) with the fused SiLU*up
-        # epilogue. The largest expert's row count bounds the grid (one host read of the
+        # prefill-sized expert GEMMs (thousands of rows per expert) are compute-bound: a
+        # grouped 256x256 kernel (G.MOE_PREFILL_TILE: the two-barrier 4-wave tile, grid.z =
+        # expert) with the fused SiLU*up epilogue. The largest expert's row count bounds the grid (one host read of the
         # offsets per MoE layer, eager prefill only) instead of n, which would launch ~8x
         # more (empty) row tiles per expert.
         offs = offsets.tolist()
         rows_max = max(b - a for a, b in zip(offs[:-1], offs[1:]))
         y = torch.empty(max(n, 1), D, dtype=x.dtype, device=dev)
         if rows_max > 0:
-            p8 = G.GemmPlan("dli", 22, 1)
+            p8 = G.GemmPlan("dli", G.MOE_PREFILL_TILE, 1)
             _gemm_native(xp, w_gu, "silu_mul", out=act, groups=E_local, group_off=offsets,
                          rows_per_group=rows_max, plan=p8)
             _gemm_native(act, w_down, "none", out=y, groups=E_local, group_off=offsets,

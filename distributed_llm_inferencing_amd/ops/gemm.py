@@ -58,6 +58,10 @@ TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256), 4: (256, 128),
          34: (256, 256), 41: (256, 256), 45: (256, 256)}
 # the 4-wave plan raced against the 8-phase one in the prefill autotune
 PREFILL_4W_TILE = int(os.environ.get("DLI_GEMM_PREFILL_4W", "45"))
+# prefill-sized grouped expert GEMMs (ops.moe_mlp's eager path): Mixtral 8x7B at 32k routed
+# rows, tile 45 vs the 8-phase tile 22: down 2,895 vs 3,071-3,239 us, gate/up 5,736 vs
+# 5,898 us (profiles/r4/moe/)
+MOE_PREFILL_TILE = int(os.environ.get("DLI_MOE_PREFILL_TILE", "45"))
 # weight-streaming skinny GEMM (gemm.hip gemv_kernel) for M <= GEMV_MAX_M rows: 16 / 32 output
 # rows per workgroup (31 for the SiLU*up gate/up pairing); not an MFMA tile, so kept apart
 GEMV_TILES = {30: 16, 31: 32, 32: 16, 33: 32}   # 32 / 33: 4 K-steps in flight per lane, M = 1

@@ -612,10 +612,13 @@ def test_grouped_gemm_all_tiles_and_splitk(gpu, epi):
             close(out, ref, rtol=2e-2, atol=2e-2)
 
 
-def test_moe_mlp_prefill_grouped_8phase_path(gpu, monkeypatch):
-    """Prefill-sized MoE (rows per expert above the threshold) takes the grouped 8-phase
-    path (grid bounded by the largest expert's rows); same result as the reference."""
+@pytest.mark.parametrize("tile", [22, 45])
+def test_moe_mlp_prefill_grouped_path(gpu, monkeypatch, tile):
+    """Prefill-sized MoE (rows per expert above the threshold) takes the grouped 256x256
+    path (grid bounded by the largest expert's rows) on the 8-phase (22) or the two-barrier
+    4-wave tile (45, the default); same result as the reference."""
     monkeypatch.setattr(ops, "_MOE_PREFILL_ROWS", 16)
+    monkeypatch.setattr(ops.G, "MOE_PREFILL_TILE", tile)
     torch.manual_seed(13)
     T, E, k, D, F = 200, 4, 2, 256, 512
     x = rnd(T, D, dev=gpu)
