@@ -1444,7 +1444,13 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(
     barrier();
   }
   bf16x8 a0[8], b0[8], a1[8], b1[8];
-  if (nk > 0) {
+  if (nk > 0 && (VAR & 32768)) {                   // column-major MFMA order (JM below)
+    b0[0] = read_frag(wbase(0, 0), wrow, 0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a0[i] = read_frag(abase(0), arow + 16 * i, 0);
+#pragma unroll
+    for (int j = 1; j < 8; ++j) b0[j] = read_frag(wbase(0, 0), wrow + 16 * j, 0);
+  } else if (nk > 0) {
     a0[0] = read_frag(abase(0), arow, 0);
 #pragma unroll
     for (int j = 0; j < 8; ++j) b0[j] = read_frag(wbase(0, 0), wrow + 16 * j, 0);
@@ -1518,14 +1524,25 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(
     // last MFMA with the 16 F0(kt+1) reads in one burst (the library kernel's placement)
     constexpr int QB1 = (VAR & (8192 | 16384)) ? 25 : 19;
     constexpr int QB2 = (VAR & 8192) ? 111 : (VAR & 16384) ? 127 : 103;
-    auto read_f0 = [&](int f) __attribute__((always_inline)) {
-      if (f >= 1 && f <= 8) b0[f - 1] = read_frag(nwb, wrow + 16 * (f - 1), 0);
-      else { const int ia = f == 0 ? 0 : f - 8; a0[ia] = read_frag(nab, arow + 16 * ia, 0); }
+    // VAR 32768 (JM): MFMAs column-major within a half (acc[i][j] with j outer), so the
+    // weight fragment — MFMA operand A — stays the same for 8 consecutive MFMAs (the
+    // library kernel's order); fragment f of a half is then read in the order B0, A0..A7,
+    // B1..B7 instead of A0, B0..B7, A1..A7
+    constexpr bool JM = (VAR & 32768) != 0;
+    auto read_fx = [&](int f, bf16x8 (&av)[8], bf16x8 (&bv)[8], const char* pa, const char* pw,
+                       int kk) __attribute__((always_inline)) {
+      if (JM) {
+        if (f >= 1 && f <= 8) av[f - 1] = read_frag(pa, arow + 16 * (f - 1), kk);
+        else { const int jb = f == 0 ? 0 : f - 8; bv[jb] = read_frag(pw, wrow + 16 * jb, kk); }
+      } else {
+        if (f >= 1 && f <= 8) bv[f - 1] = read_frag(pw, wrow + 16 * (f - 1), kk);
+        else { const int ia = f == 0 ? 0 : f - 8; av[ia] = read_frag(pa, arow + 16 * ia, kk); }
+      }
     };
+    auto read_f0 = [&](int f) __attribute__((always_inline)) { read_fx(f, a0, b0, nab, nwb, 0); };
     auto step = [&](int q) __attribute__((always_inline)) {
-      if (q < 16) {                                // F1(kt): A0, B0..B7, A1..A7
-        if (q >= 1 && q <= 8) b1[q - 1] = read_frag(wb, wrow + 16 * (q - 1), 1);
-        else { const int ia = q == 0 ? 0 : q - 8; a1[ia] = read_frag(ab, arow + 16 * ia, 1); }
+      if (q < 16) {                                // F1(kt)
+        read_fx(q, a1, b1, ab, wb, 1);
         __builtin_amdgcn_sched_barrier(0);
       }
       if (q == QB1 && !(VAR & 128)) {
@@ -1555,20 +1572,22 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(
       }
     };
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int u = 0; u < 8; ++u)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
+      for (int v = 0; v < 8; ++v) {
+        const int i = JM ? v : u, j = JM ? u : v;
         asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
                      : "+a"(acc[i][j]) : "v"(b0[j]), "v"(a0[i]));
-        step(8 * i + j);
+        step(8 * u + v);
       }
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int u = 0; u < 8; ++u)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
+      for (int v = 0; v < 8; ++v) {
+        const int i = JM ? v : u, j = JM ? u : v;
         asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
                      : "+a"(acc[i][j]) : "v"(b1[j]), "v"(a1[i]));
-        step(64 + 8 * i + j);
+        step(64 + 8 * u + v);
       }
   };
 
@@ -1597,9 +1616,15 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(
   }
   // MFMA results -> any other reader: the XDL write-back wait states (§5.7 item 2), tied to
   // the last row of accumulators written so that no copy of them is hoisted above the pad
-  asm volatile("s_nop 15\n\ts_nop 15"
-               : "+a"(acc[7][0]), "+a"(acc[7][1]), "+a"(acc[7][2]), "+a"(acc[7][3]),
-                 "+a"(acc[7][4]), "+a"(acc[7][5]), "+a"(acc[7][6]), "+a"(acc[7][7]));
+  if constexpr ((VAR & 32768) != 0) {              // column-major order: column 7 is last
+    asm volatile("s_nop 15\n\ts_nop 15"
+                 : "+a"(acc[0][7]), "+a"(acc[1][7]), "+a"(acc[2][7]), "+a"(acc[3][7]),
+                   "+a"(acc[4][7]), "+a"(acc[5][7]), "+a"(acc[6][7]), "+a"(acc[7][7]));
+  } else {
+    asm volatile("s_nop 15\n\ts_nop 15"
+                 : "+a"(acc[7][0]), "+a"(acc[7][1]), "+a"(acc[7][2]), "+a"(acc[7][3]),
+                   "+a"(acc[7][4]), "+a"(acc[7][5]), "+a"(acc[7][6]), "+a"(acc[7][7]));
+  }
   // accumulators leave the AGPR file by one pinned copy each, ahead of any row / column
   // condition (an AGPR value read inside a divergent branch made hipcc move the whole
   // accumulator set through VGPRs in the K loop)
@@ -2050,6 +2075,8 @@ static int dispatch_tile(int tile_cfg, const void* A, int lda, const void* W, in
     // 45 = 34 with the two-barrier schedule: the prefill autotune's 4-wave candidate
     // (sc1 loads, VAR 2048, measured neutral: profiles/r4/gemm4w/s17_*)
     case 45: return launch_4w<EPI, 8 | 4096>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
+    // experimental: 46 = 45 with column-major MFMA order (weight operand reused 8x)
+    case 46: return launch_4w<EPI, 8 | 4096 | 32768>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
 #if DLI_GEMM_AB_VARIANTS
     // two-barrier variants measured no faster than 45 (profiles/r4/gemm4w/s18_*):
     // 49 / 50: 45 with the barriers at MFMA 25 / 111, and at 25 / after the last MFMA
