@@ -2075,9 +2075,10 @@ static int dispatch_tile(int tile_cfg, const void* A, int lda, const void* W, in
     // 45 = 34 with the two-barrier schedule: the prefill autotune's 4-wave candidate
     // (sc1 loads, VAR 2048, measured neutral: profiles/r4/gemm4w/s17_*)
     case 45: return launch_4w<EPI, 8 | 4096>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
-    // experimental: 46 = 45 with column-major MFMA order (weight operand reused 8x)
-    case 46: return launch_4w<EPI, 8 | 4096 | 32768>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
 #if DLI_GEMM_AB_VARIANTS
+    // 46 = 45 with column-major MFMA order (weight operand reused 8x, the library's order):
+    // within 0.2 % of 45 (profiles/r4/gemm4w/s23_*)
+    case 46: return launch_4w<EPI, 8 | 4096 | 32768>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
     // two-barrier variants measured no faster than 45 (profiles/r4/gemm4w/s18_*):
     // 49 / 50: 45 with the barriers at MFMA 25 / 111, and at 25 / after the last MFMA
     case 49: return launch_4w<EPI, 8 | 4096 | 8192>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
