@@ -1315,8 +1315,32 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(
   // one 1-KiB piece f (0..15: A pieces 0-7 of K-tile ka, W pieces 8-15 of K-tile kw into W
   // slot ws); a negative K-tile skips its pieces
   constexpr int CPOL = (VAR & 2048) ? 16 : 0;
+  // VAR 65536 (VOFF, the library kernel's addressing): every piece keeps its whole byte
+  // offset in its own VGPR (16 per lane) and the K-tile advances the descriptor's base
+  // (SALU, once per K-tile and operand) instead of a per-piece soffset SGPR
+  constexpr bool VOFF = (VAR & 65536) != 0;
+  int va[8], vw[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    va[i] = VOFF ? a_off[i & 1] + i * 16 * lda : 0;
+    vw[i] = VOFF ? w_off[i & 1] + i * 16 * ldw : 0;
+  }
   auto stage_piece = [&](int ka, int kw, int ws, int f) {
     const int i = f & 7;
+    if (VOFF) {
+      if (f < 8) {
+        if (ka >= 0) {
+          const int kp = kpos(ka) * BK;
+          buf_lds16<CPOL>(a_base + kp, a_bytes - kp * 2, abase(ka) + (64 * wid + 8 * i) * 128,
+                          va[i], 0);
+        }
+      } else if (kw >= 0) {
+        const int kp = kpos(kw) * BK;
+        buf_lds16<CPOL>(w_base + kp, w_bytes - kp * 2, wbase(kw, ws) + (64 * wid + 8 * i) * 128,
+                        vw[i], 0);
+      }
+      return;
+    }
     if (f < 8) {
       if (ka >= 0)
         buf_lds16<CPOL>(a_base, a_bytes, abase(ka) + (64 * wid + 8 * i) * 128, a_off[i & 1],
@@ -2076,6 +2100,9 @@ static int dispatch_tile(int tile_cfg, const void* A, int lda, const void* W, in
     // (sc1 loads, VAR 2048, measured neutral: profiles/r4/gemm4w/s17_*)
     case 45: return launch_4w<EPI, 8 | 4096>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
 #if DLI_GEMM_AB_VARIANTS
+    // 47 = 45 with the library's DMA addressing (a voffset VGPR per piece, soffset 0, the
+    // descriptor base advanced per K-tile): -2 % .. +0.7 % (profiles/r4/gemm4w/s25_*)
+    case 47: return launch_4w<EPI, 8 | 4096 | 65536>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
     // 46 = 45 with column-major MFMA order (weight operand reused 8x, the library's order):
     // within 0.2 % of 45 (profiles/r4/gemm4w/s23_*)
     case 46: return launch_4w<EPI, 8 | 4096 | 32768>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
