@@ -1534,8 +1534,29 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(
   static_assert(!(TWO_B && RS), "two-barrier schedule: LDS-DMA staging only");
   // SA / SW: this K-tile stages A(kt+2) / W(kt+2, DEEP: kt+3); PW: the previous K-tile
   // staged W (DEEP: its pieces may still fly at B2)
+  // VAR 131072 (STAMP, diagnostic build only): s_memtime stamps around the two barriers and
+  // the DMA window, summed over the K loop per segment and written by each workgroup's
+  // first lane to the workspace (read the SHARES: every stamp drains the LDS reads)
+  constexpr bool STAMP = (VAR & 131072) != 0;
+  unsigned long long sseg[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long st_prev = 0;
+  auto stamp = [&]() __attribute__((always_inline)) -> unsigned long long {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+  };
+  auto mark = [&](int seg) __attribute__((always_inline)) {
+    if constexpr (STAMP) {
+      const unsigned long long t = stamp();
+      sseg[seg] += t - st_prev;
+      st_prev = t;
+    }
+  };
   auto ktile2 = [&](auto SA, auto SW, auto PW, bool more, int kt)
       __attribute__((always_inline)) {
+    if constexpr (STAMP) st_prev = stamp();
     constexpr bool sa = decltype(SA)::value, sw = decltype(SW)::value;
     constexpr bool pw = DEEP && decltype(PW)::value;
     constexpr bool sd = sa || sw;
@@ -1570,18 +1591,24 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(
         __builtin_amdgcn_sched_barrier(0);
       }
       if (q == QB1 && !(VAR & 128)) {
+        mark(0);                                   // MFMAs 0..QB1 + the F1 reads
         __builtin_amdgcn_s_waitcnt(0xC07F);        // lgkmcnt(0)
         barrier();
+        mark(1);                                   // B1
       }
+      if (q == QB1 + 80) mark(2);                  // the DMA window
       if (sd && !(VAR & 64) && q > QB1 && q <= QB1 + 80 && (q - QB1 - 1) % 5 == 0) {
         stage_piece(sa ? kt + 2 : -1, sw ? kt + (DEEP ? 3 : 2) : -1, wsl, (q - QB1 - 1) / 5);
         __builtin_amdgcn_sched_barrier(0);
       }
       if (q == QB2 && more && !(VAR & 128)) {
+        mark(3);                                   // MFMAs after the DMA window
         constexpr int fly = (VAR & 64) ? 0 : 8 * ((sa ? 1 : 0) + (sw ? 1 : 0) + (pw ? 1 : 0));
         wait_vmcnt<fly>();
         barrier();
+        mark(4);                                   // B2
       }
+      if (q == 127) mark(5);                       // MFMAs after B2 + the F0 reads
       if (more) {                                  // F0(kt+1)
         if (QB2 == 127) {
           if (q == 127) {
@@ -1660,6 +1687,14 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(
 
   // ---- epilogue (transposed accumulators):
   // acc[I][J][r] = C[m0 + 128 wm + 16I + fr][n0 + 128 wn + 16J + 4fq + r]
+  if constexpr (STAMP) {
+    if (threadIdx.x == 0 && ws != nullptr) {
+      unsigned long long* o = reinterpret_cast<unsigned long long*>(ws) + (long)blockIdx.x * 8;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) o[k] = sseg[k];
+      o[6] = (unsigned long long)nk;
+    }
+  }
   const int wr0 = m0 + 128 * wm, wc0 = n0 + 128 * wn;
   if (gridDim.y > 1) {
     float* slab = ws + (long)ks * M * N;
@@ -2100,6 +2135,12 @@ static int dispatch_tile(int tile_cfg, const void* A, int lda, const void* W, in
     // (sc1 loads, VAR 2048, measured neutral: profiles/r4/gemm4w/s17_*)
     case 45: return launch_4w<EPI, 8 | 4096>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
 #if DLI_GEMM_AB_VARIANTS
+    // diagnostic: 48 = 45 with s_memtime stamps (per-workgroup segment sums into ws;
+    // scripts/stamp_gemm4w.py, profiles/r4/gemm4w/s26_stamps_tile45.jsonl)
+    case 48:
+      if constexpr (EPI == EPI_BF16)
+        return launch_4w<EPI, 8 | 4096 | 131072>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
+      return (int)hipErrorInvalidValue;
     // 47 = 45 with the library's DMA addressing (a voffset VGPR per piece, soffset 0, the
     // descriptor base advanced per K-tile): -2 % .. +0.7 % (profiles/r4/gemm4w/s25_*)
     case 47: return launch_4w<EPI, 8 | 4096 | 65536>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
