@@ -35,9 +35,10 @@ def main():
     h = torch.randn(B, F, device=dev).to(torch.bfloat16)
     res = torch.randn(B, D, device=dev).to(torch.bfloat16)
     nw = torch.ones(D, device=dev, dtype=torch.bfloat16)
-    # plans measured best at M=512 by the in-situ autotuner (with their fused reduces)
+    # plans the in-situ autotuner picks at M=512 (with their fused reduces; round 4:
+    # profiles/r4/prof/llama_b512_head.wave.txt)
     G.set_plan(B, nqkv, D, "splitk", G.GemmPlan("dli", 23, 2))
-    G.set_plan(B, D, D, "splitk", G.GemmPlan("dli", 17, 4))
+    G.set_plan(B, D, D, "splitk", G.GemmPlan("dli", 16, 4))
     G.set_plan(B, 2 * F, D, "silu_mul", G.GemmPlan("dli", 22, 1))
     G.set_plan(B, D, F, "splitk", G.GemmPlan("dli", 22, 8))
     G.set_plan(B, V, D, "f32", G.GemmPlan("dli", 22, 1))
