@@ -1236,9 +1236,14 @@ __device__ __forceinline__ uint4 buf_ld16(const void* base, int nbytes, int voff
 // VAR bits: 1 = stagger-U (workgroup t starts its K loop at K-tile t % 8 and wraps: the
 // concurrent workgroups of a wave of the grid spread over memory channels), 8 / 16 = grouped
 // tile order (GM 4 / 8 tile-rows per group, as gemm8p), 2 = all 16 next-half reads up front,
-// 4 = all 16 LDS-DMA pieces of a K-tile up front (default: one per 4 MFMAs).
-// Diagnostics only (wrong results, timing of the remaining work): 64 = no LDS-DMA in the K
-// loop, 128 = also no barrier / waits.
+// 4 = all 16 LDS-DMA pieces of a K-tile up front (default: one per 4 MFMAs), 32 = deep W
+// ring (3 W stages), 1024 = register staging, 2048 = sc1 loads, 4096 = the two-barrier K-tile
+// (ktile2 below; tile 45, the default 4-wave tile), 8192 / 16384 = its other barrier
+// placements, 32768 = column-major MFMA order, 65536 = per-piece voffset addressing.
+// Diagnostics only: 64 = no LDS-DMA in the K loop, 128 = also no barrier / waits (wrong
+// results, timing of the remaining work), 131072 = s_memtime stamps (correct results).
+// Only tiles 34 (VAR 8), 41 (8 | 32) and 45 (8 | 4096) are built by default; the rest with
+// DLI_GEMM_AB=1 (measurements: profiles/r4/gemm4w/).
 template <int EPI, int VAR = 0>
 __global__ void __launch_bounds__(256, 1) gemm4w_kernel(
     const u16* __restrict__ A, int lda, const u16* __restrict__ W, int ldw,

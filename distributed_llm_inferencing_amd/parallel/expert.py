@@ -35,6 +35,7 @@ import torch
 import torch.distributed as dist
 
 from .. import ops
+from ..engine.batch import DECODE
 from ..engine.llm_engine import LLMEngine
 from ..models.configs import get_config
 from ..models.model import TransformerLM
@@ -313,6 +314,14 @@ class ExpertParallelEngine:
         self.steps = 0
         self.graph_steps = 0
         self.lockstep_syncs = 0
+        # a rank whose peers are decoding admits prompts in chunks of at most max_batch
+        # tokens, so the step stays within the peers' captured receive regions and they keep
+        # replaying their decode graphs (a larger prefill sends every rank eager for that
+        # step); DLI_EP_PREFILL_CAP=0 turns it off
+        self.prefill_cap = os.environ.get("DLI_EP_PREFILL_CAP", "1") == "1"
+        self._full_prefill = self.engine.scheduler.max_prefill_tokens
+        self._peers_decoding = False
+        self.capped_steps = 0
 
     def warmup(self):
         """Capture the decode graphs (every rank, same bucket order: the warm-up forwards
@@ -360,12 +369,22 @@ class ExpertParallelEngine:
             if bits:
                 from .transport import DataPlaneError
                 raise DataPlaneError(bits)
+        sch = eng.scheduler
+        capped = self.prefill_cap and self._peers_decoding
+        sch.max_prefill_tokens = min(self._full_prefill, self.max_batch) if capped \
+            else self._full_prefill
         meta = eng.plan_step()
         work = meta is not None or eng.has_work()
         info = self._exchange(work, 0 if meta is None else meta.num_tokens)
         if not any(w for w, _ in info):
             return eng.finish_step(None), False
         toks = [t for _, t in info]
+        if capped and meta is not None and meta.kind != DECODE:
+            self.capped_steps += 1
+        # peers with a graph-sized step (decode, or a capped prefill) keep their graphs only
+        # if this rank's next step stays graph-sized too
+        self._peers_decoding = any(0 < t <= self.max_batch
+                                   for r, (w, t) in enumerate(info) if r != self.rank and w)
         self.moe.begin_step(toks)
         # a captured decode graph sizes its receive regions for decode batches: when any
         # rank's step is larger (a prefill), every rank runs this step eagerly

@@ -223,6 +223,47 @@ def test_expert_parallel_over_fifo_mailboxes_matches_dense(tmp_path, model, worl
         assert sent <= routed                        # no padding rows cross ranks
 
 
+def _ep_cap_worker(rank, world, port, q):
+    """Rank 1 receives its prompts while rank 0 is already decoding: it must admit them in
+    chunks of at most max_batch tokens (peers keep their graph-sized steps) and still
+    produce the dense model's tokens."""
+    _env(rank, world, port, DLI_EP_COMM="ipc")
+    import torch.distributed as dist
+    from distributed_llm_inferencing_amd.parallel.expert import ExpertParallelEngine
+    eng = ExpertParallelEngine("mixtral-tiny", "cpu", max_batch=8, max_model_len=96,
+                               num_blocks=64, dtype=torch.float32)
+    sp = SamplingParams(max_length=40, do_sample=False, ignore_eos=True)
+    early = PROMPTS[:3] if rank == 0 else []
+    late = [[(7 * i + j) % 50 + 3 for j in range(20)] for i in range(3)] if rank == 1 else []
+    rids = [eng.engine.add_request(p, sp) for p in early]
+    outs, steps, big = {}, 0, 0
+    while True:
+        if steps == 4:
+            rids += [eng.engine.add_request(p, sp) for p in late]
+        o, more = eng.step()
+        outs.update({x.request_id: x.all_ids for x in o})
+        steps += 1
+        if not more and steps > 4:
+            break
+    q.put((rank, early + late, [outs[r] for r in rids], eng.capped_steps))
+    dist.barrier()
+    eng.moe.close()
+    dist.destroy_process_group()
+
+
+def test_expert_parallel_caps_prefill_while_peers_decode():
+    res = _spawn(_ep_cap_worker, 2, n_results=2)
+    eng = LLMEngine("mixtral-tiny", device="cpu", dtype=torch.float32, max_batch=8,
+                    max_model_len=96, num_blocks=64)
+    sp = SamplingParams(max_length=40, do_sample=False, ignore_eos=True)
+    for rank, prompts, out, capped in res:
+        assert out == [o.all_ids for o in eng.generate(prompts, sp)], rank
+        if rank == 1:
+            assert capped >= 3          # 60 prompt tokens admitted 8 at a time
+        else:
+            assert capped == 0
+
+
 # ------------------------------------------------------------------------------ hardening
 def _ep_overflow_worker(rank, world, port, q):
     """Rank 0 'replays' a decode graph of bucket 8 holding 5 live rows (every row of the
