@@ -19,7 +19,11 @@
 // (rope_cache), so keys come from the cache through the block table: a chunk of len queries
 // at positions [ctx - len, ctx) attends over all ctx cached keys of its sequence (earlier
 // chunks, a recomputed prefix) with the causal bound shifted by ctx - len.
-// Grid: (ceil(max_len / 64), num_seqs, Hq).
+// Grid: (ceil(max_len / (16 wph)), num_seqs, Hq * wph / 4). wph = waves per query head: 4
+// (64 rows per workgroup) in general; for batches of short prompts (max_len <= 32 / 16) a
+// workgroup packs 2 / 4 query heads of one GQA group (2 / 1 waves each): the K/V tiles it
+// stages serve every packed head, and no wave idles past a 32-token prompt (the bench's
+// 512 x 32-token prefill ran 16,384 half-idle workgroups).
 #include "common.h"
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -36,7 +40,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))
     const int* __restrict__ cu_seqlens, int hq, int hkv, float scale_log2,
     const int* __restrict__ ctx_lens, const u16* __restrict__ k_cache,
     const u16* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
-    int block_size) {
+    int block_size, int wph) {
   constexpr int KK = HD / 32, DB = HD / 16;
   constexpr int KROW = HD + 8;                     // K row in LDS (u16): 272 B for hd 128
   constexpr int VROW = HD + 16;                    // V row in LDS (u16): hd*2 + 32 B
@@ -44,15 +48,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))
   constexpr int PER = PF_KT * CH / 256;            // chunks per thread per tile (K or V)
   __shared__ __attribute__((aligned(16))) u16 ktile[PF_KT * KROW];
   __shared__ __attribute__((aligned(16))) u16 vtile[PF_KT * VROW];
-  const int seq = blockIdx.y, h = blockIdx.z;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int seq = blockIdx.y, h = blockIdx.z * (PF_WAVES / wph) + wid / wph;
   const int col = lane & 15, grp = lane >> 4;
   const int s0 = cu_seqlens[seq], len = cu_seqlens[seq + 1] - s0;
   const int nkeys = PAGED ? ctx_lens[seq] : len;                 // keys visible to the chunk
   const int qoff = nkeys - len;                                  // position of query row 0
-  const int wg_q0 = blockIdx.x * PF_WAVES * PF_QROWS;
+  const int wg_q0 = blockIdx.x * wph * PF_QROWS;
   if (wg_q0 >= len) return;                                      // workgroup-uniform exit
-  const int q0 = wg_q0 + wid * PF_QROWS;                         // this wave's first row
+  const int q0 = wg_q0 + (wid % wph) * PF_QROWS;                 // this wave's first row
   const bool active = q0 < len;
   const int G = hq / hkv, kvh = h / G;
   const u16* qbase = qkv + (long)h * HD;
@@ -76,7 +80,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))
   f32x4 o_acc[DB];
 #pragma unroll
   for (int i = 0; i < DB; ++i) o_acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int kend_wg = min(nkeys, qoff + wg_q0 + PF_WAVES * PF_QROWS);  // last row's bound
+  const int kend_wg = min(nkeys, qoff + wg_q0 + wph * PF_QROWS);       // last row's bound
   const int kend_w = min(nkeys, qoff + q0 + PF_QROWS);                 // this wave's bound
 
   uint4 kreg[PER], vreg[PER];
@@ -210,6 +214,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))
 // shortest max_seqlen that takes the 256-row kernel; below, the 64-row kernel wastes fewer
 // idle waves (settable for A/B runs and tests: dli_prefill_set_min_len)
 static int g_pl_min_len = 256;
+static int g_pf_pack = 1;                          // head packing for short prompts (A/B)
 
 // Tile image: 8-row x 32-column subtiles of 512 B (cdna_hip_programming.md §5.5 T10, image
 // (a)): conflict-free for the 32x32x16 row reads (ds_read_b128) AND the transposed reads
@@ -457,16 +462,22 @@ static int launch_prefill(void* out, int out_stride, const void* qkv, int row_st
         (const u16*)k_cache, (const u16*)v_cache, block_tables, bt_stride, block_size);
     DLI_RETURN_LAUNCH();
   }
-  const int rows_per_wg = PF_WAVES * PF_QROWS;
-  dim3 grid((max_seqlen + rows_per_wg - 1) / rows_per_wg, num_seqs, hq);
+  // waves per query head: pack 2 / 4 heads of one GQA group into a workgroup for short
+  // prompts (the packed heads share their kv head, so G must be a multiple of the pack)
+  const int G = hq / hkv;
+  int wph = PF_WAVES;
+  if (g_pf_pack && max_seqlen <= PF_QROWS && G % 4 == 0) wph = 1;
+  else if (g_pf_pack && max_seqlen <= 2 * PF_QROWS && G % 2 == 0) wph = 2;
+  const int rows_per_wg = wph * PF_QROWS;
+  dim3 grid((max_seqlen + rows_per_wg - 1) / rows_per_wg, num_seqs, hq * wph / PF_WAVES);
   if (hd == 128)
     prefill_attn_kernel<128, PAGED><<<grid, 256, 0, st>>>(
         (u16*)out, out_stride, (const u16*)qkv, row_stride, cu_seqlens, hq, hkv, sl2, ctx_lens,
-        (const u16*)k_cache, (const u16*)v_cache, block_tables, bt_stride, block_size);
+        (const u16*)k_cache, (const u16*)v_cache, block_tables, bt_stride, block_size, wph);
   else
     prefill_attn_kernel<64, PAGED><<<grid, 256, 0, st>>>(
         (u16*)out, out_stride, (const u16*)qkv, row_stride, cu_seqlens, hq, hkv, sl2, ctx_lens,
-        (const u16*)k_cache, (const u16*)v_cache, block_tables, bt_stride, block_size);
+        (const u16*)k_cache, (const u16*)v_cache, block_tables, bt_stride, block_size, wph);
   DLI_RETURN_LAUNCH();
 }
 
@@ -491,6 +502,13 @@ extern "C" int dli_prefill_attention_paged(void* out, int out_stride, const void
   return launch_prefill<true>(out, out_stride, qkv, row_stride, cu_seqlens, num_seqs,
                               max_seqlen, hq, hkv, hd, scale, ctx_lens, k_cache, v_cache,
                               block_tables, bt_stride, block_size, st);
+}
+
+// 0 / 1: head packing of the short-prompt kernel off / on; returns the previous setting
+extern "C" int dli_prefill_set_pack(int on) {
+  const int old = g_pf_pack;
+  g_pf_pack = on ? 1 : 0;
+  return old;
 }
 
 extern "C" int dli_prefill_set_min_len(int n) {

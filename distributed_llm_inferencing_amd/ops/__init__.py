@@ -352,6 +352,13 @@ def prefill_long_min_len(n: int = 0) -> int:
     return int(N.require_native().dli_prefill_set_min_len(int(n)))
 
 
+def prefill_set_pack(on: bool) -> bool:
+    """Head packing of the short-prompt prefill attention kernel (2 / 4 query heads of a GQA
+    group per workgroup when every prompt of the batch is <= 32 / 16 tokens); returns the
+    previous setting (A/B switch, on by default)."""
+    return bool(N.require_native().dli_prefill_set_pack(1 if on else 0))
+
+
 def prefill_attention_paged(qkv, cu_seqlens, max_seqlen: int, context_lens, block_tables,
                             k_cache, v_cache, hq, hkv, hd, scale, out=None):
     """Chunked prefill attention: each sequence's chunk of queries (packed rows of ``qkv``)

@@ -353,6 +353,28 @@ def test_rope_cache(gpu, hq, hkv, hd):
     assert torch.equal(vc, vc1)
 
 
+@pytest.mark.parametrize("hq,hkv,hd", [(32, 8, 128), (8, 1, 128), (12, 6, 64), (12, 12, 64)])
+@pytest.mark.parametrize("lens", [[1], [16, 3], [7, 32, 20], [32] * 5])
+def test_prefill_attention_short_prompts_packed(gpu, hq, hkv, hd, lens):
+    """Batches of prompts <= 32 / 16 tokens pack 2 / 4 query heads of a GQA group into one
+    workgroup: bit-identical to the unpacked kernel and close to the fp32 reference (G = 1:
+    no packing)."""
+    qkv, *_ = _paged_setup(gpu, lens, hq, hkv, hd, 16)
+    cu = torch.tensor([0] + list(np.cumsum(lens)), device=gpu, dtype=torch.int32)
+    scale = 1 / math.sqrt(hd)
+    old = ops.prefill_set_pack(True)
+    try:
+        packed = ops.prefill_attention(qkv, cu, max(lens), hq, hkv, hd, scale)
+        ops.prefill_set_pack(False)
+        plain = ops.prefill_attention(qkv, cu, max(lens), hq, hkv, hd, scale)
+    finally:
+        ops.prefill_set_pack(old)
+    assert torch.equal(packed, plain)
+    q, k, v = R.split_qkv(qkv, hq, hkv, hd)
+    ref = R.prefill_attention(q, k, v, cu, scale).reshape(len(qkv), -1)
+    close(packed, ref, rtol=2e-2, atol=2e-2)
+
+
 @pytest.mark.parametrize("hq,hkv,hd", [(32, 8, 128), (12, 12, 64), (8, 1, 128)])
 @pytest.mark.parametrize("lens", [[1], [7, 33, 64], [130, 5]])
 def test_prefill_attention(gpu, hq, hkv, hd, lens):
@@ -805,7 +827,10 @@ def test_decode_attention_32k_context(gpu):
 @pytest.mark.parametrize("hq,hkv,hd,bs,chunks", [
     (32, 8, 128, 16, [(100, 37), (2053, 512), (16, 16), (1, 1)]),
     (12, 12, 64, 32, [(70, 70), (300, 64), (129, 1)]),
-    (8, 1, 128, 16, [(4096, 700)])])
+    (8, 1, 128, 16, [(4096, 700)]),
+    # short chunks only: the head-packed kernel over a paged cache
+    (32, 8, 128, 16, [(100, 17), (33, 32), (5, 5)]),
+    (8, 2, 128, 16, [(64, 16), (300, 9)])])
 def test_prefill_attention_paged_chunks(gpu, hq, hkv, hd, bs, chunks):
     """Chunked prefill: each chunk of queries (positions [ctx-L, ctx)) attends over all ctx
     keys of its sequence in a scattered paged cache, vs the fp32 reference."""
