@@ -162,7 +162,9 @@ __device__ __forceinline__ void row_scan(const float* __restrict__ x, int V, F&&
 // chunk had more than CAPC ties at its threshold (overflow flag) read the full row as before.
 #define SMP_CAPC 64
 #define SMP_CHUNK_MAX 4096
-#define SMP_SPLIT_MAX_B 8
+#define SMP_SPLIT_MAX_B 8                       // default largest two-phase batch
+#define SMP_SPLIT_CAP_B 1024                    // largest batch dli_sample_set_split_max_b takes
+static int g_smp_max_b = SMP_SPLIT_MAX_B;
 
 __device__ __forceinline__ bool smp_split_ok(float T, int K, float P) {
   const bool greedy = T <= 0.f || K == 1;
@@ -440,25 +442,34 @@ __global__ void __launch_bounds__(SMP_THREADS) sample_kernel(
 
 // Bytes of the two-phase workspace dli_sample takes for a batch of B rows (0: one phase).
 extern "C" long dli_sample_workspace_bytes(int B, int V) {
-  if (B <= 0 || B > SMP_SPLIT_MAX_B) return 0;
-  return (long)SMP_SPLIT_MAX_B * 4 + (long)B * 64 * SMP_CAPC * 8;
+  if (B <= 0 || B > g_smp_max_b) return 0;
+  return (long)g_smp_max_b * 4 + (long)B * 64 * SMP_CAPC * 8;
 }
 
-// ws: nullable; when given (>= dli_sample_workspace_bytes, its first SMP_SPLIT_MAX_B ints
+// Largest batch that samples in two phases (default SMP_SPLIT_MAX_B = 8; A/B runs raise it:
+// the workspace layout follows it, so set it before the first workspace is sized). Returns
+// the previous value.
+extern "C" int dli_sample_set_split_max_b(int b) {
+  const int old = g_smp_max_b;
+  if (b >= 1 && b <= SMP_SPLIT_CAP_B) g_smp_max_b = b;
+  return old;
+}
+
+// ws: nullable; when given (>= dli_sample_workspace_bytes, its first g_smp_max_b ints
 // zero before the first call — the kernels leave them zero), batches of B <= 8 rows sample in
 // two phases (above).
 extern "C" int dli_sample(int* out_tokens, const float* logits, long row_stride, int B, int V,
                           const float* temperature, const int* top_k, const float* top_p,
                           const long long* seeds, void* ws, hipStream_t st) {
   if (B <= 0) return 0;
-  if (ws != nullptr && B <= SMP_SPLIT_MAX_B) {
+  if (ws != nullptr && B <= g_smp_max_b) {
     // P chunks per row: >= 256 workgroups in all, each chunk <= SMP_CHUNK_MAX entries
     int P = 1;
     while (P < 64 && (B * P < 256 || (V + P - 1) / P > SMP_CHUNK_MAX)) P <<= 1;
     const int L = (((V + P - 1) / P) + 3) & ~3;
     if (L <= SMP_CHUNK_MAX) {
       int* overflow = static_cast<int*>(ws);
-      float* cand_v = reinterpret_cast<float*>(overflow + SMP_SPLIT_MAX_B);
+      float* cand_v = reinterpret_cast<float*>(overflow + g_smp_max_b);
       int* cand_i = reinterpret_cast<int*>(cand_v + (long)B * 64 * SMP_CAPC);
       sample_chunk_kernel<<<dim3(P, B), 256, 0, st>>>(cand_v, cand_i, overflow, logits,
                                                        row_stride, V, L, temperature, top_k,

@@ -441,8 +441,11 @@ def _sample_ws(device, B: int, V: int):
         return None
     key = (device.type, device.index)
     ws = _sample_wss.get(key)
-    if ws is None:
-        nbytes = int(lib.dli_sample_workspace_bytes(8, V))
+    nbytes = int(lib.dli_sample_workspace_bytes(B, V))
+    if ws is None or ws.numel() < nbytes:
+        # sized for the largest two-phase batch (the library's split limit; 8 by default)
+        maxb = int(lib.dli_sample_set_split_max_b(0))
+        nbytes = max(nbytes, int(lib.dli_sample_workspace_bytes(maxb, V)))
         ws = _sample_wss[key] = torch.zeros(nbytes, dtype=torch.uint8, device=device)
     return ws
 

@@ -44,6 +44,7 @@ _SIGS = {
     "dli_prefill_attention": [P, I, P, I, P, I, I, I, I, I, F, P],
     "dli_prefill_set_min_len": [I],
     "dli_prefill_set_pack": [I],
+    "dli_sample_set_split_max_b": [I],
     "dli_decode_set_pipe": [I],
     "dli_decode_get_pipe": [],
     "dli_gemm_set_slab_store": [I],
@@ -96,6 +97,8 @@ def _load():
                 fn.restype = ctypes.c_long if name.endswith("_bytes") else ctypes.c_int
             if os.environ.get("DLI_PREFILL_PACK", "1") == "0":   # A/B: unpacked prefill
                 lib.dli_prefill_set_pack(0)
+            if os.environ.get("DLI_SAMPLE_SPLIT_MAX_B"):         # A/B: two-phase sampler
+                lib.dli_sample_set_split_max_b(int(os.environ["DLI_SAMPLE_SPLIT_MAX_B"]))
             _lib = lib
         except Exception as e:  # noqa: BLE001 - surfaced by require_native()
             _load_error = e

@@ -552,6 +552,36 @@ def test_sampling_fallback_path_adversarial(gpu):
         assert (tok % 512 == 0).all()
 
 
+@pytest.mark.parametrize("B,V", [(64, 128256), (512, 128256)])
+def test_sampling_two_phase_large_batch(gpu, B, V):
+    """The two-phase sampler with its batch limit raised (dli_sample_set_split_max_b, the
+    DLI_SAMPLE_SPLIT_MAX_B A/B switch): 32 chunks per 128k row, same tokens as one phase."""
+    lib = ops.N.require_native()
+    old = lib.dli_sample_set_split_max_b(512)
+    ops._sample_wss.clear()
+    try:
+        torch.manual_seed(16)
+        logits = torch.randn(B, V, device=gpu) * 3
+        ws = ops._sample_ws(logits.device, B, V)
+        assert ws is not None
+        for T, K, P in [(0.8, 50, 0.95), (0.0, 1, 1.0), (1.0, 64, 0.5)]:
+            temp = torch.full((B,), T, device=gpu)
+            topk = torch.full((B,), K, device=gpu, dtype=torch.int32)
+            topp = torch.full((B,), P, device=gpu)
+            seeds = torch.arange(B, device=gpu, dtype=torch.int64) * 7919 + 5
+            one = torch.empty(B, dtype=torch.int32, device=gpu)
+            two = torch.empty(B, dtype=torch.int32, device=gpu)
+            for o, w in ((one, None), (two, ws)):
+                assert lib.dli_sample(ops._p(o), ops._p(logits), logits.stride(0), B, V,
+                                      ops._p(temp), ops._p(topk), ops._p(topp), ops._p(seeds),
+                                      ops._p(w), ops._st()) == 0
+            assert torch.equal(one, two), (T, K, P)
+        torch.cuda.synchronize()
+    finally:
+        lib.dli_sample_set_split_max_b(old)
+        ops._sample_wss.clear()
+
+
 @pytest.mark.parametrize("B,V", [(1, 128256), (3, 50257), (8, 128256), (2, 1000)])
 def test_sampling_two_phase_matches_one_phase(gpu, B, V):
     """Small batches sample in two phases (per-chunk candidate lists, sampling.hip
