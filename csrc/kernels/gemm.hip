@@ -1951,18 +1951,18 @@ __device__ __forceinline__ float dot8_acc(const bf16x8v w, const bf16x8v x, floa
   return acc;
 }
 
-// The weight stream of one workgroup: res[m][j] = sum over this K slice of
-// A[m, :] . W[n_base + j, :] (j < R = 4 RW), reduced across the wave and staged in LDS.
+// The weight stream of one workgroup: res[m][wid * RW + r] = sum over this K slice of
+// A[m, :] . W[r0 + r, :] (r < RW), reduced across the wave and staged in LDS.
 template <int MB, int RW, int UNROLL>
 __device__ __forceinline__ void gemv_core(const u16* __restrict__ A, int lda,
                                           const u16* __restrict__ W, int ldw, int M, int N,
-                                          int K, int k_split_len, int n_base, int ks,
+                                          int K, int k_split_len, int r0, int ks,
                                           float (&res)[MB][4 * RW]) {
+  // r0: this wave's first weight row (rows r0 .. r0 + RW - 1 land in res[.][wid * RW ..])
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int kb = ks * k_split_len;
   const int klen = min(k_split_len, K - kb);
   const int nchunk = klen >> 3;                     // 8-element chunks of the K slice
-  const int r0 = n_base + wid * RW;                 // this wave's first row
   const bf16x8v* wrow[RW];
 #pragma unroll
   for (int r = 0; r < RW; ++r) {
@@ -2018,22 +2018,41 @@ __device__ __forceinline__ void gemv_core(const u16* __restrict__ A, int lda,
     }
 }
 
-template <int MB, int RW, int EPI, int UNROLL>
+// H16 (SiLU*up only, RW = 4): 16 rows per workgroup as 8 gate + 8 up rows of one 32-row
+// gate/up block (waves 0-1 the gate half h, waves 2-3 the matching up half), so the pairing
+// runs at the 16-row grid (2x the workgroups of the 32-row tile; profiles/r4/b1/)
+template <int MB, int RW, int EPI, int UNROLL, bool H16 = false>
 __global__ void __launch_bounds__(256) gemv_kernel(
     const u16* __restrict__ A, int lda, const u16* __restrict__ W, int ldw,
     void* __restrict__ C, int ldc, int M, int N, int K, int k_split_len,
     const u16* __restrict__ bias, float* __restrict__ ws) {
   constexpr int R = 4 * RW;
+  static_assert(!H16 || (EPI == EPI_SILU && RW == 4), "H16 pairs 8 gate + 8 up rows");
   __shared__ float res[MB][R];
   const int n_base = blockIdx.x * R;
   const int ks = blockIdx.y;
-  gemv_core<MB, RW, UNROLL>(A, lda, W, ldw, M, N, K, k_split_len, n_base, ks, res);
+  const int wid = threadIdx.x >> 6;
+  const int blk = blockIdx.x >> 1, half = blockIdx.x & 1;
+  // weight row of res column j
+  auto row_of = [&](int j) {
+    return H16 ? blk * 32 + (j < 8 ? half * 8 + j : 16 + half * 8 + (j - 8)) : n_base + j;
+  };
+  gemv_core<MB, RW, UNROLL>(A, lda, W, ldw, M, N, K, k_split_len, row_of(wid * RW), ks, res);
   __syncthreads();
   // epilogue: one thread per (row m, output column)
   if (ws != nullptr && gridDim.y > 1) {             // fp32 partial slab of this K slice
     for (int t = threadIdx.x; t < MB * R; t += 256) {
-      const int m = t / R, j = t % R, n = n_base + j;
+      const int m = t / R, j = t % R, n = row_of(j);
       if (m < M && n < N) ws[((long)ks * M + m) * N + n] = res[m][j];
+    }
+    return;
+  }
+  if (H16) {                                        // res 0-7 gate, 8-15 the matching up
+    for (int t = threadIdx.x; t < MB * 8; t += 256) {
+      const int m = t / 8, j = t % 8;
+      const int f = blk * 16 + half * 8 + j;
+      if (m < M && blk * 32 < N)
+        ((u16*)C)[(long)m * ldc + f] = f2bf(silu_f(res[m][j]) * res[m][j + 8]);
     }
     return;
   }
@@ -2052,17 +2071,18 @@ __global__ void __launch_bounds__(256) gemv_kernel(
   }
 }
 
-template <int MB, int RW, int EPI, int UNROLL = 2>
+template <int MB, int RW, int EPI, int UNROLL = 2, bool H16 = false>
 static int launch_gemv(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M,
                        int N, int K, int splits, const void* bias, void* ws, hipStream_t st) {
   constexpr int R = 4 * RW;
-  if (M > MB || (EPI == EPI_SILU && (R != 32 || N % 32)) || K % 8 || lda % 8 || ldw % 8)
+  if (M > MB || (EPI == EPI_SILU && ((R != 32 && !H16) || N % 32)) || K % 8 || lda % 8 ||
+      ldw % 8)
     return (int)hipErrorInvalidValue;
   int ksl = K / splits;
   ksl = (ksl / 8) * 8;
   if (ksl * splits != K) return (int)hipErrorInvalidValue;
   dim3 grid((N + R - 1) / R, splits);
-  gemv_kernel<MB, RW, EPI, UNROLL><<<grid, 256, 0, st>>>((const u16*)A, lda, (const u16*)W, ldw, C, ldc,
+  gemv_kernel<MB, RW, EPI, UNROLL, H16><<<grid, 256, 0, st>>>((const u16*)A, lda, (const u16*)W, ldw, C, ldc,
                                                  M, N, K, ksl, (const u16*)bias,
                                                  splits > 1 ? (float*)ws : nullptr);
   if (splits > 1 && C != nullptr) {
@@ -2089,6 +2109,14 @@ static int dispatch_gemv(int tile_cfg, const void* A, int lda, const void* W, in
   if (tile_cfg == 33)
     return M <= 1 ? launch_gemv<1, 8, EPI, 4>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st)
                   : (int)hipErrorInvalidValue;
+  // 29: SiLU*up gate/up (M = 1) on the 16-row grid of tile 32 (8 gate + 8 up rows per
+  // workgroup), 4 K-steps in flight per lane
+  if (tile_cfg == 29) {
+    if constexpr (EPI == EPI_SILU)
+      return M <= 1 ? launch_gemv<1, 4, EPI, 4, true>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st)
+                    : (int)hipErrorInvalidValue;
+    return (int)hipErrorInvalidValue;
+  }
   if (M <= 1)
     return r32 ? launch_gemv<1, 8, EPI>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st)
                : launch_gemv<1, 4, EPI>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st);
@@ -2177,7 +2205,7 @@ static int dispatch_tile(int tile_cfg, const void* A, int lda, const void* W, in
     case 39: return launch_4w<EPI, 8 | 64 | 128>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, go, groups, st);
 #endif
     // skinny weight-streaming GEMM for M <= 4 (no grouped mode)
-    case 30: case 31: case 32: case 33:
+    case 29: case 30: case 31: case 32: case 33:
       if (go != nullptr) return (int)hipErrorInvalidValue;
       return dispatch_gemv<EPI>(tile_cfg, A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st);
 #undef DLI_CFG8
@@ -2191,14 +2219,14 @@ static int dispatch_tile(int tile_cfg, const void* A, int lda, const void* W, in
 // stages, 12 = 160x128 (MoE experts of ~130-190 rows in one pass); 13-17 = 8-wave tiles
 // 256x256, 256x128, 128x256 (2 stages) and 256x128, 128x256 (3 stages); 18/19 = 128x96 and
 // 20/21 = 128x64 with 2/3 stages; 22 = 256x256 8-phase ping-pong; 23/24 = 128x192 (3/2
-// stages), 25 = 256x192, 8 waves; 26 = 256x224 ping-pong; 30 / 31 = the M <= 4 weight
-// stream (16 / 32 rows per workgroup). ws: fp32 [splits, M, N] when splits>1.
+// stages), 25 = 256x192, 8 waves; 26 = 256x224 ping-pong; 29-33 = the M <= 4 weight
+// stream (16 / 32 rows per workgroup, dispatch_gemv). ws: fp32 [splits, M, N] when splits>1.
 // group_off (nullable): int[groups+1] row offsets; M is then the max rows of any group.
 extern "C" int dli_gemm(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M,
                         int N, int K, int epi, int tile_cfg, int splits, const void* bias,
                         void* ws, const int* group_off, int groups, hipStream_t st) {
   if (M <= 0 || N <= 0) return 0;
-  if ((tile_cfg < 30 && K % BK) || lda % 8 || ldw % 8 || splits < 1)
+  if (((tile_cfg < 29 || tile_cfg > 33) && K % BK) || lda % 8 || ldw % 8 || splits < 1)
     return (int)hipErrorInvalidValue;
   if (epi == EPI_SILU && N % 32) return (int)hipErrorInvalidValue;
   if (splits > 1 && ws == nullptr) return (int)hipErrorInvalidValue;

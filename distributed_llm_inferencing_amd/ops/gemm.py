@@ -64,7 +64,9 @@ PREFILL_4W_TILE = int(os.environ.get("DLI_GEMM_PREFILL_4W", "45"))
 MOE_PREFILL_TILE = int(os.environ.get("DLI_MOE_PREFILL_TILE", "45"))
 # weight-streaming skinny GEMM (gemm.hip gemv_kernel) for M <= GEMV_MAX_M rows: 16 / 32 output
 # rows per workgroup (31 for the SiLU*up gate/up pairing); not an MFMA tile, so kept apart
-GEMV_TILES = {30: 16, 31: 32, 32: 16, 33: 32}   # 32 / 33: 4 K-steps in flight per lane, M = 1
+GEMV_TILES = {30: 16, 31: 32, 32: 16, 33: 32,   # 32 / 33: 4 K-steps in flight per lane, M = 1
+              29: 16}   # 29: SiLU*up at M = 1 on the 16-row grid (8 gate + 8 up rows)
+GEMV_M1_ONLY = (29, 32, 33)
 GEMV_MAX_M = 4
 TILE_WAVES = {13: (2, 4), 14: (4, 2), 15: (2, 4), 16: (4, 2), 17: (2, 4),
               22: (2, 4), 23: (2, 4), 24: (2, 4), 25: (4, 2),
@@ -74,6 +76,8 @@ TILE_WAVES = {13: (2, 4), 14: (4, 2), 15: (2, 4), 16: (4, 2), 17: (2, 4),
 def tile_ok(tile: int, epi: str) -> bool:
     """The SiLU*up epilogue pairs 16-column gate/up blocks inside a wave's column range,
     which must therefore be a multiple of 32."""
+    if tile == 29:
+        return epi == "silu_mul"
     if tile in GEMV_TILES:
         return epi != "silu_mul" or tile in (31, 33)
     if epi != "silu_mul":
@@ -470,7 +474,7 @@ def candidate_plans(M: int, N: int, K: int, epi: str):
             out.append(GemmPlan("dli", tile, splits))
     if M <= GEMV_MAX_M:
         for tile in GEMV_TILES:
-            if tile in excl or not tile_ok(tile, epi) or (tile in (32, 33) and M > 1):
+            if tile in excl or not tile_ok(tile, epi) or (tile in GEMV_M1_ONLY and M > 1):
                 continue
             for splits in (1, 2, 4, 8):
                 if K % (64 * splits) == 0 and K // splits >= 512:

@@ -136,12 +136,14 @@ def test_gemm_4wave_256(gpu, M, N, K, epi, tile):
 
 @pytest.mark.parametrize("M", [1, 2, 3, 4])
 @pytest.mark.parametrize("N,K,epi", [(6144, 4096, "none"), (4096, 14336, "none"),
-                                     (28672, 4096, "silu_mul"), (50257, 768, "f32"),
+                                     (28672, 4096, "silu_mul"), (96, 768, "silu_mul"),
+                                     (50257, 768, "f32"),
                                      (2304, 768, "bias")])
 def test_gemv_skinny(gpu, M, N, K, epi):
-    """The M <= 4 weight-streaming GEMM (tiles 30 / 31) against the fp32 reference: every
+    """The M <= 4 weight-streaming GEMM (tiles 29-33) against the fp32 reference: every
     epilogue, split-K 1/2/4 (reduce kernel), a K (768) that is not a multiple of the
-    512-element wave step, and a final partial row block (N = 50257)."""
+    512-element wave step, and a final partial row block (N = 50257). Tile 29 (M = 1 SiLU*up
+    on the 16-row grid, 8 gate + 8 up rows per workgroup) runs on the gate/up shapes."""
     torch.manual_seed(7)
     x, w, b = rnd(M, K, dev=gpu), rnd(N, K, dev=gpu, scale=0.05), rnd(N, dev=gpu)
     if epi == "silu_mul":
@@ -153,7 +155,7 @@ def test_gemv_skinny(gpu, M, N, K, epi):
     else:
         ref = R.linear(x, w, out_dtype=torch.float32)
     for tile in G.GEMV_TILES:
-        if not G.tile_ok(tile, epi) or (tile in (32, 33) and M > 1):
+        if not G.tile_ok(tile, epi) or (tile in G.GEMV_M1_ONLY and M > 1):
             continue
         for splits in (1, 2, 4):
             if K % (64 * splits):
