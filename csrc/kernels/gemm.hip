@@ -2109,12 +2109,14 @@ static int dispatch_gemv(int tile_cfg, const void* A, int lda, const void* W, in
   if (tile_cfg == 33)
     return M <= 1 ? launch_gemv<1, 8, EPI, 4>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st)
                   : (int)hipErrorInvalidValue;
-  // 29: SiLU*up gate/up (M = 1) on the 16-row grid of tile 32 (8 gate + 8 up rows per
-  // workgroup), 4 K-steps in flight per lane
+  // 29: SiLU*up gate/up on the 16-row grid (8 gate + 8 up rows per workgroup); 4 K-steps
+  // in flight per lane at M = 1 (tile 32's depth), 2 at M = 2..4 (tile 30's)
   if (tile_cfg == 29) {
-    if constexpr (EPI == EPI_SILU)
-      return M <= 1 ? launch_gemv<1, 4, EPI, 4, true>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st)
-                    : (int)hipErrorInvalidValue;
+    if constexpr (EPI == EPI_SILU) {
+      if (M <= 1) return launch_gemv<1, 4, EPI, 4, true>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st);
+      if (M <= 2) return launch_gemv<2, 4, EPI, 2, true>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st);
+      if (M <= 4) return launch_gemv<4, 4, EPI, 2, true>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st);
+    }
     return (int)hipErrorInvalidValue;
   }
   if (M <= 1)

@@ -446,6 +446,8 @@ def _sample_ws(device, B: int, V: int):
         # sized for the largest two-phase batch (the library's split limit; 8 by default)
         maxb = int(lib.dli_sample_set_split_max_b(0))
         nbytes = max(nbytes, int(lib.dli_sample_workspace_bytes(maxb, V)))
+        if ws is not None:
+            G._retired.append(ws)        # a captured graph may still hold it (ops.gemm)
         ws = _sample_wss[key] = torch.zeros(nbytes, dtype=torch.uint8, device=device)
     return ws
 

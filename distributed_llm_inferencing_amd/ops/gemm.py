@@ -65,8 +65,8 @@ MOE_PREFILL_TILE = int(os.environ.get("DLI_MOE_PREFILL_TILE", "45"))
 # weight-streaming skinny GEMM (gemm.hip gemv_kernel) for M <= GEMV_MAX_M rows: 16 / 32 output
 # rows per workgroup (31 for the SiLU*up gate/up pairing); not an MFMA tile, so kept apart
 GEMV_TILES = {30: 16, 31: 32, 32: 16, 33: 32,   # 32 / 33: 4 K-steps in flight per lane, M = 1
-              29: 16}   # 29: SiLU*up at M = 1 on the 16-row grid (8 gate + 8 up rows)
-GEMV_M1_ONLY = (29, 32, 33)
+              29: 16}   # 29: SiLU*up on the 16-row grid (8 gate + 8 up rows), M <= 4
+GEMV_M1_ONLY = (32, 33)
 GEMV_MAX_M = 4
 TILE_WAVES = {13: (2, 4), 14: (4, 2), 15: (2, 4), 16: (4, 2), 17: (2, 4),
               22: (2, 4), 23: (2, 4), 24: (2, 4), 25: (4, 2),
@@ -104,14 +104,21 @@ class GemmPlan:
 _plan_cache: dict = {}
 _ws_lock = threading.Lock()
 _workspaces: dict = {}
+# buffers a larger workspace replaced: a captured hipGraph keeps the pointer it was captured
+# with, so a replaced buffer must outlive every graph (the prefill autotune runs after the
+# decode graphs are captured and grows the workspace; freeing the old buffer let eager
+# tensors take its memory while graph replays still wrote split-K slabs into it)
+_retired: list = []
 
 
 def workspace(device: torch.device, nbytes: int) -> torch.Tensor:
-    """Grow-only scratch (bytes) per device."""
+    """Grow-only scratch (bytes) per device. Never freed: see ``_retired``."""
     key = (device.type, device.index)
     with _ws_lock:
         ws = _workspaces.get(key)
         if ws is None or ws.numel() < nbytes:
+            if ws is not None:
+                _retired.append(ws)
             ws = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
             _workspaces[key] = ws
         return ws
@@ -148,7 +155,9 @@ def _heuristic(M: int, N: int, K: int, epi: str) -> GemmPlan:
     if M <= GEMV_MAX_M:
         # batch-1 / tiny batches: stream the weights (gemv_kernel) with enough workgroups
         # (>= 512, two per CU) to keep ~64 KB of loads in flight per CU
-        tile = 31 if epi == "silu_mul" else 30
+        # gate/up at M = 1: the 16-row SiLU grid (tile 29) 39.5 vs 49.0 us for the 32-row
+        # tile 31 (profiles/r4/b1/s37_gemv_sweep_m1.jsonl)
+        tile = (29 if M == 1 else 31) if epi == "silu_mul" else 30
         wgs = -(-N // GEMV_TILES[tile])
         splits = 1
         while (wgs * splits < 512 and K % (64 * splits * 2) == 0

@@ -358,3 +358,26 @@ def test_build_refuses_scratch_in_asm_mfma_kernels():
                 "gemm.hip:1:1: remark:     ScratchSize [bytes/lane]: 1040\n")
     with pytest.raises(RuntimeError, match="1040 B/lane"):
         build.check_scratch(bad, "gemm.hip")
+
+
+def test_gemm_workspace_growth_keeps_the_replaced_buffer_alive():
+    """ops.gemm.workspace grows by replacement; a hipGraph captured with the old buffer keeps
+    writing split-K slabs into it on replay (the prefill autotune grows the workspace after
+    the decode graphs are captured), so the old buffer must never return to the allocator."""
+    from distributed_llm_inferencing_amd.ops import gemm as G
+    dev = torch.device("cpu")
+    key = (dev.type, dev.index)
+    saved, n_ret = G._workspaces.pop(key, None), len(G._retired)
+    try:
+        small = G.workspace(dev, 1024)
+        ptr = small.data_ptr()
+        assert G.workspace(dev, 512) is small                 # fits: same buffer
+        big = G.workspace(dev, small.numel() + 1)
+        assert big is not small and big.numel() > small.numel()
+        assert any(t.data_ptr() == ptr for t in G._retired[n_ret:])
+    finally:
+        del G._retired[n_ret:]
+        if saved is not None:
+            G._workspaces[key] = saved
+        else:
+            G._workspaces.pop(key, None)
