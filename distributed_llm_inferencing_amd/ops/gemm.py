@@ -155,9 +155,9 @@ def _heuristic(M: int, N: int, K: int, epi: str) -> GemmPlan:
     if M <= GEMV_MAX_M:
         # batch-1 / tiny batches: stream the weights (gemv_kernel) with enough workgroups
         # (>= 512, two per CU) to keep ~64 KB of loads in flight per CU
-        # gate/up at M = 1: the 16-row SiLU grid (tile 29) 39.5 vs 49.0 us for the 32-row
-        # tile 31 (profiles/r4/b1/s37_gemv_sweep_m1.jsonl)
-        tile = (29 if M == 1 else 31) if epi == "silu_mul" else 30
+        # gate/up at M <= 2: the 16-row SiLU grid (tile 29) 39.5 / 43.3 vs 49.0 / 51.0 us for
+        # the 32-row tile 31 at M = 1 / 2 (profiles/r4/b1/s37_*, s38_gemv_sweep_m2.jsonl)
+        tile = (29 if M <= 2 else 31) if epi == "silu_mul" else 30
         wgs = -(-N // GEMV_TILES[tile])
         splits = 1
         while (wgs * splits < 512 and K % (64 * splits * 2) == 0

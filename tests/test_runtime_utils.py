@@ -297,6 +297,13 @@ def test_prefill_gemm_plan_is_own_kernel(monkeypatch):
     # 256x224 joins the autotune candidates where it lands on whole waves of the chip
     assert not any(p.tile == 26 for p in G.candidate_plans(512, 28672, 4096, "silu_mul"))
     assert any(p.tile == 26 for p in G.candidate_plans(512, 57344, 8192, "silu_mul"))
+    # batch 1-2 gate/up: the 16-row SiLU weight stream (tile 29, 8 gate + 8 up rows per
+    # workgroup); it competes in the decode autotune up to M = 4 and never outside SiLU
+    assert G.plan(1, 28672, 4096, "silu_mul") == G.GemmPlan("dli", 29, 1)
+    assert G.plan(2, 28672, 4096, "silu_mul").tile == 29
+    assert any(p.tile == 29 for p in G.candidate_plans(4, 28672, 4096, "silu_mul"))
+    assert not any(p.tile == 29 for p in G.candidate_plans(1, 4096, 4096, "splitk"))
+    assert not any(p.tile == 29 for p in G.candidate_plans(8, 28672, 4096, "silu_mul"))
     G.clear_plans()
     monkeypatch.setenv("DLI_GEMM_PREFILL_BLAS", "1")
     assert G.plan(16384, 6144, 4096, "none").backend == "hipblaslt"
