@@ -14,9 +14,17 @@ the single-GPU engine; N > 1 splits the 32 layers into N contiguous stages (one 
 ``parallel/pipeline.py``) with N + 1 microbatches of --batch requests in flight.
 
     python bench.py                               # N=1 defaults
+    python bench.py --gpus 8                      # spawns its 8 ranks (launch.py)
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8
 
-Rank 0 prints one JSON line.
+Without torchrun's environment, ``--gpus N > 1`` starts N child ranks itself (one per GPU,
+127.0.0.1 rendezvous) before anything touches the GPU, waits for them and exits with the
+first failing rank's code. ``DLI_SAME_DEVICE=1`` puts every rank on cuda:0 (a 1-GPU
+rehearsal: gloo process group, device-mailbox data plane).
+
+Rank 0 prints one JSON line; multi-rank lines name the resolved data plane (``ipc`` /
+``rccl`` / ``torch-rccl`` / ``torch-gloo``), the rank count, every rank's device and the
+number of distinct GPUs behind them.
 """
 from __future__ import annotations
 
@@ -101,7 +109,7 @@ def run_single(args, barrier=None):
         barrier()
     dt = time.perf_counter() - t0
     return {"tokens": toks, "seconds": dt, "latencies": lats, "global_batch": args.batch,
-            "parallelism": "single", "engine": eng.stats.snapshot()}
+            "parallelism": "single", "engine": eng.stats.snapshot(), "data_plane": "none"}
 
 
 def run_data_parallel(args, world, rank):
@@ -122,13 +130,16 @@ def run_data_parallel(args, world, rank):
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     lats = [None] * world
     dist.all_gather_object(lats, res["latencies"])
+    from distributed_llm_inferencing_amd.parallel.transport import gather_rank_info
+    infos = gather_rank_info(torch.device("cuda", local) if torch.cuda.is_available()
+                             else torch.device("cpu"))
     dist.barrier()
     dist.destroy_process_group()
     if rank != 0:
         return None
     return {"tokens": float(t[1].item()), "seconds": float(mx[0].item()),
             "latencies": [x for l in lats for x in l], "global_batch": args.batch * world,
-            "parallelism": f"dp{world}"}
+            "parallelism": f"dp{world}", "data_plane": "none", "ranks_info": infos}
 
 
 def run_pipeline(args, world, rank):
@@ -173,6 +184,16 @@ def main():
                          "replicas")
     a = ap.parse_args()
 
+    from distributed_llm_inferencing_amd import launch
+    if a.gpus > 1 and not launch.under_launcher():
+        # the plain form `python bench.py --gpus N`: start the N ranks here, before any GPU
+        # call in this process (counting devices does not initialise HIP)
+        n_dev = launch.visible_gpus()
+        if 0 < n_dev < a.gpus and os.environ.get("DLI_SAME_DEVICE", "0") != "1":
+            sys.exit(f"bench.py: --gpus {a.gpus} but only {n_dev} GPU(s) visible "
+                     "(DLI_SAME_DEVICE=1 rehearses every rank on cuda:0)")
+        sys.exit(launch.spawn_self(a.gpus))
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     if world > 1 or a.gpus > 1:
@@ -204,7 +225,16 @@ def main():
                    "seq_len": a.max_length, "prompt_len": a.prompt_len,
                    "parallelism": res["parallelism"],
                    "sampling": "T=0.8 top_k=50 top_p=0.95"},
+        "data_plane": res.get("data_plane", "none"),
+        "ranks": world,
+        "launcher": os.environ.get("DLI_LAUNCHER", "torchrun" if world > 1 else "none"),
     }
+    infos = res.get("ranks_info")
+    if infos:
+        from distributed_llm_inferencing_amd.parallel.transport import distinct_gpus
+        line["rank_devices"] = [{k: i[k] for k in ("rank", "device", "pci", "host")
+                                 if k in i} for i in infos]
+        line["distinct_gpus"] = distinct_gpus(infos)
     lfl = _like_for_like_value()
     if lfl and a.model == "llama3-8b":
         # like-for-like batch: HF generate over 512 prompts per call on the same GPU

@@ -7,8 +7,9 @@ launcher for an 8-GPU MI355X box.
     serve-master    [--port 8000]                       Flask master (dashboard + API)
     serve-worker    [--port 5000] [--gpu i]             one worker bound to one GPU (or CPU)
     serve-node      --gpus N [--base-port 5000] [--master URL]
-                    one worker process per GPU (HIP_VISIBLE_DEVICES=i, port base+i), each
-                    registered with the master as a node
+                    one worker process per GPU (--gpu i, port base+i; every GPU stays
+                    visible to every worker so a ring formed over them by join-pipeline
+                    can map its peers' memory), each registered with the master as a node
     serve-pipeline  --model M [--port 5000] [--shard-dir D]
                     (under torchrun) N-rank layer-sharded pipeline; rank 0 serves the worker
                     API and reports the stages as shards; --shard-dir serves the files
@@ -34,6 +35,23 @@ import sys
 import time
 
 
+def node_commands(gpus: int, base_port: int = 5000, preload: str = ""):
+    """[(argv, env)] of serve-node's workers: worker i selects GPU i with ``--gpu i`` and
+    sees every GPU of the node. (Masking each worker to its own GPU with a visibility
+    variable would leave a join-pipeline ring over them unable to open its peers' memory:
+    the IPC mailboxes and RCCL's P2P path both need the peer device visible.)"""
+    out = []
+    for i in range(gpus):
+        env = {k: v for k, v in os.environ.items()
+               if k not in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES",
+                            "CUDA_VISIBLE_DEVICES")}
+        env.update(USE_GPU="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+        cmd = [sys.executable, "-m", "distributed_llm_inferencing_amd.worker.server",
+               "--port", str(base_port + i), "--gpu", str(i), "--preload", preload]
+        out.append((cmd, env))
+    return out
+
+
 def _serve_node(argv):
     import argparse
 
@@ -45,11 +63,7 @@ def _serve_node(argv):
     ap.add_argument("--preload", default="")
     a = ap.parse_args(argv)
     procs = []
-    for i in range(a.gpus):
-        env = dict(os.environ, HIP_VISIBLE_DEVICES=str(i), USE_GPU="1",
-                   HSA_ENABLE_IPC_MODE_LEGACY="0")
-        cmd = [sys.executable, "-m", "distributed_llm_inferencing_amd.worker.server",
-               "--port", str(a.base_port + i), "--gpu", "0", "--preload", a.preload]
+    for i, (cmd, env) in enumerate(node_commands(a.gpus, a.base_port, a.preload)):
         procs.append(subprocess.Popen(cmd, env=env))
     if a.master:
         for i in range(a.gpus):
@@ -109,6 +123,9 @@ def _serve_pipeline(argv):
     s.use_gpu = torch.cuda.is_available()
     st = WorkerState(s, dev)
     st.pipeline_model = a.model
+    ch = eng.channel
+    st.data_plane = {"kind": "pipeline", "plane": ch.data_plane, "control": ch.ctrl_kind,
+                     "fallback": ch.fallback, "ranks": ch.world}
     st.pipeline_service = PipelineService(eng, name=a.model)
     st.tokenizers[a.model] = eng.head.tok
     st.pipeline_shards = [] if a.no_shard_report else [
@@ -198,10 +215,13 @@ def _join_pipeline(argv):
             return 1
     t0 = time.time()
     while time.time() - t0 < a.timeout:
-        states = [requests.get(f"{u}/health", headers=hdr, timeout=10).json()
-                  .get("pipeline", {}).get("state") for u in nodes]
+        pipes = [requests.get(f"{u}/health", headers=hdr, timeout=10).json()
+                 .get("pipeline", {}) for u in nodes]
+        states = [p.get("state") for p in pipes]
         if all(s == "serving" for s in states):
-            print(json.dumps({"model": a.model, "stages": len(nodes), "head": nodes[0]}))
+            print(json.dumps({"model": a.model, "stages": len(nodes), "head": nodes[0],
+                              "data_plane": [p.get("data_plane") for p in pipes],
+                              "fallback": [p.get("data_plane_fallback") for p in pipes]}))
             return 0
         if "failed" in states:
             print(f"join failed: {states}")

@@ -27,6 +27,7 @@ next step is planned against its in-flight one before the lockstep exchange).
 """
 from __future__ import annotations
 
+import logging
 import os
 import time
 from typing import List, Optional
@@ -43,6 +44,7 @@ from ..models import weights as W
 
 # a step whose largest per-rank token count exceeds this exchanges exact counts per layer
 EP_BOUND_MAX_TOKENS = int(os.environ.get("DLI_EP_BOUND_MAX_TOKENS", "1024"))
+_log = logging.getLogger("dli.expert")
 
 
 class ExpertParallelMoE:
@@ -277,6 +279,7 @@ class ExpertParallelEngine:
         # host and they pass their self-test, else the torch all-to-all (resolve_comm)
         requested = comm or os.environ.get("DLI_EP_COMM", "auto")
         self.comm = resolve_comm(requested, dev, self.ctrl_group)
+        self.fallback: Optional[str] = None
         self.moe = ExpertParallelMoE(cfg.num_experts, cfg.top_k_experts)
         er = self.moe.expert_range()
         if model_dir is not None:
@@ -301,6 +304,13 @@ class ExpertParallelEngine:
                     raise RuntimeError("IPC expert data plane failed its self-test")
                 self.moe.close()
                 self.comm, ipc = "torch", False
+                self.fallback = "ipc self-test failed"
+                _log.warning("expert-parallel rank %d: IPC mailboxes failed their self-test; "
+                             "the all-to-all falls back to torch.distributed (%s)",
+                             self.rank, dist.get_backend())
+        from .transport import data_plane_name
+        self.data_plane = data_plane_name(
+            self.comm, dist.get_backend() == "nccl" or (ipc and dev.type == "cuda"))
         # with the mailbox data plane the decode forward is captured (graphs); the torch
         # data plane needs host-side split sizes per layer and runs eagerly
         graphs = ipc and dev.type == "cuda" and os.environ.get("DLI_NO_GRAPHS", "0") != "1"
@@ -505,6 +515,8 @@ def bench_expert_parallel(args, world, rank, make_prompts):
     lat_t = torch.tensor(lats, dtype=torch.float64, device=cdev)
     gathered = [torch.zeros_like(lat_t) for _ in range(world)]
     dist.all_gather(gathered, lat_t)
+    from .transport import gather_rank_info
+    infos = gather_rank_info(dev)
     dist.barrier()
     eng.moe.close()
     dist.destroy_process_group()
@@ -512,4 +524,5 @@ def bench_expert_parallel(args, world, rank, make_prompts):
         return None
     return {"tokens": int(tt.item()), "seconds": float(dt.item()),
             "latencies": torch.cat(gathered).tolist(), "global_batch": args.batch * world,
-            "parallelism": f"dp{world}-ep{world}" + ("-ipc" if eng.comm == "ipc" else "")}
+            "parallelism": f"dp{world}-ep{world}", "data_plane": eng.data_plane,
+            "ranks_info": infos}

@@ -323,7 +323,9 @@ class PipelineHead:
         ph = self.phase_s
         pc = time.perf_counter
         tt = time.thread_time       # this thread's CPU time: host cost without preemption
-        check = ch.check if N > 1 and getattr(ch, "ipc", None) is not None else None
+        # every plane: a dead peer seen by the watchdog (any plane) or the device mailboxes'
+        # error word (ipc) fails the session at the next tick boundary
+        check = getattr(ch, "check", None) if N > 1 else None
         while True:
             t0 = pc()
             c0 = tt()
@@ -584,9 +586,12 @@ def serve_session(stage: StageWorker, channel, bufs: Optional[_StageBuffers] = N
     prev_out = None                 # my layer output of tick k-1 (hidden / tokens / final hidden)
     prev_vp = False
     my_cand = None                  # my candidates of microbatch k-1-N
+    chk = getattr(channel, "check", None)
     while True:
         if faults.active():
             faults.check("pipeline.stage", tick=k)
+        if chk is not None:
+            chk()                            # a dead peer fails the session here
         meta = None
         if k >= r:
             h, p = channel.recv_ctrl()
@@ -966,6 +971,8 @@ def bench_pipeline(args, world: int, rank: int, make_prompts):
     dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
                       device=device if dist.get_backend() == "nccl" else "cpu")
     dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    from .transport import gather_rank_info
+    infos = gather_rank_info(device)
     eng.shutdown() if rank == 0 else eng.serve()
     dist.barrier()
     eng.channel.close()
@@ -978,7 +985,8 @@ def bench_pipeline(args, world: int, rank: int, make_prompts):
     snap["head_host_ms_per_decode_tick"] = round(1e3 * hd[0] / max(1, hd[1]), 4)
     snap["control_plane"] = eng.channel.ctrl_kind
     return {"tokens": toks, "seconds": float(dt.item()), "latencies": lats,
-            "global_batch": per_wave, "parallelism": f"pp{world}", "engine": snap}
+            "global_batch": per_wave, "parallelism": f"pp{world}", "engine": snap,
+            "data_plane": eng.channel.data_plane, "ranks_info": infos}
 
 
 def run_one_session(eng: DistributedPipelineEngine):

@@ -143,10 +143,14 @@ def bench_tensor_parallel(args, world, rank, make_prompts):
     cdev = dev if dist.get_backend() == "nccl" else torch.device("cpu")
     dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=cdev)
     dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    from .transport import gather_rank_info
+    infos = gather_rank_info(dev)
     dist.barrier()
+    plane = "torch-rccl" if dist.get_backend() == "nccl" else "torch-gloo"
     dist.destroy_process_group()
     if rank != 0:
         return None
     # every rank produced the same tokens for the same requests: count them once
     return {"tokens": toks, "seconds": float(dt.item()), "latencies": lats,
-            "global_batch": batch, "parallelism": f"tp{world}"}
+            "global_batch": batch, "parallelism": f"tp{world}", "data_plane": plane,
+            "ranks_info": infos}

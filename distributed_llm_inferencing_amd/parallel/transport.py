@@ -28,6 +28,7 @@ the step, cols = hidden size), so the data plane carries no headers at all.
 from __future__ import annotations
 
 import itertools
+import logging
 import os
 import socket
 import threading
@@ -46,6 +47,18 @@ from ..utils.tracing import trace_range
 H_TICK = 12
 _HDR_BYTES = HEADER_LEN * 8
 _ring_ids = itertools.count()
+_log = logging.getLogger("dli.transport")
+
+
+def data_plane_name(comm: str, nccl: bool) -> str:
+    """The resolved data plane as records report it: ``ipc`` (device mailboxes; on a CPU
+    rank their shared-memory host model, ``ipc-host``), ``rccl`` (comm.cpp's own
+    communicator), ``torch-rccl`` / ``torch-gloo`` (torch.distributed point-to-point)."""
+    if comm == "ipc":
+        return "ipc" if nccl else "ipc-host"
+    if comm == "rccl":
+        return "rccl"
+    return "torch-rccl" if nccl else "torch-gloo"
 
 
 def ctrl_slot_bytes(max_seqs: int, max_tokens: int, table_width: int) -> int:
@@ -99,6 +112,7 @@ class PipeChannel:
         self._hdr_rx = torch.empty(HEADER_LEN, dtype=torch.int64)    # gloo fallback
         self._pay_rx = torch.empty(self.ctrl_bytes // 4, dtype=torch.int32)
         self.exchanges = 0
+        self.fallback: Optional[str] = None      # why the requested plane was not used
         if self.world > 1:
             self._init_ctrl(ctrl or os.environ.get("DLI_PP_CTRL", "auto"))
             # every rank joins one grouped ring exchange up front, so whatever point-to-point
@@ -133,6 +147,11 @@ class PipeChannel:
                 self.comm = "torch"
                 self.nccl = dist.get_backend() == "nccl"
                 self.data_device = self.device if self.nccl else torch.device("cpu")
+                self.fallback = "ipc self-test failed"
+                _log.warning("pipeline rank %d: IPC mailboxes failed their self-test; the "
+                             "data plane falls back to torch.distributed (%s)", self.rank,
+                             dist.get_backend())
+        self.data_plane = data_plane_name(self.comm, self.nccl) if self.world > 1 else "none"
 
     # ------------------------------------------------------------------ setup
     def _init_rccl(self) -> None:
@@ -506,6 +525,41 @@ def _is_gpu_ep(ep) -> bool:
     return type(ep).__name__ == "IpcEndpoint"
 
 
+def rank_info(device: torch.device) -> dict:
+    """Where this rank runs: host, process, device ordinal, the physical GPU behind it
+    (PCI bus id when the runtime reports one) and the visibility mask it was started with.
+    A multi-rank record carries every rank's entry, so a reader can tell N GPUs from N
+    ranks sharing one."""
+    dev = torch.device(device)
+    info = {"rank": dist.get_rank() if dist.is_initialized() else 0,
+            "host": socket.gethostname(), "pid": os.getpid(), "device": str(dev)}
+    if dev.type == "cuda":
+        idx = dev.index if dev.index is not None else torch.cuda.current_device()
+        p = torch.cuda.get_device_properties(idx)
+        bus = [getattr(p, k, None) for k in ("pci_domain_id", "pci_bus_id", "pci_device_id")]
+        if all(b is not None for b in bus):
+            info["pci"] = "%04x:%02x:%02x" % tuple(int(b) for b in bus)
+        info["name"] = p.name
+        for k in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+            if os.environ.get(k):
+                info[k] = os.environ[k]
+    return info
+
+
+def gather_rank_info(device: torch.device, group=None) -> List[dict]:
+    """``rank_info`` of every rank of ``group`` (an object all-gather: every rank calls)."""
+    out = [None] * dist.get_world_size(group)
+    dist.all_gather_object(out, rank_info(device), group=group)
+    return out
+
+
+def distinct_gpus(infos: Sequence[dict]) -> int:
+    """Physical GPUs behind a list of ``rank_info`` entries (by PCI id, else by ordinal)."""
+    keys = {(i.get("host"), i.get("pci") or (i.get("HIP_VISIBLE_DEVICES"), i.get("device")))
+            for i in infos if str(i.get("device", "")).startswith("cuda")}
+    return len(keys)
+
+
 def init_distributed(backend: Optional[str] = None, device: Optional[torch.device] = None,
                      init_method: Optional[str] = None, world_size: Optional[int] = None,
                      rank: Optional[int] = None):
@@ -532,8 +586,12 @@ def init_distributed(backend: Optional[str] = None, device: Optional[torch.devic
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29511")
     if backend is None:
+        # ranks sharing one GPU (DLI_SAME_DEVICE=1 rehearsals) cannot form an RCCL
+        # communicator (one rank per device): their process group is gloo, the data plane
+        # is still the device mailboxes
+        same = os.environ.get("DLI_SAME_DEVICE", "0") == "1"
         backend = os.environ.get("DLI_DIST_BACKEND") or (
-            "nccl" if torch.cuda.is_available() else "gloo")
+            "nccl" if torch.cuda.is_available() and not same else "gloo")
     kw = {"timeout": timedelta(seconds=float(os.environ.get("DLI_PP_TIMEOUT_S", "600")))}
     if backend == "nccl" and device is not None:
         kw["device_id"] = device

@@ -482,6 +482,10 @@ class RcclComm:
             raise RuntimeError(f"ncclCommInitRank failed: {L.dli_comm_error_string(r).decode()}")
         self._h = h.value
         self.world, self.rank = world, rank
+        # the tick thread enqueues exchanges while the pipeline watchdog may abort the
+        # communicator: every use of the handle holds this lock, and an aborted handle is
+        # never dereferenced again (exchange raises instead)
+        self._lock = threading.Lock()
 
     @staticmethod
     def available() -> bool:
@@ -509,26 +513,37 @@ class RcclComm:
             return n, ptrs, nbytes, peers
         ns, sp, sb, spe = pack(sends)
         nr, rp, rb, rpe = pack(recvs)
-        r = lib().dli_comm_exchange(self._h, ctypes.c_void_p(stream), ns, sp, sb, spe, nr, rp,
-                                    rb, rpe)
+        with self._lock:
+            if self._h is None:
+                raise RuntimeError("RCCL exchange on an aborted / closed communicator")
+            r = lib().dli_comm_exchange(self._h, ctypes.c_void_p(stream), ns, sp, sb, spe, nr,
+                                        rp, rb, rpe)
         if r != 0:
             raise RuntimeError(f"RCCL exchange failed: {lib().dli_comm_error_string(r).decode()}")
 
     def async_error(self) -> int:
         """0 while healthy, else -(ncclResult_t) of the communicator's asynchronous error."""
-        return int(lib().dli_comm_async_error(self._h)) if self._h is not None else 0
+        if not self._lock.acquire(timeout=0.05):
+            return 0                    # an exchange is being enqueued: ask again next period
+        try:
+            return int(lib().dli_comm_async_error(self._h)) if self._h is not None else 0
+        finally:
+            self._lock.release()
 
     def abort(self) -> None:
         """ncclCommAbort: release the communicator without waiting for peers (a dead
-        neighbour); queued RCCL kernels return so the stream drains."""
-        h, self._h = self._h, None
-        if h is not None:
-            lib().dli_comm_abort(h)
+        neighbour); queued RCCL kernels return so the stream drains. Waits for an exchange
+        being enqueued on another thread to finish first (never frees a handle in use)."""
+        with self._lock:
+            h, self._h = self._h, None
+            if h is not None:
+                lib().dli_comm_abort(h)
 
     def close(self) -> None:
-        if self._h is not None:
-            lib().dli_comm_destroy(self._h)
-            self._h = None
+        with self._lock:
+            h, self._h = self._h, None
+            if h is not None:
+                lib().dli_comm_destroy(h)
 
     def __del__(self):
         try:

@@ -94,6 +94,12 @@ class WorkerState:
         self.pipeline: Optional[dict] = None            # ring this worker joined via /load_shard
         self._pipe_engine = None
         self.lock = threading.RLock()
+        # set while no ring teardown is running: a teardown drains a GPU stream and destroys
+        # the process group outside the lock, and a re-forming join must not rendezvous (or
+        # be torn down) under it
+        self._teardown_idle = threading.Event()
+        self._teardown_idle.set()
+        self.data_plane: Optional[dict] = None          # resolved plane of a multi-rank engine
         os.makedirs(settings.model_cache_dir, exist_ok=True)
 
     # ------------------------------------------------------------------ models
@@ -177,16 +183,25 @@ class WorkerState:
             raise ValueError("pipeline spec needs init_method and world_size >= 2")
         if not 0 <= shard_id < world:
             raise ValueError(f"shard {shard_id} outside a {world}-stage pipeline")
-        with self.lock:
-            if self.pipeline is not None and self.pipeline["state"] in ("joining", "serving"):
-                if (self.pipeline["model_name"], self.pipeline["rank"]) == (name, shard_id):
-                    return False
-                raise ValueError(f"this worker already serves stage {self.pipeline['rank']} "
-                                 f"of {self.pipeline['model_name']}")
-            if self.pipeline is not None:           # failed / stopped: re-form from scratch
-                self._clear_pipeline()
-            self.pipeline = {"model_name": name, "rank": shard_id, "world_size": world,
-                             "init_method": init_method, "state": "joining", "error": None}
+        while True:
+            if not self._teardown_idle.wait(timeout=120.0):
+                raise RuntimeError("the previous ring is still tearing down; retry later")
+            with self.lock:
+                if not self._teardown_idle.is_set():
+                    continue                        # a teardown started meanwhile
+                if (self.pipeline is not None
+                        and self.pipeline["state"] in ("joining", "serving")):
+                    if (self.pipeline["model_name"], self.pipeline["rank"]) == (name, shard_id):
+                        return False
+                    raise ValueError(f"this worker already serves stage "
+                                     f"{self.pipeline['rank']} of "
+                                     f"{self.pipeline['model_name']}")
+                if self.pipeline is not None:       # failed / stopped: re-form from scratch
+                    self._clear_pipeline()
+                self.pipeline = {"model_name": name, "rank": shard_id, "world_size": world,
+                                 "init_method": init_method, "state": "joining",
+                                 "error": None}
+                break
         shard_dir = os.path.dirname(path.rstrip("/"))
         threading.Thread(target=self._join, args=(name, shard_id, world, init_method,
                                                   shard_dir), daemon=True,
@@ -212,6 +227,14 @@ class WorkerState:
                                             dtype=_shard_dtype(shard_dir, rank))
             eng.warmup()
             self._pipe_engine = eng
+            ch = eng.channel
+            rec["data_plane"] = ch.data_plane
+            rec["control_plane"] = ch.ctrl_kind
+            if ch.fallback:
+                rec["data_plane_fallback"] = ch.fallback
+            self.data_plane = {"kind": "pipeline", "plane": ch.data_plane,
+                               "control": ch.ctrl_kind, "fallback": ch.fallback,
+                               "ranks": ch.world}
             if rank == 0:
                 with self.lock:
                     self.tokenizers[name] = eng.head.tok
@@ -236,14 +259,21 @@ class WorkerState:
             rec["state"] = "stopped"
         except BaseException as e:  # noqa: BLE001 — reported by /health
             log.error("pipeline join (%s stage %d/%d) failed: %s", name, rank, world, e)
-            rec["state"], rec["error"] = "failed", str(e)
-            # a retry with a new spec must rendezvous afresh, not reuse this group
-            eng = eng or self._pipe_engine
-            self._pipe_engine = None
+            # a retry with a new spec must rendezvous afresh, not reuse this group: the
+            # state reads "failed" only once the old group is gone
+            with self.lock:
+                eng = eng or self._pipe_engine
+                self._pipe_engine = None
+                self._teardown_idle.clear()
+                rec["state"], rec["error"] = "tearing_down", str(e)
             try:
                 self._abort_ring(eng)
             except Exception as e2:  # noqa: BLE001
                 log.warning("pipeline teardown after a failed join: %s", e2)
+            finally:
+                with self.lock:
+                    rec["state"] = "failed"
+                    self._teardown_idle.set()
 
     def _abort_ring(self, eng) -> None:
         """Tear down a broken ring's transports + process group without a goodbye: the data
@@ -280,11 +310,21 @@ class WorkerState:
         log.error("pipeline %s failed: %s", getattr(self, "pipeline_model", None), err)
         with self.lock:
             eng, self._pipe_engine = self._pipe_engine, None
-            if self.pipeline is not None:
-                self.pipeline["state"], self.pipeline["error"] = "failed", str(err)
-        self._abort_ring(eng)
-        if self.device.type == "cuda":
-            torch.cuda.empty_cache()
+            rec = self.pipeline
+            self._teardown_idle.clear()
+            if rec is not None:
+                rec["state"], rec["error"] = "tearing_down", str(err)
+        try:
+            self._abort_ring(eng)
+            if self.device.type == "cuda":
+                torch.cuda.empty_cache()
+        finally:
+            # "failed" (re-formable) only after the old group is destroyed: a join that
+            # raced this teardown waits on _teardown_idle instead of rendezvousing under it
+            with self.lock:
+                if rec is not None:
+                    rec["state"] = "failed"
+                self._teardown_idle.set()
 
     def _clear_pipeline(self) -> None:
         """Forget a failed / stopped ring before joining a new one."""
@@ -449,6 +489,8 @@ def create_worker_app(settings: Optional[Settings] = None, device: Optional[str]
             # balances (the reference's ModelShard rows are unique per (model, shard))
             shard_info += getattr(st, "pipeline_shards", None) or []
         extra = {"pipeline": st.pipeline} if st.pipeline is not None else {}
+        if st.data_plane is not None:
+            extra["data_plane"] = st.data_plane
         return jsonify({"status": "healthy", "resources": st.resources(), **extra,
                         "loaded_models": list(st.services.keys()),
                         "loaded_tokenizers": list(st.tokenizers.keys()),
@@ -597,7 +639,10 @@ def create_worker_app(settings: Optional[Settings] = None, device: Optional[str]
         out = {name: svc.stats() for name, svc in st.services.items()}
         if getattr(st, "pipeline_service", None) is not None:
             out[st.pipeline_model] = st.pipeline_service.stats()
-        return jsonify({"engines": out, "resources": st.resources()})
+        body = {"engines": out, "resources": st.resources()}
+        if st.data_plane is not None:
+            body["data_plane"] = st.data_plane
+        return jsonify(body)
 
     return app
 
@@ -621,6 +666,10 @@ def main(argv=None):
     if a.gpu is not None:
         s.use_gpu = True
         dev = f"cuda:{a.gpu}"
+        if torch.cuda.is_available():
+            # every GPU of the node is visible (serve-node): make this worker's GPU the
+            # current one, so nothing lands on device 0 by default
+            torch.cuda.set_device(a.gpu)
     kw = {"max_batch": a.max_batch} if a.max_batch else None
     app = create_worker_app(s, dev, kw)
     for m in [m for m in a.preload.split(",") if m]:

@@ -71,3 +71,31 @@ def test_bench_torchrun_two_ranks(mode, model, par, gb):
                 "--model", model, "--mode", mode, *COMMON])
     _check(rec, 2, 1, 1, par)
     assert rec["config"]["global_batch"] == gb
+
+
+def test_bench_spawns_its_own_ranks():
+    """The driver's plain form ``python bench.py --gpus N`` (no torchrun): bench.py starts
+    the N ranks itself and rank 0's line names the data plane and every rank's device."""
+    rec = _run([sys.executable, "bench.py", "--gpus", "2", "--model", "llama-tiny",
+                "--mode", "pp", *COMMON])
+    _check(rec, 2, 1, 1, "pp2")
+    assert rec["config"]["global_batch"] == 12
+    assert rec["launcher"] == "spawn" and rec["ranks"] == 2
+    assert rec["data_plane"] in ("torch-gloo", "ipc-host")
+    assert [d["rank"] for d in rec["rank_devices"]] == [0, 1]
+
+
+def test_spawn_failure_ends_the_job():
+    """One rank failing stops the others and the parent returns its exit code (no hang on
+    a peer that waits forever for the dead rank)."""
+    import time
+    from distributed_llm_inferencing_amd import launch
+    code = ("import os, sys, time\n"
+            "r = int(os.environ['RANK'])\n"
+            "assert os.environ['MASTER_ADDR'] == '127.0.0.1' and os.environ['WORLD_SIZE'] == '3'\n"
+            "sys.exit(7) if r == 1 else time.sleep(120)\n")
+    t0 = time.monotonic()
+    rc = launch.spawn([sys.executable, "-c", code], 3)
+    assert rc == 7
+    assert time.monotonic() - t0 < 60
+
