@@ -18,6 +18,14 @@ launcher for an 8-GPU MI355X box.
                     K data-parallel replicas, each a pipeline of gpus/K stages (SURVEY.md
                     §2.5 "DP replicas"); every replica head registers as a node and the
                     master's dispatcher load-balances across them (least in flight)
+    serve-expert    --model mixtral-8x7b --gpus N [--base-port 5000] [--master URL]
+                    expert-parallel deployment (BASELINE.json config 5): N ranks, one per
+                    GPU, each an HTTP worker on port base+rank holding experts
+                    [r E/N, (r+1) E/N) and all attention weights; every rank registers
+                    as a node and reports its expert shard, the master balances requests
+                    across them, and the ranks' MoE layers exchange rows every step
+                    (device mailboxes on one node). Spawns its ranks itself, or runs one
+                    rank under torchrun
     shard-model     --model_name M --num_shards N [--output_dir D] [--policy even|hbm|balanced]
     join-pipeline   --model M --shard-dir D --nodes URL0,URL1,... [--rendezvous tcp://H:P]
                     assign shard i of an export to node i over the worker API (/load_shard
@@ -138,6 +146,87 @@ def _serve_pipeline(argv):
     app.run(host="0.0.0.0", port=a.port, threaded=True)
 
 
+def _register_nodes(master: str, ports, prefix: str, timeout_s: float = 1800.0,
+                    alive=lambda: True) -> None:
+    """Add each worker (127.0.0.1:port) to the master once it answers (/api/nodes/add/
+    probes its /health first, as the reference's add_node does)."""
+    import requests
+    t0 = time.time()
+    for i, port in enumerate(ports):
+        while time.time() - t0 < timeout_s and alive():
+            try:
+                r = requests.post(f"{master}/api/nodes/add/",
+                                  data={"hostname": f"{prefix}{i}", "ip_address": "127.0.0.1",
+                                        "port": port}, timeout=10)
+                if r.status_code == 200:
+                    break
+            except requests.RequestException:
+                pass
+            time.sleep(1)
+
+
+def _serve_expert(argv):
+    import argparse
+    ap = argparse.ArgumentParser("dli serve-expert")
+    ap.add_argument("--model", default="mixtral-8x7b")
+    ap.add_argument("--gpus", type=int, default=8)
+    ap.add_argument("--base-port", type=int, default=5000)
+    ap.add_argument("--master", default=None)
+    ap.add_argument("--max-batch", type=int, default=256)
+    ap.add_argument("--max-model-len", type=int, default=2048)
+    ap.add_argument("--model-dir", default=None,
+                    help="exported weights (shard-model output or a HF directory): each rank "
+                         "reads all attention tensors and only its own experts' rows")
+    a = ap.parse_args(argv)
+    from . import launch
+    if not launch.under_launcher():
+        import threading
+        procs = launch.start([sys.executable, "-m", "distributed_llm_inferencing_amd.cli",
+                              "serve-expert", *argv], a.gpus)
+        if a.master:
+            threading.Thread(target=_register_nodes, daemon=True, args=(
+                a.master, [a.base_port + r for r in range(a.gpus)], "ep",
+                1800.0, lambda: all(p.poll() is None for p in procs))).start()
+        return launch.wait(procs)
+    return _serve_expert_rank(a)
+
+
+def _serve_expert_rank(a):
+    """One EP rank: engine + lockstep service + the worker HTTP API on base_port + rank."""
+    import logging
+
+    import torch
+    from .config import get_settings
+    from .parallel.expert import ExpertParallelEngine
+    from .worker.server import WorkerState, create_worker_app
+    from .worker.service import ExpertService
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    if os.environ.get("DLI_SAME_DEVICE", "0") == "1":
+        local = 0
+    cuda = torch.cuda.is_available() and os.environ.get("USE_GPU", "1") != "0"
+    if cuda:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local) if cuda else torch.device("cpu")
+    kw = {} if cuda else {"num_blocks": 512, "dtype": torch.float32}
+    eng = ExpertParallelEngine(a.model, dev, max_batch=a.max_batch,
+                               max_model_len=a.max_model_len, model_dir=a.model_dir, **kw)
+    eng.warmup()
+    logging.basicConfig(level=logging.INFO)
+    s = get_settings()
+    s.use_gpu = cuda
+    st = WorkerState(s, str(dev))
+    st.pipeline_model = a.model
+    st.pipeline_service = ExpertService(eng, name=a.model.replace("/", "_"))
+    st.tokenizers[a.model] = eng.engine.tokenizer
+    st.pipeline_shards = [eng.shard_record(a.model)]
+    st.data_plane = {"kind": "expert", "plane": eng.data_plane, "fallback": eng.fallback,
+                     "ranks": eng.world, "rank": eng.rank}
+    app = create_worker_app(s, state=st)
+    app.run(host="0.0.0.0", port=a.base_port + eng.rank, threaded=True)
+    return 0
+
+
 def cluster_plan(gpus: int, dp: int, base_port: int = 5000, rdzv_base: int = 29600):
     """[(replica, visible_devices, http_port, rendezvous_port)] for K pipelines of gpus/K."""
     if dp < 1 or gpus % dp:
@@ -224,7 +313,7 @@ def _join_pipeline(argv):
                               "fallback": [p.get("data_plane_fallback") for p in pipes]}))
             return 0
         if "failed" in states:
-            print(f"join failed: {states}")
+            print(f"join failed: {states}: {[p.get('error') for p in pipes]}")
             return 1
         time.sleep(1)
     print(f"join timed out: {states}")
@@ -249,6 +338,8 @@ def main(argv=None):
         return _serve_pipeline(rest)
     if cmd == "serve-cluster":
         return _serve_cluster(rest)
+    if cmd == "serve-expert":
+        return _serve_expert(rest)
     if cmd == "shard-model":
         from .shard.writer import main as m
         return m(rest)

@@ -192,8 +192,10 @@ class Dispatcher:
                     return False, None
                 with self._lock:
                     self._loaded.add((node["id"], model))
+            # seed = this master's request id: the sampled tokens of a request do not depend
+            # on which node (or which retry) serves it
             payload = {"model_name": model, "prompt": prompt, "max_length": self.max_length,
-                       "timeout": WORKER_TIMEOUT}
+                       "timeout": WORKER_TIMEOUT, "seed": int(rid)}
             if shard_ids is not None:
                 payload["shard_ids"] = sorted(shard_ids)
             r = self._post(node, "/inference", payload, HTTP_INFER_TIMEOUT)
@@ -422,8 +424,10 @@ class AsyncDispatcher(Dispatcher):
                     return False, None
                 with self._lock:
                     self._loaded.add((node["id"], model))
+            # seed = this master's request id: the sampled tokens of a request do not depend
+            # on which node (or which retry) serves it
             payload = {"model_name": model, "prompt": prompt, "max_length": self.max_length,
-                       "timeout": WORKER_TIMEOUT}
+                       "timeout": WORKER_TIMEOUT, "seed": int(rid)}
             if shard_ids is not None:
                 payload["shard_ids"] = sorted(shard_ids)
             st, text = await self._post_async(node, "/inference", payload, HTTP_INFER_TIMEOUT)

@@ -41,8 +41,12 @@ def auto_num_blocks(cfg: ModelConfig, num_layers: int, block_size: int, device,
         if reserve_bytes is None:
             reserve_bytes = max(8 << 30, int(0.03 * total))
         if os.environ.get("DLI_SAME_DEVICE", "0") == "1":
-            fraction /= max(1, int(os.environ.get("LOCAL_WORLD_SIZE",
-                                                  os.environ.get("WORLD_SIZE", "1"))))
+            ranks = os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE"))
+            if ranks is None:
+                # a worker that joined a ring by init_method (no launcher environment)
+                import torch.distributed as dist
+                ranks = dist.get_world_size() if dist.is_initialized() else 1
+            fraction /= max(1, int(ranks))
         budget = max(0, int(free * fraction) - reserve_bytes)
     else:
         budget = 256 << 20                  # CPU (tests / the gpt2 plumbing config)

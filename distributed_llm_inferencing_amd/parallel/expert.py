@@ -332,6 +332,10 @@ class ExpertParallelEngine:
         self._full_prefill = self.engine.scheduler.max_prefill_tokens
         self._peers_decoding = False
         self.capped_steps = 0
+        # serving: a rank asks the group to stop (ExpertService.close); every rank learns it
+        # from the lockstep exchange and leaves the loop once no rank has work
+        self.stop_requested = False
+        self.stopping = False
 
     def warmup(self):
         """Capture the decode graphs (every rank, same bucket order: the warm-up forwards
@@ -353,14 +357,20 @@ class ExpertParallelEngine:
             self.moe.static = False
 
     def _exchange(self, work: bool, tokens: int) -> List[List[int]]:
-        """The per-step lockstep exchange: (has work, tokens of the next forward) of every
-        rank — the one host sync of a decode step."""
-        cdev = self.device if dist.get_backend() == "nccl" else torch.device("cpu")
-        mine = torch.tensor([1 if work else 0, tokens], dtype=torch.int64, device=cdev)
+        """The per-step lockstep exchange: (has work, tokens of the next forward, stop) of
+        every rank, host to host over the gloo control group. It never waits on a GPU: an
+        RCCL all-gather read back with ``.tolist()`` would drain this rank's stream (the
+        in-flight step included) before the next step could even be planned, defeating
+        lookahead; the routing itself stays on the device (mailbox headers)."""
+        mine = torch.tensor([1 if work else 0, tokens, 1 if self.stop_requested else 0],
+                            dtype=torch.int64)
         allv = [torch.empty_like(mine) for _ in range(self.world)]
-        dist.all_gather(allv, mine)
+        dist.all_gather(allv, mine, group=self.ctrl_group)
         self.lockstep_syncs += 1
-        return torch.stack(allv).tolist()
+        rows = torch.stack(allv).tolist()
+        if any(r[2] for r in rows):
+            self.stopping = True
+        return [r[:2] for r in rows]
 
     def _idle_forward(self):
         """Join every MoE exchange of one forward with zero local rows."""
@@ -421,6 +431,21 @@ class ExpertParallelEngine:
         rids = [self.engine.add_request(p, params) for p in prompts]
         done = {o.request_id: o for o in self.run_until_idle()}
         return [done[r] for r in rids]
+
+    def shard_record(self, model_name: str) -> dict:
+        """This rank as a worker shard row (``loaded_shards`` of /health): shard id = rank,
+        metadata = the experts it holds. Every rank serves whole requests (DP attention), so
+        the master balances across the shard holders by load."""
+        e0, e1 = self.moe.expert_range()
+        return {"model_name": model_name, "shard_id": self.rank, "path": f"ep{self.rank}",
+                "metadata": {"model_name": model_name, "shard_id": self.rank,
+                             "num_shards": self.world, "kind": "expert",
+                             "experts": [e0, e1], "num_experts": self.cfg.num_experts,
+                             "start_layer": 0, "end_layer": self.cfg.num_layers - 1,
+                             "total_layers": self.cfg.num_layers}}
+
+    def close(self) -> None:
+        self.moe.close()
 
 
 def _dir_config(model_dir: str, name: str):

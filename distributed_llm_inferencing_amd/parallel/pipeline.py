@@ -694,7 +694,8 @@ def build_stage(cfg: ModelConfig, rank: int, world: int, device, max_batch: int,
                 policy: str = "balanced", seed: int = 0, use_graphs=None,
                 num_blocks: Optional[int] = None, dtype=torch.bfloat16,
                 vocab_parallel: bool = False, microbatches: Optional[int] = None,
-                max_tokens: int = 0, shard_dir: Optional[str] = None):
+                max_tokens: int = 0, shard_dir: Optional[str] = None,
+                max_kv_tokens: int = 0):
     if shard_dir is not None:
         from ..shard.writer import stage_plan_from_metadata
         plans = [stage_plan_from_metadata(read_shard_dir(shard_dir, i, world)[1])
@@ -710,7 +711,8 @@ def build_stage(cfg: ModelConfig, rank: int, world: int, device, max_batch: int,
     if num_blocks is None:
         # this stage's layers' KV from its free HBM (288 GB per MI355X); every stage holds
         # the same block ids (the head's allocator), so all take the smallest pool
-        cap = _stage_capacity_blocks(cfg, plan, block_size, device, kv_fraction, cap_tokens=0)
+        cap = _stage_capacity_blocks(cfg, plan, block_size, device, kv_fraction,
+                                     cap_tokens=max_kv_tokens)
         t = torch.tensor([cap], dtype=torch.int64,
                          device=device if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MIN)     # block ids are global: same pool size
@@ -730,7 +732,7 @@ class DistributedPipelineEngine:
                  block_size: int = 16, policy: str = "balanced", seed: int = 0,
                  use_graphs=None, max_prefill_tokens: int = 16384, num_blocks=None,
                  dtype=torch.bfloat16, vocab_parallel: Optional[bool] = None,
-                 shard_dir: Optional[str] = None):
+                 shard_dir: Optional[str] = None, max_kv_tokens: int = 0):
         self.rank, self.world = init_distributed(device=torch.device(device)
                                                  if torch.device(device).type == "cuda" else None)
         if shard_dir is not None:
@@ -753,7 +755,7 @@ class DistributedPipelineEngine:
             self.cfg, self.rank, self.world, self.device, max_batch, max_model_len, block_size,
             policy=policy, seed=seed, use_graphs=use_graphs, num_blocks=num_blocks, dtype=dtype,
             vocab_parallel=self.vocab_parallel, microbatches=self.microbatches,
-            max_tokens=max_tokens, shard_dir=shard_dir)
+            max_tokens=max_tokens, shard_dir=shard_dir, max_kv_tokens=max_kv_tokens)
         esz = torch.empty(0, dtype=dtype).element_size()
         D = self.cfg.hidden_size
         # mailbox sizes of the IPC data plane: a whole step's hidden rows on r -> r + 1; the

@@ -224,7 +224,8 @@ class WorkerState:
             eng = DistributedPipelineEngine(name, self.device, max_batch=kw["max_batch"],
                                             max_model_len=kw["max_model_len"],
                                             num_blocks=kw["num_blocks"], shard_dir=shard_dir,
-                                            dtype=_shard_dtype(shard_dir, rank))
+                                            dtype=_shard_dtype(shard_dir, rank),
+                                            max_kv_tokens=kw.get("max_kv_tokens") or 0)
             eng.warmup()
             self._pipe_engine = eng
             ch = eng.channel
@@ -258,7 +259,7 @@ class WorkerState:
             dist.destroy_process_group()
             rec["state"] = "stopped"
         except BaseException as e:  # noqa: BLE001 — reported by /health
-            log.error("pipeline join (%s stage %d/%d) failed: %s", name, rank, world, e)
+            log.exception("pipeline join (%s stage %d/%d) failed: %s", name, rank, world, e)
             # a retry with a new spec must rendezvous afresh, not reuse this group: the
             # state reads "failed" only once the old group is gone
             with self.lock:

@@ -224,3 +224,100 @@ class PipelineService:
     def close(self):
         self._stop.set()
         self._t.join(5)
+
+
+class ExpertService:
+    """Same interface, backed by one rank of an ExpertParallelEngine (``cli serve-expert``):
+    every rank is a worker node of its own (DP attention, its own requests and KV) whose MoE
+    layers exchange rows with the other ranks every step. The ranks step in lockstep, so
+    this thread keeps stepping while ANY rank has work — an idle rank joins every exchange
+    with an empty forward — and all ranks idle together (one lockstep exchange every
+    ``idle_s``) when none has. ``close`` raises the stop bit of the exchange: every rank
+    leaves its loop once no rank has work. A failed exchange (a peer died) fails every
+    pending request and sets ``error`` (the worker answers 503, the master's dispatcher
+    retries on another node)."""
+
+    def __init__(self, ep_engine, name: str = "expert", idle_s: float = 0.002):
+        self.engine = ep_engine
+        self.name = name
+        self.idle_s = idle_s
+        self._inbox: "queue.Queue[tuple]" = queue.Queue()
+        self._futs = {}
+        self._ids = 0
+        self._lock = threading.Lock()
+        self.error: Optional[BaseException] = None
+        self.stopped = threading.Event()
+        self._t = threading.Thread(target=self._run, name=f"dli-ep-{name}", daemon=True)
+        self._t.start()
+
+    def submit(self, prompt, params=None) -> Future:
+        fut: Future = Future()
+        if self.error is not None or self.stopped.is_set():
+            fut.set_exception(PipelineFailed(f"expert group {self.name} is down: {self.error}"))
+            return fut
+        with self._lock:
+            self._ids += 1
+            rid = f"{self.name}-r{self.engine.rank}-{self._ids}"
+        self._inbox.put((rid, prompt, params, fut))
+        return fut
+
+    def generate(self, prompt, params=None, timeout=None):
+        return self.submit(prompt, params).result(timeout=timeout)
+
+    def _admit(self) -> None:
+        eng = self.engine.engine
+        while True:
+            try:
+                rid, prompt, params, fut = self._inbox.get_nowait()
+            except queue.Empty:
+                return
+            try:
+                eng.add_request(prompt, params, request_id=rid)
+                self._futs[rid] = fut
+            except Exception as e:  # noqa: BLE001
+                fut.set_exception(e)
+
+    def _fail_all(self, err: BaseException) -> None:
+        exc = PipelineFailed(f"expert group {self.name} failed: {err}")
+        for f in self._futs.values():
+            if not f.done():
+                f.set_exception(exc)
+        self._futs.clear()
+        while True:
+            try:
+                *_, fut = self._inbox.get_nowait()
+            except queue.Empty:
+                return
+            fut.set_exception(exc)
+
+    def _run(self):
+        ep = self.engine
+        try:
+            while True:
+                self._admit()
+                outs, more = ep.step()
+                for o in outs:
+                    f = self._futs.pop(o.request_id, None)
+                    if f is not None and not f.done():
+                        f.set_result(o)
+                if ep.stopping and not more:
+                    break
+                if not more:
+                    time.sleep(self.idle_s)     # every rank saw the same "no work"
+        except BaseException as e:  # noqa: BLE001 — a peer died or the data plane broke
+            self.error = e
+            self._fail_all(e)
+        finally:
+            self.stopped.set()
+
+    def stats(self) -> dict:
+        s = self.engine.engine.stats.snapshot()
+        s.update(queued=self._inbox.qsize(), in_flight=len(self._futs),
+                 lockstep_steps=self.engine.steps, graph_steps=self.engine.graph_steps,
+                 failed=None if self.error is None else str(self.error))
+        return s
+
+    def close(self, timeout: float = 30.0) -> None:
+        """Ask the whole group to stop (collective: every rank's service leaves its loop)."""
+        self.engine.stop_requested = True
+        self.stopped.wait(timeout)

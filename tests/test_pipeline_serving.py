@@ -279,6 +279,9 @@ def test_load_shard_joins_pipeline_ring(tmp_path):
         hs = [requests.get(f"{u}/health", timeout=5).json() for u in urls]
         states = [h["pipeline"]["state"] for h in hs]
         assert states == ["serving", "serving"], hs
+        # every stage reports the data plane its ring resolved (CPU ranks: gloo)
+        assert [h["pipeline"]["data_plane"] for h in hs] == ["torch-gloo"] * 2
+        assert all(h["data_plane"]["plane"] == "torch-gloo" for h in hs)
         assert sorted(s["shard_id"] for s in hs[0]["loaded_shards"]) == [0, 1]
         assert hs[1]["loaded_shards"] == []   # the master routes this model to stage 0
         body = {"model_name": "llama-tiny", "prompt": "pipeline join", "max_length": 24,
