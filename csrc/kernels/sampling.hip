@@ -123,8 +123,37 @@ __device__ uint32_t radix_kth(const uint32_t* keys, int n, uint32_t k, uint32_t*
   return prefix;
 }
 
+// Logits arrive as fp32 or as bf16 (u16: the LM head's output in the model dtype, as HF's
+// `lm_head(hidden).float()` produces them); every comparison runs on the exact fp32 value.
+__device__ __forceinline__ float ldv(const float* x, int i) { return x[i]; }
+__device__ __forceinline__ float ldv(const u16* x, int i) { return bf2f(x[i]); }
+
 // Visit every element of a row with 16-B loads, 4 loads in flight per thread (the sampler is
 // one workgroup per row, so memory-level parallelism per CU comes from ILP, not occupancy).
+template <typename F>
+__device__ __forceinline__ void row_scan(const u16* __restrict__ x, int V, F&& f) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  int done = 0;
+  if ((reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+    const int V8 = V >> 3;
+    const uint4* x8 = reinterpret_cast<const uint4*>(x);
+    auto eight = [&](const uint4 v, int base) {
+      f(__uint_as_float(v.x << 16), base);     f(__uint_as_float(v.x & 0xffff0000u), base + 1);
+      f(__uint_as_float(v.y << 16), base + 2); f(__uint_as_float(v.y & 0xffff0000u), base + 3);
+      f(__uint_as_float(v.z << 16), base + 4); f(__uint_as_float(v.z & 0xffff0000u), base + 5);
+      f(__uint_as_float(v.w << 16), base + 6); f(__uint_as_float(v.w & 0xffff0000u), base + 7);
+    };
+    int i = tid;
+    for (; i + 3 * nt < V8; i += 4 * nt) {
+      const uint4 a = x8[i], b = x8[i + nt], c = x8[i + 2 * nt], d = x8[i + 3 * nt];
+      eight(a, 8 * i); eight(b, 8 * (i + nt)); eight(c, 8 * (i + 2 * nt)); eight(d, 8 * (i + 3 * nt));
+    }
+    for (; i < V8; i += nt) eight(x8[i], 8 * i);
+    done = V8 * 8;
+  }
+  for (int j = done + tid; j < V; j += nt) f(bf2f(x[j]), j);
+}
+
 template <typename F>
 __device__ __forceinline__ void row_scan(const float* __restrict__ x, int V, F&& f) {
   const int tid = threadIdx.x, nt = blockDim.x;
@@ -171,9 +200,10 @@ __device__ __forceinline__ bool smp_split_ok(float T, int K, float P) {
   return greedy || (K >= 1 && K <= SMP_CAPC);      // K <= 0 means 'no top-k': whole row
 }
 
+template <typename LT>
 __global__ void __launch_bounds__(256) sample_chunk_kernel(
     float* __restrict__ cand_v, int* __restrict__ cand_i, int* __restrict__ overflow,
-    const float* __restrict__ logits, long row_stride, int V, int L,
+    const LT* __restrict__ logits, long row_stride, int V, int L,
     const float* __restrict__ temperature, const int* __restrict__ top_k,
     const float* __restrict__ top_p) {
   __shared__ uint32_t keys[SMP_CHUNK_MAX];
@@ -186,8 +216,8 @@ __global__ void __launch_bounds__(256) sample_chunk_kernel(
   if (!smp_split_ok(T, K, top_p[row])) return;        // sample_kernel reads the full row
   const int keff = (T <= 0.f || K == 1) ? 1 : K;
   const int lo = c * L, n = max(0, min(V, lo + L) - lo);
-  const float* x = logits + (long)row * row_stride + lo;
-  for (int e = tid; e < n; e += 256) keys[e] = f2key(x[e]);
+  const LT* x = logits + (long)row * row_stride + lo;
+  for (int e = tid; e < n; e += 256) keys[e] = f2key(ldv(x, e));
   __syncthreads();
   // the chunk's keff-th largest key (0: fewer than keff entries -> keep them all)
   const uint32_t tau = n > 0 ? radix_kth(keys, n, (uint32_t)min(keff, n), hist, tmp, sel) : 0u;
@@ -216,8 +246,9 @@ __global__ void __launch_bounds__(256) sample_chunk_kernel(
   }
 }
 
+template <typename LT>
 __global__ void __launch_bounds__(SMP_THREADS) sample_kernel(
-    int* __restrict__ out_tokens, const float* __restrict__ logits, long row_stride, int V,
+    int* __restrict__ out_tokens, const LT* __restrict__ logits, long row_stride, int V,
     const float* __restrict__ temperature, const int* __restrict__ top_k,
     const float* __restrict__ top_p, const long long* __restrict__ seeds,
     const float* __restrict__ cand_v, const int* __restrict__ cand_i,
@@ -232,7 +263,8 @@ __global__ void __launch_bounds__(SMP_THREADS) sample_kernel(
   __shared__ int si[16];
   __shared__ uint32_t s_sel[3], s_cnt;
   const int row = blockIdx.x, tid = threadIdx.x;
-  const float* x = logits + (long)row * row_stride;
+  const LT* xl = logits + (long)row * row_stride;
+  const float* xc = nullptr;                     // two-phase mode: the row's candidate list
   const float T = temperature[row];
   const int K = top_k[row];
   const float P = top_p[row];
@@ -243,7 +275,7 @@ __global__ void __launch_bounds__(SMP_THREADS) sample_kernel(
   const int* map = nullptr;
   if (cand_v != nullptr && smp_split_ok(T, K, P)) {
     if (overflow[row] == 0) {
-      x = cand_v + (long)row * ncand;
+      xc = cand_v + (long)row * ncand;
       map = cand_i + (long)row * ncand;
       V = ncand;
     }
@@ -251,10 +283,15 @@ __global__ void __launch_bounds__(SMP_THREADS) sample_kernel(
     if (tid == 0) overflow[row] = 0;                          // zero for the next call
   }
   auto vocab_id = [&](int j) { return map != nullptr ? map[j] : j; };
+  // every pass over the row: the candidate list (fp32) or the logits row (fp32 / bf16)
+  auto scan = [&](int n, auto&& f) {
+    if (xc != nullptr) row_scan(xc, n, f);
+    else row_scan(xl, n, f);
+  };
 
   if (T <= 0.f || K == 1) {                                  // greedy
     ArgMax a{-INFINITY, 0x7fffffff};
-    row_scan(x, V, [&](float v, int i) { a = amax(a, ArgMax{v, i}); });
+    scan(V, [&](float v, int i) { a = amax(a, ArgMax{v, i}); });
     a = block_argmax(a, sv, si);
     if (tid == 0) out_tokens[row] = a.i < V ? vocab_id(a.i) : 0;
     return;
@@ -270,7 +307,7 @@ __global__ void __launch_bounds__(SMP_THREADS) sample_kernel(
         const int i = base + j;
         if (i < V) {
           const float g = -__logf(-__logf(u01(rr[j])));
-          a = amax(a, ArgMax{x[i] * invT + g, i});
+          a = amax(a, ArgMax{(xc != nullptr ? xc[i] : ldv(xl, i)) * invT + g, i});
         }
       }
     }
@@ -295,7 +332,7 @@ __global__ void __launch_bounds__(SMP_THREADS) sample_kernel(
   //  full radix select below.
   if (Keff <= 256) {
     uint32_t mk = 0u;
-    row_scan(x, (V >> 4) << 2, [&](float v, int) { mk = max(mk, f2key(v)); });
+    scan((V >> 4) << 2, [&](float v, int) { mk = max(mk, f2key(v)); });
     ckey[tid] = mk;
     __syncthreads();
     const uint32_t tau0 = radix_kth(ckey, SMP_THREADS, (uint32_t)Keff, hist, sv, s_sel);
@@ -303,7 +340,7 @@ __global__ void __launch_bounds__(SMP_THREADS) sample_kernel(
     int ti[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) { tk[j] = 0u; ti[j] = 0x7fffffff; }
-    row_scan(x, V, [&](float v, int i) {
+    scan(V, [&](float v, int i) {
       uint32_t k = f2key(v);
       if (k >= tau0 && k > tk[7]) {
         int id = i;
@@ -350,7 +387,7 @@ __global__ void __launch_bounds__(SMP_THREADS) sample_kernel(
     const int shift = 24 - 8 * pass;
     for (int i = tid; i < 256; i += blockDim.x) hist[i] = 0;
     __syncthreads();
-    row_scan(x, V, [&](float v, int) {
+    scan(V, [&](float v, int) {
       const uint32_t k = f2key(v);
       if ((k & pmask) == prefix) atomicAdd(&hist[(k >> shift) & 255u], 1u);
     });
@@ -366,7 +403,7 @@ __global__ void __launch_bounds__(SMP_THREADS) sample_kernel(
   // ---- gather everything at or above the boundary bin
   if (tid == 0) s_cnt = 0;
   __syncthreads();
-  row_scan(x, V, [&](float v, int i) {
+  scan(V, [&](float v, int i) {
     const uint32_t k = f2key(v);
     if ((k & pmask) >= prefix) {
       const uint32_t pos = atomicAdd(&s_cnt, 1u);
@@ -458,9 +495,10 @@ extern "C" int dli_sample_set_split_max_b(int b) {
 // ws: nullable; when given (>= dli_sample_workspace_bytes, its first g_smp_max_b ints
 // zero before the first call — the kernels leave them zero), batches of B <= 8 rows sample in
 // two phases (above).
-extern "C" int dli_sample(int* out_tokens, const float* logits, long row_stride, int B, int V,
-                          const float* temperature, const int* top_k, const float* top_p,
-                          const long long* seeds, void* ws, hipStream_t st) {
+template <typename LT>
+static int launch_sample(int* out_tokens, const LT* logits, long row_stride, int B, int V,
+                         const float* temperature, const int* top_k, const float* top_p,
+                         const long long* seeds, void* ws, hipStream_t st) {
   if (B <= 0) return 0;
   if (ws != nullptr && B <= g_smp_max_b) {
     // P chunks per row: >= 256 workgroups in all, each chunk <= SMP_CHUNK_MAX entries
@@ -471,18 +509,34 @@ extern "C" int dli_sample(int* out_tokens, const float* logits, long row_stride,
       int* overflow = static_cast<int*>(ws);
       float* cand_v = reinterpret_cast<float*>(overflow + g_smp_max_b);
       int* cand_i = reinterpret_cast<int*>(cand_v + (long)B * 64 * SMP_CAPC);
-      sample_chunk_kernel<<<dim3(P, B), 256, 0, st>>>(cand_v, cand_i, overflow, logits,
-                                                       row_stride, V, L, temperature, top_k,
-                                                       top_p);
-      sample_kernel<<<B, SMP_THREADS, 0, st>>>(out_tokens, logits, row_stride, V, temperature,
-                                               top_k, top_p, seeds, cand_v, cand_i, overflow,
-                                               P * SMP_CAPC);
+      sample_chunk_kernel<LT><<<dim3(P, B), 256, 0, st>>>(cand_v, cand_i, overflow, logits,
+                                                          row_stride, V, L, temperature, top_k,
+                                                          top_p);
+      sample_kernel<LT><<<B, SMP_THREADS, 0, st>>>(out_tokens, logits, row_stride, V,
+                                                  temperature, top_k, top_p, seeds, cand_v,
+                                                  cand_i, overflow, P * SMP_CAPC);
       DLI_RETURN_LAUNCH();
     }
   }
-  sample_kernel<<<B, SMP_THREADS, 0, st>>>(out_tokens, logits, row_stride, V, temperature, top_k,
-                                           top_p, seeds, nullptr, nullptr, nullptr, 0);
+  sample_kernel<LT><<<B, SMP_THREADS, 0, st>>>(out_tokens, logits, row_stride, V, temperature,
+                                              top_k, top_p, seeds, nullptr, nullptr, nullptr, 0);
   DLI_RETURN_LAUNCH();
+}
+
+extern "C" int dli_sample(int* out_tokens, const float* logits, long row_stride, int B, int V,
+                          const float* temperature, const int* top_k, const float* top_p,
+                          const long long* seeds, void* ws, hipStream_t st) {
+  return launch_sample(out_tokens, logits, row_stride, B, V, temperature, top_k, top_p, seeds,
+                       ws, st);
+}
+
+// the same over bf16 logits (row_stride in elements)
+extern "C" int dli_sample_bf16(int* out_tokens, const void* logits, long row_stride, int B,
+                               int V, const float* temperature, const int* top_k,
+                               const float* top_p, const long long* seeds, void* ws,
+                               hipStream_t st) {
+  return launch_sample(out_tokens, static_cast<const u16*>(logits), row_stride, B, V,
+                       temperature, top_k, top_p, seeds, ws, st);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -495,14 +549,15 @@ extern "C" int dli_sample(int* out_tokens, const float* logits, long row_stride,
 //      == tau in index order) already in ascending index order — the order the candidate
 //      merge on rank 0 requires (ranks concatenate ascending vocab slices).
 // Replaces torch.topk + torch.sort + gather on the pipeline's hot path.
+template <typename T>
 __global__ void __launch_bounds__(SMP_THREADS) topk_rows_kernel(
-    float* __restrict__ out_v, int* __restrict__ out_i, const float* __restrict__ x,
+    float* __restrict__ out_v, int* __restrict__ out_i, const T* __restrict__ x,
     long row_stride, int V, int c, int id_offset) {
   __shared__ uint32_t hist[256];
   __shared__ float sv[16];
   __shared__ uint32_t s_sel[3];
   const int row = blockIdx.x, tid = threadIdx.x;
-  const float* xr = x + (long)row * row_stride;
+  const T* xr = x + (long)row * row_stride;
   uint32_t prefix = 0, pmask = 0, k_rem = (uint32_t)c;
   for (int pass = 0; pass < 4; ++pass) {
     const int shift = 24 - 8 * pass;
@@ -526,7 +581,7 @@ __global__ void __launch_bounds__(SMP_THREADS) topk_rows_kernel(
   const int lo = min(V, tid * per), hi = min(V, lo + per);
   uint32_t n_gt = 0, n_eq = 0;
   for (int e = lo; e < hi; ++e) {
-    const uint32_t k = f2key(xr[e]);
+    const uint32_t k = f2key(ldv(xr, e));
     n_gt += k > tau;
     n_eq += k == tau;
   }
@@ -536,7 +591,7 @@ __global__ void __launch_bounds__(SMP_THREADS) topk_rows_kernel(
   uint32_t eq_before = (uint32_t)eq_incl - n_eq;            // ties in earlier slices
   uint32_t before = (uint32_t)gt_incl - n_gt + min(eq_before, k_rem);
   for (int e = lo; e < hi && before < (uint32_t)c; ++e) {
-    const float v = xr[e];
+    const float v = ldv(xr, e);
     const uint32_t k = f2key(v);
     bool take = k > tau;
     if (k == tau) { take = eq_before < k_rem; ++eq_before; }
@@ -552,6 +607,16 @@ extern "C" int dli_topk_rows(float* out_v, int* out_i, const float* x, long row_
                              int V, int c, int id_offset, hipStream_t st) {
   if (rows <= 0) return 0;
   if (c < 1 || c > V || V > (1 << 24)) return (int)hipErrorInvalidValue;
-  topk_rows_kernel<<<rows, SMP_THREADS, 0, st>>>(out_v, out_i, x, row_stride, V, c, id_offset);
+  topk_rows_kernel<float><<<rows, SMP_THREADS, 0, st>>>(out_v, out_i, x, row_stride, V, c,
+                                                         id_offset);
+  DLI_RETURN_LAUNCH();
+}
+
+extern "C" int dli_topk_rows_bf16(float* out_v, int* out_i, const void* x, long row_stride,
+                                  int rows, int V, int c, int id_offset, hipStream_t st) {
+  if (rows <= 0) return 0;
+  if (c < 1 || c > V || V > (1 << 24)) return (int)hipErrorInvalidValue;
+  topk_rows_kernel<u16><<<rows, SMP_THREADS, 0, st>>>(out_v, out_i, static_cast<const u16*>(x),
+                                                       row_stride, V, c, id_offset);
   DLI_RETURN_LAUNCH();
 }

@@ -100,9 +100,15 @@ struct ErrRef {
   uint64_t* host;                    // pinned host word (device address): polled by the host
 };
 
+// The device mirror takes the read-modify-write; the pinned host word only a plain
+// system-scope store of the accumulated bits (a device atomic on host memory needs PCIe
+// AtomicOps from the root complex, which a host may not provide). Bits only ever grow, so a
+// racing store can at worst drop another raiser's bit from the host copy — never clear the
+// word: the host's per-tick poll still sees a nonzero error.
 __device__ __forceinline__ void raise_err(ErrRef e, uint64_t bit) {
-  __hip_atomic_fetch_or(e.dev, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  __hip_atomic_fetch_or(e.host, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const uint64_t v =
+      __hip_atomic_fetch_or(e.dev, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) | bit;
+  __hip_atomic_store(e.host, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Sender: payload -> peer mailbox (after the header), header {++seq, bytes}. A plain
@@ -466,8 +472,12 @@ void* dli_ipc_create(int world, int rank, const long long* cap, const char* host
         khz <= 0)
       khz = 100000;
     e->khz = khz;
+    // the budget covers the longest legitimate gap between a peer's send and this rank's
+    // receive (a long prefill on a shared GPU, a first-use library load): 120 s by default,
+    // DLI_IPC_WAIT_S per deployment. A dead peer is caught long before by the pipeline
+    // watchdog (process liveness on the control ring), which aborts the endpoint.
     const char* bs = getenv("DLI_IPC_WAIT_S");
-    const double secs = bs ? atof(bs) : 20.0;
+    const double secs = bs ? atof(bs) : 120.0;
     e->wait_budget = (unsigned long long)(secs * 1000.0 * khz);
   }
   // FREE words start at 1 (every mailbox empty), READY words and the error mirror at 0

@@ -51,9 +51,9 @@ def _hipcc() -> str:
 # -inf as the masked-score / running-max sentinel (poison under ninf -> NaNs).
 KERNEL_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-fno-gpu-rdc",
                 "-munsafe-fp-atomics", "-Wno-unused-result"]
-# DLI_GEMM_AB=1: also build the 4-wave GEMM's A/B variants (tiles 35-40, 42-44)
-if os.environ.get("DLI_GEMM_AB", "0") == "1":
-    KERNEL_FLAGS.append("-DDLI_GEMM_AB_VARIANTS=1")
+# DLI_GEMM_AB=1: also build the 4-wave GEMM's losing A/B variants (csrc/ab/, tiles 35-40,
+# 42-44, 46-53) into the kernel library; the production build never compiles them
+GEMM_AB = os.environ.get("DLI_GEMM_AB", "0") == "1"
 RUNTIME_FLAGS = ["-O2", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",
                  "-Wno-unused-result"]
 
@@ -123,8 +123,11 @@ def _link(objs, out: Path, extra=()):
 
 def _group_sources(kind: str):
     if kind == "kernels":
-        return (sorted((CSRC / "kernels").glob("*.hip")), sorted((CSRC / "kernels").glob("*.h")),
-                KERNEL_FLAGS)
+        srcs = sorted((CSRC / "kernels").glob("*.hip"))
+        if GEMM_AB:
+            srcs += sorted((CSRC / "ab").glob("*.hip"))
+        return srcs, sorted((CSRC / "kernels").glob("*.h")), KERNEL_FLAGS + (
+            ["-DDLI_GEMM_AB_VARIANTS=1"] if GEMM_AB else [])
     return (sorted((CSRC / "runtime").glob("*.cpp")), sorted((CSRC / "runtime").glob("*.h")),
             RUNTIME_FLAGS)
 
@@ -162,13 +165,13 @@ def build(force: bool = False, jobs: int = 0, verbose: bool = True) -> dict:
     jobs = jobs or min(8, os.cpu_count() or 4)
     if force and OBJDIR.exists():
         shutil.rmtree(OBJDIR)
-    k_srcs, k_hdrs, _ = _group_sources("kernels")
+    k_srcs, k_hdrs, k_flags = _group_sources("kernels")
     r_srcs, r_hdrs, _ = _group_sources("runtime")
     out = {}
     # --no-undefined: a kernel whose host-side handle hipcc failed to emit (it happens
     # silently, e.g. for a lambda capturing an __amdgpu_buffer_rsrc_t) fails the link here
     # instead of the library failing to load on the GPU box
-    out["kernels"] = _build_group(k_srcs, k_hdrs, KERNEL_FLAGS, LIBDIR / "libdli_kernels.so", jobs,
+    out["kernels"] = _build_group(k_srcs, k_hdrs, k_flags, LIBDIR / "libdli_kernels.so", jobs,
                                   extra=("-Wl,--no-undefined",), kind="kernels")
     if r_srcs:
         out["runtime"] = _build_group(r_srcs, r_hdrs, RUNTIME_FLAGS, LIBDIR / "libdli_runtime.so",

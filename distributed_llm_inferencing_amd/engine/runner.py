@@ -196,9 +196,9 @@ class StageRunner:
                 add(lp.get("w_gu"), "silu_mul"), add(lp.get("w_down"), "splitk")
         if m.is_last and not m.vocab_parallel:
             head = m.params["embed"] if m.cfg.tie_embeddings else m.params.get("lm_head")
-            add(head, "f32")
+            add(head, ops.HEAD_EPI)
         if m.vocab_parallel:                 # this rank's slice of the LM head
-            add(m.params.get("head_slice"), "f32")
+            add(m.params.get("head_slice"), ops.HEAD_EPI)
         return shapes, weights
 
     def tune_lock(self):
@@ -251,7 +251,7 @@ class StageRunner:
 
     def autotune_prefill(self, max_tokens: int) -> None:
         """GEMM plans of prefill steps, one per power-of-two token bucket from 2048 up to the
-        bucket of ``max_tokens``: our 8-phase kernel against hipBLASLt, the faster pinned
+        bucket of ``max_tokens``: our 8-phase kernel against our 4-wave kernel, the faster pinned
         (``ops.gemm.prefill_candidates``). Skipped like the decode autotune
         (DLI_GEMM_AUTOTUNE=0, non-GPU) and by DLI_TUNE_PREFILL=0."""
         if (os.environ.get("DLI_GEMM_AUTOTUNE", "1") != "1" or self.device.type != "cuda"

@@ -224,11 +224,14 @@ class TransformerLM:
         return ops.rmsnorm(hidden, p["final_norm"], cfg.norm_eps)
 
     def head_logits(self, h: torch.Tensor) -> torch.Tensor:
+        """LM head in the model dtype (``ops.HEAD_EPI``), as HF's ``lm_head(h).float()``:
+        the sampler reads the bf16 logits and compares their exact fp32 values."""
         p = self.params
-        return ops.linear(h, p["embed"] if self.cfg.tie_embeddings else p["lm_head"], epi="f32")
+        return ops.linear(h, p["embed"] if self.cfg.tie_embeddings else p["lm_head"],
+                          epi=ops.HEAD_EPI)
 
     def logits(self, hidden: torch.Tensor, b: DeviceBatch) -> torch.Tensor:
-        """Final norm + LM head on the last token of each sequence -> fp32 [S, V]."""
+        """Final norm + LM head on the last token of each sequence -> [S, V] logits."""
         return self.head_logits(self.final_hidden(hidden, b))
 
     def head_candidates(self, h: torch.Tensor, c: int = 64):

@@ -20,7 +20,11 @@ from . import reference as R
 _native_call = N.call
 _p = N.ptr
 _FUSED_OFF = __import__("os").environ.get("DLI_NO_FUSED_REDUCE", "0") == "1"   # A/B switch
-# rows per expert from which eager (prefill) MoE GEMMs go to hipBLASLt per expert
+# batch-1: split-K combine + add + RMSNorm inside the GEMV launch (DLI_GEMV_FUSED_NORM=1). Off by
+# default: its serial tail (two arrival tickets, one workgroup normalising the row) measured
+# 0.8 % slower per token than GEMV + splitk_add_rmsnorm (profiles/r5/s03/bench.jsonl)
+_FUSED_GEMV_NORM = os.environ.get("DLI_GEMV_FUSED_NORM", "0") == "1"
+# rows per expert from which eager (prefill) MoE GEMMs take the grouped 256x256 tile
 _MOE_PREFILL_ROWS = int(__import__("os").environ.get("DLI_MOE_PREFILL_ROWS", "1024"))
 
 
@@ -107,22 +111,6 @@ def _gemm_native(x, w, epi: str, bias=None, out=None, plan: Optional[G.GemmPlan]
     if out is None:
         dt = torch.float32 if epi == "f32" else x.dtype
         out = torch.empty(M, out_n, dtype=dt, device=x.device)
-    if plan.backend == "hipblaslt" and group_off is None:
-        # plain library GEMM (hipBLASLt) + our epilogue kernel as a separate pass
-        if epi in ("none", "splitk"):
-            torch.matmul(x, w.t(), out=out)
-            return out
-        if epi == "f32":           # hipBLASLt bf16 x bf16 -> fp32 output (LM head logits)
-            torch.mm(x, w.t(), out_dtype=torch.float32, out=out)
-            return out
-        y = torch.matmul(x, w.t())
-        if epi == "silu_mul":
-            _native_call("dli_silu_mul", _p(out), _p(y), M, out_n, _st())
-        elif epi in ("bias", "bias_gelu"):
-            _native_call("dli_bias_act", _p(y), _p(bias), M, Nn, 1 if epi == "bias_gelu" else 0,
-                         _st())
-            out.copy_(y)
-        return out
     splits = plan.splits
     ws = None
     if splits > 1:
@@ -165,7 +153,7 @@ def _splitk_plan(x, w):
         return None
     M, K = x.shape
     p = G.plan(M, w.shape[0], K, "splitk")
-    return p if (p.backend == "dli" and p.splits > 1) else None
+    return p if p.splits > 1 else None
 
 
 def linear_add_rmsnorm(x, w, residual, norm_w, eps, plan: Optional[G.GemmPlan] = None):
@@ -176,7 +164,7 @@ def linear_add_rmsnorm(x, w, residual, norm_w, eps, plan: Optional[G.GemmPlan] =
     if plan is None:
         p = _splitk_plan(x, w)
     else:
-        p = plan if (plan.backend == "dli" and plan.splits > 1) else None
+        p = plan if plan.splits > 1 else None
     if p is None:
         y = linear(x, w) if plan is None else _gemm_native(x, w, "none", plan=plan)
         if norm_w is None:
@@ -186,9 +174,17 @@ def linear_add_rmsnorm(x, w, residual, norm_w, eps, plan: Optional[G.GemmPlan] =
     M, K = x.shape
     Nn = w.shape[0]
     ws = G.workspace(x.device, p.splits * M * Nn * 4)
+    out = torch.empty_like(residual) if norm_w is not None else None
+    if (p.tile in G.GEMV_FUSED_NORM_TILES and M <= G.GEMV_MAX_M and p.splits in (2, 4, 8)
+            and residual.is_contiguous() and _FUSED_GEMV_NORM):
+        # batch-1 decode: the split-K combine + residual add + RMSNorm run inside the GEMV's
+        # own launch (arrival tickets; gemm.hip gemv_addnorm_kernel), no second kernel
+        _native_call("dli_gemv_add_rmsnorm", _p(x), x.stride(0), _p(w), w.stride(-2), M, Nn,
+                     K, p.tile, p.splits, _p(residual), _p(out), _p(norm_w), eps, _p(ws),
+                     _p(G.tickets(x.device, Nn // 16 + 2, _st())), _st())
+        return out
     _native_call("dli_gemm", _p(x), x.stride(0), _p(w), w.stride(-2), None, Nn, M, Nn, K,
                  0, p.tile, p.splits, None, _p(ws), None, 1, _st())
-    out = torch.empty_like(residual) if norm_w is not None else None
     _native_call("dli_splitk_add_rmsnorm", _p(out), _p(residual), _p(ws), p.splits, M, Nn,
                  _p(norm_w), eps, _st())
     return out
@@ -201,7 +197,7 @@ def linear_rope_cache(x, w, positions, slot_mapping, cos_sin, k_cache, v_cache, 
     if plan is None:
         p = _splitk_plan(x, w)
     else:
-        p = plan if (plan.backend == "dli" and plan.splits > 1) else None
+        p = plan if plan.splits > 1 else None
     if p is None:
         qkv = linear(x, w) if plan is None else _gemm_native(x, w, "none", plan=plan)
         rope_and_cache(qkv, positions, slot_mapping, cos_sin, k_cache, v_cache, hq, hkv, hd,
@@ -452,8 +448,15 @@ def _sample_ws(device, B: int, V: int):
     return ws
 
 
+# LM-head logits in the model dtype (bf16), as HF computes them (``lm_head(h)`` in the model's
+# dtype, then ``.float()``): half the bytes written by the head GEMM and read by the sampler.
+# DLI_FP32_LOGITS=1: the fp32-output head (the round-4 path), for A/B runs.
+HEAD_EPI = "f32" if os.environ.get("DLI_FP32_LOGITS", "0") == "1" else "none"
+
+
 def sample(logits, temperature, top_k, top_p, seeds, generator=None, ids=None):
-    """logits fp32 [B, V] -> int32 tokens [B]. temperature<=0 -> greedy. With ``ids``
+    """logits fp32 or bf16 [B, V] -> int32 tokens [B] (every comparison on the exact fp32
+    value of each logit). temperature<=0 -> greedy. With ``ids``
     [B, V] the row holds candidates (vocab-parallel LM head) in ascending token-id order,
     and the sampled column is mapped to its token id (ties then break by token id exactly
     as over the full vocabulary)."""
@@ -462,7 +465,10 @@ def sample(logits, temperature, top_k, top_p, seeds, generator=None, ids=None):
                         ids=ids)
     B, V = logits.shape
     out = torch.empty(B, dtype=torch.int32, device=logits.device)
-    _native_call("dli_sample", _p(out), _p(logits), logits.stride(0), B, V, _p(temperature),
+    if logits.dtype not in (torch.float32, torch.bfloat16):
+        logits = logits.float()
+    fn = "dli_sample_bf16" if logits.dtype == torch.bfloat16 else "dli_sample"
+    _native_call(fn, _p(out), _p(logits), logits.stride(0), B, V, _p(temperature),
                  _p(top_k), _p(top_p), _p(seeds), _p(_sample_ws(logits.device, B, V)), _st())
     if ids is not None:
         out = ids.gather(1, out.long().unsqueeze(1)).squeeze(1).to(torch.int32)
@@ -470,22 +476,25 @@ def sample(logits, temperature, top_k, top_p, seeds, generator=None, ids=None):
 
 
 def head_candidates(h, w_slice, offset: int, c: int):
-    """Vocab-parallel LM head slice on this rank: fp32 logits for token ids
-    ``[offset, offset + V_r)`` and the top-``c`` per row, returned in ascending token-id
-    order (values fp32 [S, c], ids int32 [S, c]). The union over ranks contains every
-    token a top-k <= c sampler can pick."""
-    if not _use_native(h):
-        v, i = R.head_candidates(h, w_slice, offset, c)
-        i, perm = torch.sort(i, dim=-1)
-        return v.gather(1, perm), i
-    lg = linear(h, w_slice, epi="f32")
+    """Vocab-parallel LM head slice on this rank: logits (``HEAD_EPI``: the model dtype, as
+    the single-stage head) for token ids ``[offset, offset + V_r)`` and the top-``c`` per
+    row (ties broken by the lower token id), returned in ascending token-id order (values
+    fp32 [S, c], ids int32 [S, c]). The union over ranks contains every token a top-k <= c
+    sampler can pick."""
+    lg = linear(h, w_slice, epi=HEAD_EPI)
     S, V = lg.shape
     c = min(c, V)
+    if not _use_native(h):
+        # stable descending sort: equal logits keep ascending token-id order
+        v, i = torch.sort(lg.float(), dim=-1, descending=True, stable=True)
+        v, i = v[:, :c], (i[:, :c] + offset).to(torch.int32)
+        i, perm = torch.sort(i, dim=-1)
+        return v.gather(1, perm), i
     v = torch.empty(S, c, dtype=torch.float32, device=h.device)
     i = torch.empty(S, c, dtype=torch.int32, device=h.device)
     # HIP top-c per row, written in ascending id order (sampling.hip topk_rows_kernel)
-    _native_call("dli_topk_rows", _p(v), _p(i), _p(lg), lg.stride(0), S, V, c, int(offset),
-                 _st())
+    fn = "dli_topk_rows_bf16" if lg.dtype == torch.bfloat16 else "dli_topk_rows"
+    _native_call(fn, _p(v), _p(i), _p(lg), lg.stride(0), S, V, c, int(offset), _st())
     return v, i
 
 

@@ -6,13 +6,11 @@ The projection GEMMs of a decode step are skinny (M = batch) and of a prefill st
 * a tile from {64x64, 64x128, 128x128, 128x256, 256x128} sized to M,
 * a split-K factor so the grid covers the 256 CUs (cdna_hip_programming.md §5 'Projection
   GEMM at M = 256': choose SPLITK so that tiles * SPLITK ~ 0.5-1x the CU count),
-* the backend: decode GEMMs (the hipGraph steps) always on our MFMA kernels, tiles
-  autotuned at graph capture (on by default; ``DLI_GEMM_AUTOTUNE=0`` disables it). Prefill
-  GEMMs: our 8-phase 256x256 kernel or the one-wave-per-SIMD 256x256 kernel (tile 45),
-  whichever the warmup measures faster per token bucket (``prefill_candidates``). hipBLASLt
-  is off the hot path: ``DLI_TUNE_PREFILL_BLAS=1`` lets it compete in the prefill autotune,
-  ``DLI_GEMM_BACKEND=hipblaslt``, ``DLI_GEMM_PREFILL_BLAS=1`` and ``DLI_GEMM_DECODE_BLAS=1``
-  force it (ablations; ``DLI_GEMM_NO_BLAS=1`` vetoes all of them).
+* every GEMM runs on our kernels (no vendor-library backend): decode GEMMs (the hipGraph
+  steps) on tiles autotuned at graph capture (on by default; ``DLI_GEMM_AUTOTUNE=0``
+  disables it); prefill GEMMs on our 8-phase 256x256 kernel or the one-wave-per-SIMD 256x256
+  kernel (tile 45), whichever the warmup measures faster per token bucket
+  (``prefill_candidates``).
 
 Split-K partial slabs live in a grow-only per-device workspace; engines warm every shape
 up before hipGraph capture so no allocation happens inside a capture.
@@ -68,6 +66,9 @@ GEMV_TILES = {30: 16, 31: 32, 32: 16, 33: 32,   # 32 / 33: 4 K-steps in flight p
               29: 16}   # 29: SiLU*up on the 16-row grid (8 gate + 8 up rows), M <= 4
 GEMV_M1_ONLY = (32, 33)
 GEMV_MAX_M = 4
+# weight-streaming tiles whose split-K combine + residual add + RMSNorm run in-launch
+# (ops.linear_add_rmsnorm -> dli_gemv_add_rmsnorm)
+GEMV_FUSED_NORM_TILES = (30, 31, 32, 33)
 TILE_WAVES = {13: (2, 4), 14: (4, 2), 15: (2, 4), 16: (4, 2), 17: (2, 4),
               22: (2, 4), 23: (2, 4), 24: (2, 4), 25: (4, 2),
               26: (4, 2), 27: (2, 4), 28: (4, 2)}
@@ -96,7 +97,7 @@ NUM_CUS = int(os.environ.get("DLI_NUM_CUS", "256"))
 
 @dataclass(frozen=True)
 class GemmPlan:
-    backend: str      # "dli" | "hipblaslt"
+    backend: str      # "dli": our kernels (the only backend)
     tile: int
     splits: int
 
@@ -109,6 +110,25 @@ _workspaces: dict = {}
 # decode graphs are captured and grows the workspace; freeing the old buffer let eager
 # tensors take its memory while graph replays still wrote split-K slabs into it)
 _retired: list = []
+
+
+_tickets: dict = {}
+
+
+def tickets(device: torch.device, n: int, stream: int = 0) -> torch.Tensor:
+    """Zeroed uint32 arrival counters for in-launch split-K combines, one buffer per (device,
+    stream) — launches on one stream never overlap — grow-only and never freed (captured
+    graphs keep the pointer). Every launch's last arrivers reset the counters they used, so
+    they are zero again for the next launch on the stream."""
+    key = (device.type, device.index, int(stream))
+    with _ws_lock:
+        t = _tickets.get(key)
+        if t is None or t.numel() < n:
+            if t is not None:
+                _retired.append(t)
+            t = torch.zeros(max(n, 4096), dtype=torch.int32, device=device)
+            _tickets[key] = t
+        return t
 
 
 def workspace(device: torch.device, nbytes: int) -> torch.Tensor:
@@ -131,17 +151,12 @@ def _heuristic(M: int, N: int, K: int, epi: str) -> GemmPlan:
     """Fitted to profiles/r1_gemm/gemm_bench.json and profiles/r1_gemm8p/ (MI355X, random
     bf16 operands): skinny decode GEMMs (M <= 512) on the 2/3-stage tiles below (autotuned
     at capture); fat prefill GEMMs (M >= LARGE_M) on the 256x256 8-phase ping-pong kernel
-    (tile 22) with its fused epilogue (SiLU*up, bias+GELU, fp32) unless the prefill
-    autotune (``prefill_candidates``) measured hipBLASLt faster for the bucket.
-    ``DLI_GEMM_PREFILL_BLAS=1`` routes plain prefill GEMMs to hipBLASLt without measuring
-    (ablation)."""
+    (tile 22) with its fused epilogue (SiLU*up, bias+GELU, fp32); the prefill autotune
+    (``prefill_candidates``) may pin the 4-wave tile instead."""
     # M > 512: mixed prefill+decode steps of a full batch and prefill — 256x256 8-phase
     # tiles (the 128-row tiles below ran a 512 + 300-token mixed step's GEMMs ~2.5x slower
     # than the tuned decode step: 26.7 ms per mixed step end to end, profiles/r3/e2e/)
     if M >= LARGE_M or M > 512:
-        if (os.environ.get("DLI_GEMM_PREFILL_BLAS", "0") == "1" and epi in ("none", "splitk")
-                and os.environ.get("DLI_GEMM_NO_BLAS", "0") != "1"):
-            return GemmPlan("hipblaslt", 2, 1)
         # mid-sized steps (serving refills / mixed steps of ~1-2k rows): 256x256 tiles leave
         # most CUs idle on the N = 4096 / 6144 projections (M = 1200: 80 / 120 tiles), so
         # split K while the grid stays within one wave of the chip
@@ -274,10 +289,7 @@ def plan(M: int, N: int, K: int, epi: str) -> GemmPlan:
     p = _plan_cache.get(key)
     if p is not None:
         return p
-    forced = os.environ.get("DLI_GEMM_BACKEND", "")
     p = _heuristic(M, N, K, epi)
-    if forced == "hipblaslt" and epi == "none":
-        p = GemmPlan("hipblaslt", p.tile, 1)
     _plan_cache[key] = p
     return p
 
@@ -346,9 +358,6 @@ def autotune(shapes, weights: dict, device, iters: int = 6, log=None,
         best = None
         t_shape = time.perf_counter()
         for p in (candidates or candidate_plans)(M, N, K, epi):
-            if p.backend == "hipblaslt" and epi not in ("none", "splitk", "silu_mul", "f32"):
-                continue
-
             def run(p=p):
                 for w in ws_:
                     if is_qkv and decode_qkv:
@@ -371,7 +380,7 @@ def autotune(shapes, weights: dict, device, iters: int = 6, log=None,
         if best is not None:
             _plan_cache[key] = best[0]
             _tuned.add(key)
-            if epi == "splitk" and (best[0].splits == 1 or best[0].backend != "dli"):
+            if epi == "splitk" and best[0].splits == 1:
                 _plan_cache[(_bucket(M), N, K, "none")] = best[0]
                 _tuned.add((_bucket(M), N, K, "none"))
             out[(M, N, K, epi)] = best
@@ -423,25 +432,14 @@ _GRAPH_TUNE = os.environ.get("DLI_GEMM_TUNE_GRAPH", "1") == "1"
 
 def prefill_candidates(M: int, N: int, K: int, epi: str):
     """Prefill-sized GEMMs (M > 1024 rows): our 8-phase 256x256 kernel with the heuristic's
-    split count against hipBLASLt (+ our SiLU*up pass for gate/up; the residual add + RMSNorm
-    and RoPE/cache consumers run as their own kernels after either). At these sizes the GEMM
-    is MFMA-bound, so the autotuner times them warm (``cold_bytes`` 1). Measured at
-    M = 16384 on MI355X: ours 1.37-1.46 PF, hipBLASLt 1.57-1.62 PF on the plain projections
-    (profiles/r3/prefill_gemm/). Not a candidate by default since round 4: with tile 41 in
-    the autotune the whole b512 bench lost 0.35 % without it (43,820 -> 43,665 tok/s, same
-    box, profiles/r4/README.md); ``DLI_TUNE_PREFILL_BLAS=1`` restores it."""
+    split count against our one-wave-per-SIMD 256x256 kernel (PREFILL_4W_TILE, the
+    two-barrier schedule) at the same split, 1-4 % apart on the square / QKV / gate-up /
+    down prefill shapes (profiles/r4/gemm4w/), measured per shape and bucket. At these sizes
+    the GEMM is MFMA-bound, so the autotuner times them warm (``cold_bytes`` 1)."""
     out = [_heuristic(M, N, K, epi)]
-    # the one-wave-per-SIMD 256x256 kernel (PREFILL_4W_TILE: the two-barrier schedule) at
-    # the same split: 1-4 % faster than the 8-phase tile on the square / QKV / gate-up /
-    # down prefill shapes (profiles/r4/gemm4w/), measured per shape and bucket
     base = out[0]
-    if base.backend == "dli" and base.tile == 22 and PREFILL_4W_TILE > 0:
+    if base.tile == 22 and PREFILL_4W_TILE > 0:
         out.append(GemmPlan("dli", PREFILL_4W_TILE, base.splits))
-    if (epi in ("none", "splitk", "silu_mul", "f32")
-            and os.environ.get("DLI_GEMM_NO_BLAS", "0") != "1"
-            and os.environ.get("DLI_TUNE_PREFILL_BLAS", "0") == "1"
-            and out[0].backend != "hipblaslt"):
-        out.append(GemmPlan("hipblaslt", 0, 1))
     return out
 
 
@@ -488,13 +486,4 @@ def candidate_plans(M: int, N: int, K: int, epi: str):
             for splits in (1, 2, 4, 8):
                 if K % (64 * splits) == 0 and K // splits >= 512:
                     out.append(GemmPlan("dli", tile, splits))
-    # hipBLASLt (+ our epilogue pass for silu_mul) competes for decode-sized GEMMs only when
-    # DLI_GEMM_DECODE_BLAS=1: measured in-situ at M = 512 our kernels (8-wave 256x256 gate/up
-    # with fused SiLU, 3-stage 128-row tiles) run the decode layer as fast as the library mix
-    # (249.5 vs 257 us per layer, profiles/r1_final/), so the decode hot path stays entirely
-    # on hand-written MFMA kernels.
-    if (epi in ("none", "splitk", "silu_mul", "f32")
-            and os.environ.get("DLI_GEMM_DECODE_BLAS", "0") == "1"
-            and os.environ.get("DLI_GEMM_NO_BLAS") != "1"):
-        out.append(GemmPlan("hipblaslt", 0, 1))
     return out

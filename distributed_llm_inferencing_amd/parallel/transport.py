@@ -513,7 +513,7 @@ def ipc_selftest(ep, group, wait_s: float = 10.0) -> bool:
         ok = False
     finally:
         try:
-            ep.set_wait(float(os.environ.get("DLI_IPC_WAIT_S", "20")))
+            ep.set_wait(float(os.environ.get("DLI_IPC_WAIT_S", "120")))
         except Exception:  # noqa: BLE001
             pass
     verdicts = [None] * dist.get_world_size(group)

@@ -175,6 +175,73 @@ def test_gemv_skinny(gpu, M, N, K, epi):
         G.clear_plans()
 
 
+@pytest.mark.parametrize("M,N,K", [(1, 4096, 4096), (1, 4096, 14336), (2, 1024, 2048),
+                                   (4, 2048, 1536), (3, 1000, 1024)])
+def test_gemv_in_launch_add_rmsnorm(gpu, M, N, K):
+    """Batch-1 decode: split-K combine + residual add + RMSNorm inside the GEMV launch
+    (arrival tickets, gemm.hip gemv_addnorm_kernel) == the fp32 reference; the residual is
+    bit-identical to the two-kernel path (same slice order); the tickets reset themselves
+    (20 back-to-back launches, then graph replays, all equal)."""
+    torch.manual_seed(21)
+    ops._FUSED_GEMV_NORM = True
+    x, w = rnd(M, K, dev=gpu), rnd(N, K, dev=gpu, scale=0.05)
+    r0, nw = rnd(M, N, dev=gpu), rnd(N, dev=gpu)
+    ref_out, ref_res = R.fused_add_rmsnorm(R.linear(x, w), r0, nw, 1e-5)
+    for tile in G.GEMV_FUSED_NORM_TILES:
+        if tile in G.GEMV_M1_ONLY and M > 1:
+            continue
+        for splits in (2, 4, 8):
+            if K % (8 * splits):
+                continue
+            G.set_plan(M, N, K, "splitk", G.GemmPlan("dli", tile, splits))
+            res = r0.clone()
+            out = ops.linear_add_rmsnorm(x, w, res, nw, 1e-5)
+            close(out, ref_out, rtol=2e-2, atol=3e-2)
+            close(res, ref_res, rtol=1e-2, atol=2e-2)
+            # the two-kernel path (gemv slabs + splitk_add_rmsnorm): same residual bits
+            ops._FUSED_GEMV_NORM = False
+            try:
+                res2 = r0.clone()
+                out2 = ops.linear_add_rmsnorm(x, w, res2, nw, 1e-5)
+            finally:
+                ops._FUSED_GEMV_NORM = True
+            assert torch.equal(res, res2), (tile, splits)
+            close(out, out2, rtol=1e-2, atol=1e-2)
+            # add-only (a stage's last layer)
+            res3 = r0.clone()
+            assert ops.linear_add_rmsnorm(x, w, res3, None, 1e-5) is None
+            assert torch.equal(res3, res)
+            # back-to-back launches on one stream: every launch sees zeroed tickets
+            outs = []
+            for _ in range(20):
+                rr = r0.clone()
+                outs.append((ops.linear_add_rmsnorm(x, w, rr, nw, 1e-5), rr))
+            torch.cuda.synchronize()
+            assert all(torch.equal(o, out) and torch.equal(rr, res) for o, rr in outs)
+    # captured and replayed (the decode step's form)
+    G.set_plan(M, N, K, "splitk", G.GemmPlan("dli", 30, 2))
+    res_g = r0.clone()
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(st):
+        ops.linear_add_rmsnorm(x, w, res_g.clone(), nw, 1e-5)       # warm the workspace
+    torch.cuda.current_stream().wait_stream(st)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out_g = ops.linear_add_rmsnorm(x, w, res_g, nw, 1e-5)
+    want_out, want_res = None, None
+    for _ in range(5):
+        res_g.copy_(r0)
+        g.replay()
+        torch.cuda.synchronize()
+        if want_out is None:
+            want_out, want_res = out_g.clone(), res_g.clone()
+        assert torch.equal(out_g, want_out) and torch.equal(res_g, want_res)
+    close(want_out, ref_out, rtol=2e-2, atol=3e-2)
+    G.clear_plans()
+    ops._FUSED_GEMV_NORM = os.environ.get("DLI_GEMV_FUSED_NORM", "0") == "1"
+
+
 def test_prefill_autotune_pins_a_correct_plan(gpu):
     """StageRunner.autotune_prefill's measurement (ops.gemm.autotune over prefill_candidates:
     our 8-phase kernel vs hipBLASLt) pins one plan per shape, and whichever it pins computes
@@ -261,11 +328,6 @@ def test_gemm_epilogues(gpu, epi, M, N, K):
             close(out, ref, rtol=2e-2, atol=2e-2)
             if epi == "f32":
                 assert out.dtype == torch.float32
-    # hipBLASLt plan (autotune candidate) + our epilogue pass
-    out = ops._gemm_native(x, w, epi, bias=b if "bias" in epi else None,
-                           plan=G.GemmPlan("hipblaslt", 0, 1))
-    close(out, ref, rtol=2e-2, atol=2e-2)
-    assert out.dtype == (torch.float32 if epi == "f32" else BF)
 
 
 @pytest.mark.parametrize("M,N,K", [(3, 512, 1024), (256, 4096, 4096), (77, 4096, 14336),
@@ -690,7 +752,7 @@ def test_vocab_parallel_candidates_sample_like_full_vocab(gpu):
     B, D, V, N = 64, 256, 8000, 4
     h = rnd(B, D, dev=gpu)
     w = rnd(V, D, dev=gpu, scale=0.2)
-    full = ops.linear(h, w, epi="f32")
+    full = ops.linear(h, w, epi=ops.HEAD_EPI)                # the single-stage head's logits
     bounds = [round(i * V / N) for i in range(N + 1)]
     vals, ids = zip(*[ops.head_candidates(h, w[bounds[r]:bounds[r + 1]].contiguous(), bounds[r],
                                           64) for r in range(N)])
@@ -766,12 +828,53 @@ def test_head_candidates_native_matches_reference(gpu):
     h = rnd(19, 256, dev=gpu)
     w = rnd(3000, 256, dev=gpu, scale=0.1)
     v, i = ops.head_candidates(h, w, 5000, 64)
-    lg = ops.linear(h, w, epi="f32")                   # same logits the op ranks
-    rv, ri = torch.topk(lg, 64, dim=-1)
+    lg = ops.linear(h, w, epi=ops.HEAD_EPI).float()    # same logits the op ranks
+    # ties (frequent in bf16) go to the lower token id: a stable descending sort
+    rv, ri = torch.sort(lg, dim=-1, descending=True, stable=True)
+    rv, ri = rv[:, :64], ri[:, :64]
     ri, perm = torch.sort((ri + 5000).to(torch.int32), dim=-1)
     assert torch.equal(i, ri)
     assert torch.equal(v, rv.gather(1, perm))
-    close(v, R.linear(h, w, out_dtype=torch.float32).gather(1, (i - 5000).long()))
+    close(v, R.linear(h, w, out_dtype=torch.float32).gather(1, (i - 5000).long()),
+          rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("B,V", [(512, 128256), (7, 32000), (3, 50257), (64, 1000)])
+def test_sampler_bf16_logits_equal_fp32_upcast(gpu, B, V):
+    """The sampler reads bf16 logits (the LM head in the model dtype, as HF's
+    ``lm_head(h).float()``) and compares their exact fp32 values: every token equals
+    sampling the fp32 upcast of the same logits — greedy, top-k/top-p, plain temperature,
+    the one- and the two-phase (small-batch) paths."""
+    torch.manual_seed(22)
+    lg = (torch.randn(B, V, device=gpu) * 3).to(BF)
+    temp = torch.full((B,), 0.8, device=gpu)
+    topk = torch.full((B,), 50, device=gpu, dtype=torch.int32)
+    topp = torch.full((B,), 0.95, device=gpu)
+    topk[1::5] = 1                                            # greedy rows
+    topk[2::5] = 0                                            # top-p over the whole row
+    temp[3::5] = 0.0                                          # greedy by temperature
+    topp[4::5] = 1.0
+    seeds = torch.arange(B, device=gpu, dtype=torch.int64) * 104729 + 3
+    a = ops.sample(lg, temp, topk, topp, seeds)
+    b = ops.sample(lg.float(), temp, topk, topp, seeds)
+    assert torch.equal(a, b)
+
+
+def test_topk_rows_bf16(gpu):
+    from distributed_llm_inferencing_amd.ops import _native
+    torch.manual_seed(5)
+    S, V, c = 11, 16000, 64
+    x = (torch.randn(S, V, device=gpu)).to(BF)               # bf16: many ties
+    st = torch.cuda.current_stream().cuda_stream
+    out = []
+    for t in (x, x.float()):
+        v = torch.empty(S, c, device=gpu)
+        i = torch.empty(S, c, dtype=torch.int32, device=gpu)
+        fn = "dli_topk_rows_bf16" if t.dtype == BF else "dli_topk_rows"
+        _native.call(fn, v.data_ptr(), i.data_ptr(), t.data_ptr(), t.stride(0), S, V, c, 7, st)
+        out.append((v, i))
+    torch.cuda.synchronize()
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
 
 
 def test_ep_pack_and_combine(gpu):

@@ -272,8 +272,8 @@ def test_decode_core_matches_python_scheduler():
 
 
 def test_prefill_gemm_plan_is_own_kernel(monkeypatch):
-    """Prefill-sized GEMMs plan onto the 8-phase MFMA kernel (tile 22), never hipBLASLt,
-    unless the ablation switch asks for the library."""
+    """Prefill-sized GEMMs plan onto the 8-phase MFMA kernel (tile 22); every plan the
+    planner or the autotune can produce is one of our kernels (no library backend left)."""
     from distributed_llm_inferencing_amd.ops import gemm as G
     G.clear_plans()
     for epi in ("none", "silu_mul", "splitk", "f32"):
@@ -305,25 +305,22 @@ def test_prefill_gemm_plan_is_own_kernel(monkeypatch):
     assert not any(p.tile == 29 for p in G.candidate_plans(1, 4096, 4096, "splitk"))
     assert not any(p.tile == 29 for p in G.candidate_plans(8, 28672, 4096, "silu_mul"))
     G.clear_plans()
-    monkeypatch.setenv("DLI_GEMM_PREFILL_BLAS", "1")
-    assert G.plan(16384, 6144, 4096, "none").backend == "hipblaslt"
-    assert G.plan(16384, 28672, 4096, "silu_mul").backend == "dli"
-    G.clear_plans()
-    monkeypatch.delenv("DLI_GEMM_PREFILL_BLAS")
-    # prefill autotune (StageRunner.autotune_prefill): our 8-phase plan vs our 4-wave deep-W
-    # plan at the same split; hipBLASLt only when DLI_TUNE_PREFILL_BLAS=1 asks for it
+    # prefill autotune (StageRunner.autotune_prefill): our 8-phase plan vs our 4-wave plan at
+    # the same split
     c = G.prefill_candidates(16384, 28672, 4096, "silu_mul")
     t4 = G.PREFILL_4W_TILE
     assert c == [G.GemmPlan("dli", 22, 1), G.GemmPlan("dli", t4, 1)]
     assert G.prefill_candidates(2048, 4096, 4096, "splitk") == \
         [G.GemmPlan("dli", 22, 2), G.GemmPlan("dli", t4, 2)]
     assert all(p.backend == "dli" for p in G.prefill_candidates(4096, 4096, 4096, "bias_gelu"))
-    monkeypatch.setenv("DLI_TUNE_PREFILL_BLAS", "1")
-    assert [p.backend for p in G.prefill_candidates(16384, 6144, 4096, "none")] == \
-        ["dli", "dli", "hipblaslt"]
-    monkeypatch.setenv("DLI_GEMM_NO_BLAS", "1")
+    for env in ("DLI_TUNE_PREFILL_LIB", "DLI_GEMM_PREFILL_LIB", "DLI_GEMM_DECODE_LIB"):
+        monkeypatch.setenv(env, "1")             # no switch reaches a library backend
+    monkeypatch.setenv("DLI_GEMM_BACKEND", "library")
+    G.clear_plans()
+    assert G.plan(16384, 6144, 4096, "none") == G.GemmPlan("dli", 22, 1)
     assert [p.backend for p in G.prefill_candidates(16384, 6144, 4096, "none")] == ["dli", "dli"]
-    monkeypatch.delenv("DLI_TUNE_PREFILL_BLAS")
+    assert all(p.backend == "dli" for p in G.candidate_plans(512, 4096, 4096, "splitk"))
+    G.clear_plans()
     # the 4-wave tiles stay out of the decode autotune (tile 41 cost the step 1.8 %)
     tiles = {p.tile for p in G.candidate_plans(512, 4096, 4096, "none")}
     assert not tiles & {41, 45} and 34 in tiles
