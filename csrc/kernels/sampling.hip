@@ -400,18 +400,42 @@ __global__ void __launch_bounds__(SMP_THREADS) sample_kernel(
     pmask |= 255u << shift;
     if (above_total + s_sel[2] <= SMP_CAP) break;
   }
-  // ---- gather everything at or above the boundary bin
+  // ---- gather everything at or above the boundary bin. When that is more than SMP_CAP
+  // (the 4 passes ran out: prefix is the exact CAP-th key, and its ties overflow), keep every
+  // key strictly above it and the lowest-index ties: a deterministic set, whatever the order
+  // of the atomics below (bf16 logits tie often)
+  const bool overflow_ties = above_total + s_sel[2] > SMP_CAP;
   if (tid == 0) s_cnt = 0;
   __syncthreads();
   scan(V, [&](float v, int i) {
     const uint32_t k = f2key(v);
-    if ((k & pmask) >= prefix) {
+    if (overflow_ties ? k > prefix : (k & pmask) >= prefix) {
       const uint32_t pos = atomicAdd(&s_cnt, 1u);
       if (pos < SMP_CAP) { ckey[pos] = k; cidx[pos] = i; }
     }
   });
   __syncthreads();
   n = (int)min(s_cnt, (uint32_t)SMP_CAP);
+  if (overflow_ties) {
+    // ordered compaction of the ties over contiguous per-thread slices of the row
+    const uint32_t need = (uint32_t)SMP_CAP - (uint32_t)n;
+    const int per = (V + SMP_THREADS - 1) / SMP_THREADS;
+    const int lo = min(V, tid * per), hi = min(V, lo + per);
+    auto val = [&](int e) { return xc != nullptr ? xc[e] : ldv(xl, e); };
+    uint32_t n_eq = 0;
+    for (int e = lo; e < hi; ++e) n_eq += f2key(val(e)) == prefix;
+    __syncthreads();                              // sv reuse by block_scan
+    uint32_t before = (uint32_t)block_scan((float)n_eq, sv) - n_eq;   // exact: < 2^24
+    for (int e = lo; e < hi && before < need; ++e) {
+      if (f2key(val(e)) == prefix) {
+        ckey[n + before] = prefix;
+        cidx[n + before] = e;
+        ++before;
+      }
+    }
+    __syncthreads();
+    n = SMP_CAP;
+  }
   }
   int npow = 1;
   while (npow < n) npow <<= 1;

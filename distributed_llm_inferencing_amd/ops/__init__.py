@@ -448,10 +448,13 @@ def _sample_ws(device, B: int, V: int):
     return ws
 
 
-# LM-head logits in the model dtype (bf16), as HF computes them (``lm_head(h)`` in the model's
-# dtype, then ``.float()``): half the bytes written by the head GEMM and read by the sampler.
-# DLI_FP32_LOGITS=1: the fp32-output head (the round-4 path), for A/B runs.
-HEAD_EPI = "f32" if os.environ.get("DLI_FP32_LOGITS", "0") == "1" else "none"
+# LM-head output dtype. Default fp32 (the head GEMM accumulates in fp32 and stores it).
+# DLI_BF16_LOGITS=1 stores the model dtype instead, as HF's ``lm_head(h).float()`` rounds it:
+# same-box A/B at batch 512 (profiles/r5/s05/ab.jsonl) gave no gain — the head GEMM is
+# MFMA-bound at the same 407 us either way and only the sampler got 20 us faster — while a
+# request's tokens then depend on which GEMM plan (batch size) computed its logits (one
+# bf16 rounding flip changes a draw), which breaks batch-invariant seeded sampling.
+HEAD_EPI = "none" if os.environ.get("DLI_BF16_LOGITS", "0") == "1" else "f32"
 
 
 def sample(logits, temperature, top_k, top_p, seeds, generator=None, ids=None):

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Session 5: same-box A/B of two decode-step knobs on the driver's bench (alternated x2):
+# Session 5: GPU kernel/engine/parallel tests, then a same-box A/B of decode-step knobs on the driver's bench (alternated x2):
 # sc1 (write-through) split-K slab stores for the generic-tile family (decode O / QKV), and
 # the 256x224 gate/up tile admitted to the autotune; then a rocprofv3 wave summary at HEAD
 # (summarised on the box: the raw trace exceeds what gpurun copies back).
@@ -11,11 +11,16 @@ run() { local arm=$1 r=$2; shift 2; timeout -k 10 240 env "$@" python3 bench.py 
         local rc=$?; echo "rc[$arm $r]=$rc"; [ $rc -eq 0 ] || { tail -20 $O/${arm}_$r.log; exit $rc; }
         echo "{\"arm\": \"$arm\", \"run\": $r, \"bench\": $(grep -h '^{"metric"' $O/${arm}_$r.log)}" >> $O/ab.jsonl
         grep -o '"value": [0-9.]*' $O/${arm}_$r.log; }
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_kernels_gpu.py tests/test_engine_gpu.py tests/test_parallel_gpu.py -k "not batch_invariant" > $O/tests.log 2>&1
+rc=$?; echo "rc[tests]=$rc"; tail -2 $O/tests.log; [ $rc -eq 0 ] || exit $rc
 for r in 1 2; do
   run base $r DLI_AB=0
+  run fp32_logits $r DLI_FP32_LOGITS=1
   run tiles_sc1 $r DLI_SLAB_STORE_TILES=2
   run t26 $r DLI_GEMM_EXCLUDE=27,41,45
 done
+timeout -k 10 300 python3 scripts/bench_moe_tiles.py --batch 512 --which down > $O/moe_down_b512.log 2>&1
+echo "rc[moe]=$?"
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o wave -- python3 bench.py --steps 1 --warmup 1 > $O/prof.log 2>&1
 rc=$?; echo "rc[prof]=$rc"; [ $rc -eq 0 ] || exit $rc
