@@ -23,7 +23,8 @@
 //
 // Files: gemm_common.h (shared epilogue / split-K pieces), gemm_tiles.hip (ids 0-21, 23-25),
 // gemm8p.hip (22, 26-28), gemm4w.h + gemm4w.hip (34, 41, 45), gemv.hip (29-33 and the fused
-// batch-1 combine); csrc/ab/gemm4w_variants.hip holds losing A/B variants (DLI_GEMM_AB=1).
+// batch-1 combine). The losing 4-wave A/B variants of round 4 are documented, not built
+// (profiles/r4/gemm4w/).
 #include "gemm_common.h"
 
 extern "C" int dli_gemm_set_slab_store(int mode) {
@@ -66,7 +67,5 @@ extern "C" int dli_gemm(const void* A, int lda, const void* W, int ldw, void* C,
   if (r == DLI_NOT_MINE) r = gemm_8p_dispatch(epi, tile_cfg, DLI_GEMM_PASS);
   if (r == DLI_NOT_MINE) r = gemm_4w_dispatch(epi, tile_cfg, DLI_GEMM_PASS);
   if (r == DLI_NOT_MINE) r = gemm_gemv_dispatch(epi, tile_cfg, DLI_GEMM_PASS);
-  if (r == DLI_NOT_MINE && dli_gemm4w_ab_dispatch != nullptr)
-    r = dli_gemm4w_ab_dispatch(epi, tile_cfg, DLI_GEMM_PASS);
   return r == DLI_NOT_MINE ? (int)hipErrorInvalidValue : r;
 }

@@ -1,6 +1,6 @@
 // The 4-wave 256x256 MFMA GEMM (gemm4w_kernel: one wave per SIMD, 128x128 wave tiles,
 // accumulators pinned in the AGPR file) and its launcher, shared by the production tiles
-// (gemm4w.hip: 34, 41, 45) and the A/B variants (csrc/ab/gemm4w_variants.hip, DLI_GEMM_AB=1).
+// (gemm4w.hip: 34, 41, 45).
 #pragma once
 #include "gemm_common.h"
 
@@ -48,8 +48,8 @@ __device__ __forceinline__ uint4 buf_ld16(const void* base, int nbytes, int voff
 // placements, 32768 = column-major MFMA order, 65536 = per-piece voffset addressing.
 // Diagnostics only: 64 = no LDS-DMA in the K loop, 128 = also no barrier / waits (wrong
 // results, timing of the remaining work), 131072 = s_memtime stamps (correct results).
-// Only tiles 34 (VAR 8), 41 (8 | 32) and 45 (8 | 4096) are built by default; the rest with
-// DLI_GEMM_AB=1 (measurements: profiles/r4/gemm4w/).
+// Only tiles 34 (VAR 8), 41 (8 | 32) and 45 (8 | 4096) are instantiated; the other VAR bits
+// are the round-4 A/B variants, kept for diagnostics (measurements: profiles/r4/gemm4w/).
 template <int EPI, int VAR = 0>
 __global__ void __launch_bounds__(256, 1) gemm4w_kernel(
     const u16* __restrict__ A, int lda, const u16* __restrict__ W, int ldw,

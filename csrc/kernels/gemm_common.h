@@ -227,9 +227,6 @@ int gemm_gemv_dispatch(int epi, int tile_cfg, DLI_GEMM_ARGS);
 int gemm_tiles_set_slab_store(int mode);
 int gemm_8p_set_slab_store(int mode);
 int gemm_4w_set_slab_store(int mode);
-// the losing 4-wave A/B variants (csrc/ab/gemm4w_variants.hip), linked only into builds with
-// DLI_GEMM_AB=1: a weak reference, null in the production library
-extern "C" int dli_gemm4w_ab_dispatch(int epi, int tile_cfg, DLI_GEMM_ARGS) __attribute__((weak));
 
 // EPI -> template argument, for a family's dispatch<EPI>(tile_cfg, ...)
 #define DLI_EPI_SWITCH(FN)                                                         \

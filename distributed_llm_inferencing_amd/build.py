@@ -51,9 +51,6 @@ def _hipcc() -> str:
 # -inf as the masked-score / running-max sentinel (poison under ninf -> NaNs).
 KERNEL_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-fno-gpu-rdc",
                 "-munsafe-fp-atomics", "-Wno-unused-result"]
-# DLI_GEMM_AB=1: also build the 4-wave GEMM's losing A/B variants (csrc/ab/, tiles 35-40,
-# 42-44, 46-53) into the kernel library; the production build never compiles them
-GEMM_AB = os.environ.get("DLI_GEMM_AB", "0") == "1"
 RUNTIME_FLAGS = ["-O2", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",
                  "-Wno-unused-result"]
 
@@ -123,11 +120,8 @@ def _link(objs, out: Path, extra=()):
 
 def _group_sources(kind: str):
     if kind == "kernels":
-        srcs = sorted((CSRC / "kernels").glob("*.hip"))
-        if GEMM_AB:
-            srcs += sorted((CSRC / "ab").glob("*.hip"))
-        return srcs, sorted((CSRC / "kernels").glob("*.h")), KERNEL_FLAGS + (
-            ["-DDLI_GEMM_AB_VARIANTS=1"] if GEMM_AB else [])
+        return (sorted((CSRC / "kernels").glob("*.hip")), sorted((CSRC / "kernels").glob("*.h")),
+                KERNEL_FLAGS)
     return (sorted((CSRC / "runtime").glob("*.cpp")), sorted((CSRC / "runtime").glob("*.h")),
             RUNTIME_FLAGS)
 

@@ -50,9 +50,8 @@ TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256), 4: (256, 128),
          # 256x256, 4 waves (one per SIMD), 128x128 wave tiles, accumulators pinned in the AGPR
          # file (gemm4w_kernel); 41 = 34 with a 3-stage weight ring (160 KiB LDS: W fetched a
          # K-tile further ahead); 45 = 34 with two barriers per K-tile (the buffer released
-         # after 20 MFMAs, the next-next K-tile's DMA over 80 MFMAs). A/B variants 35-40 and
-         # 42-44 / 49-53 are built only with DLI_GEMM_AB=1 (build.py) and never planned
-         # (profiles/r4/gemm4w/)
+         # after 20 MFMAs, the next-next K-tile's DMA over 80 MFMAs). The losing A/B variants
+         # 35-40 / 42-44 / 46-53 are not instantiated (profiles/r4/gemm4w/)
          34: (256, 256), 41: (256, 256), 45: (256, 256)}
 # the 4-wave plan raced against the 8-phase one in the prefill autotune
 PREFILL_4W_TILE = int(os.environ.get("DLI_GEMM_PREFILL_4W", "45"))
