@@ -21,4 +21,5 @@ for r in 1 2; do
   run overlap $r DLI_DECODE_OVERLAP=1
 done
 run sc1_8p 1 DLI_SLAB_STORE_8P=2
+run head45 1 DLI_GEMM_HEAD_4W=1
 exit 0

@@ -389,3 +389,25 @@ def test_gemm_workspace_growth_keeps_the_replaced_buffer_alive():
             G._workspaces[key] = saved
         else:
             G._workspaces.pop(key, None)
+
+
+def test_autotune_final_round_picks_the_lowest_median():
+    """ops.gemm._final_round: finalists within the band are re-timed round-robin and the lowest
+    median wins, so one lucky first-pass sample cannot pin a plan."""
+    from distributed_llm_inferencing_amd.ops import gemm as G
+    seq = {"a": iter([1.30, 1.30, 1.30]), "b": iter([1.00, 1.01, 0.99]),
+           "c": iter([5.0, 5.0, 5.0])}
+
+    class FakeOps:
+        @staticmethod
+        def benchmark(run, iters, warmup, graph):
+            return next(seq[run()])
+    plans = {k: G.GemmPlan("dli", i, 1) for i, k in enumerate("abc")}
+    # first pass: "a" got a lucky 0.97 ms, "b" 1.02, "c" far outside the band
+    timed = [(0.97, plans["a"], lambda: "a"), (1.02, plans["b"], lambda: "b"),
+             (1.5, plans["c"], lambda: "c")]
+    best = G._final_round(FakeOps, timed, iters=3, n_copies=1)
+    assert best[0] == plans["b"] and abs(best[1] - 1.01) < 1e-9     # median of 4 samples
+    assert G._final_round(FakeOps, [], 3, 1) is None
+    one = [(2.0, plans["c"], lambda: "c")]
+    assert G._final_round(FakeOps, one, 3, 1) == (plans["c"], 2.0)
