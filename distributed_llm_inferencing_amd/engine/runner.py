@@ -238,15 +238,8 @@ class StageRunner:
         m = self.model
         moe = (m.cfg.is_moe and m.layers and m.layers[0].get("w_gu") is not None
                and m.layers[0]["w_gu"].dim() == 3)
-        from ..models import model as MM
         for b in (buckets or self.buckets):
             shapes, weights = self.gemm_shapes(b)
-            lp = m.layers[0] if m.layers else {}
-            if (MM.OVERLAP and b >= MM.OVERLAP_MIN and m.cfg.arch != "gpt2"
-                    and lp.get("wqkv") is not None and lp.get("wo") is not None):
-                # the overlapped attention block runs its QKV / O GEMMs on half batches
-                qo = (tuple(lp["wqkv"].shape), tuple(lp["wo"].shape))
-                shapes = [s for s in self.gemm_shapes(b // 2)[0] if (s[1], s[2]) in qo] + shapes
             c = m.cfg
             qkv = ((c.num_heads, c.num_kv_heads, c.head_dim) if c.arch != "gpt2" else None)
             G.autotune(shapes, weights, self.device, log=log, qkv_heads=qkv)

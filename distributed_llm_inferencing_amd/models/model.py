@@ -17,21 +17,15 @@ expert-parallel all-to-all implementation installed by ``parallel/expert.py``).
 from __future__ import annotations
 
 import math
-import os
 from typing import Callable, Dict, List, Optional, Tuple
 
 import torch
 
 from .. import ops
 from ..engine.batch import DeviceBatch
-from ..ops import gemm as G
 from ..ops import reference as R
 from .configs import ModelConfig
 from . import weights as W
-
-# decode attention block as two overlapped half batches (TransformerLM._attn_block_overlapped)
-OVERLAP = os.environ.get("DLI_DECODE_OVERLAP", "0") == "1"
-OVERLAP_MIN = int(os.environ.get("DLI_OVERLAP_MIN", "256"))
 
 
 class TransformerLM:
@@ -152,15 +146,6 @@ class TransformerLM:
                 h = ops.add_rmsnorm(pending, residual, lp["attn_norm"], eps)
                 pending = None
             attn = None
-            if not b.is_prefill and self._overlap_ok(h, lp, b, kc):
-                h = self._attn_block_overlapped(h, lp, b, kc, vc, residual, eps)
-                if cfg.is_moe:
-                    pending = self.moe_fn(h, lp, self.layer_start + li)
-                    continue
-                act = ops.linear(h, lp["w_gu"], epi="silu_mul")
-                nxt = self.layers[li + 1]["attn_norm"] if li + 1 < n else None
-                h = self._proj_add_norm(act, lp["w_down"], residual, nxt, eps)
-                continue
             if not b.is_prefill:             # decode: reduce + RoPE + KV write + attention fused
                 attn = ops.linear_rope_attention(h, lp["wqkv"], b.positions, b.slot_mapping,
                                                  self.cos_sin, kc, vc, b.block_tables,
@@ -181,59 +166,6 @@ class TransformerLM:
         if pending is not None:
             residual.add_(pending)
         return residual
-
-    def _overlap_ok(self, h, lp, b: DeviceBatch, kc) -> bool:
-        """Decode batches of >= OVERLAP_MIN rows run the attention block as two half batches
-        on two streams (``_attn_block_overlapped``) where both halves take the fused
-        attention kernel."""
-        B = h.shape[0]
-        if (not OVERLAP or B < OVERLAP_MIN or self.tp_reduce is not None or not h.is_cuda
-                or kc is None):
-            return False
-        c = self.cfg
-        half = h[: B // 2]
-        return (ops.fused_attention_ok(half, lp["wqkv"], kc, b.max_context, c.num_kv_heads,
-                                       c.head_dim)
-                and ops.fused_attention_ok(h[B // 2:], lp["wqkv"], kc, b.max_context,
-                                           c.num_kv_heads, c.head_dim))
-
-    def _attn_block_overlapped(self, h, lp, b: DeviceBatch, kc, vc, residual, eps):
-        """QKV GEMM -> fused RoPE/KV/attention -> O GEMM -> add + RMSNorm for a decode batch
-        as two half batches on two streams, the second started once the first's QKV GEMM
-        is enqueued-and-done: half A's attention (HBM-bound) then runs beside half B's QKV
-        GEMM (MFMA-bound), A's O projection beside B's attention. Rows are independent, so
-        each half's output equals the whole batch's rows under the half's GEMM plans. The
-        second stream uses its own split-K scratch (``ops.gemm.ws_slot``); both join before
-        the MLP. Captured into the decode hipGraph as a fork / join."""
-        c = self.cfg
-        B = h.shape[0]
-        hb = B // 2
-        cur = torch.cuda.current_stream(h.device)
-        side = self._side_stream(h.device)
-        out = torch.empty_like(h)
-        ev = torch.cuda.Event()
-
-        def part(lo, hi, mid=None):
-            a = ops.linear_rope_attention(
-                h[lo:hi], lp["wqkv"], b.positions[lo:hi], b.slot_mapping[lo:hi], self.cos_sin,
-                kc, vc, b.block_tables[lo:hi], b.context_lens[lo:hi], b.max_context,
-                c.num_heads, c.num_kv_heads, c.head_dim, self.scale, mid=mid)
-            ops.linear_add_rmsnorm(a, lp["wo"], residual[lo:hi], lp["mlp_norm"], eps,
-                                   out=out[lo:hi])
-
-        side.wait_stream(cur)
-        part(0, hb, mid=lambda: ev.record(cur))
-        with torch.cuda.stream(side), G.ws_slot(1):
-            side.wait_event(ev)
-            part(hb, B)
-        cur.wait_stream(side)
-        return out
-
-    def _side_stream(self, device):
-        s = getattr(self, "_side", None)
-        if s is None:
-            s = self._side = torch.cuda.Stream(device)
-        return s
 
     def _proj_add_norm(self, x, w, residual, norm_w, eps):
         if self.tp_reduce is None:

@@ -156,12 +156,10 @@ def _splitk_plan(x, w):
     return p if p.splits > 1 else None
 
 
-def linear_add_rmsnorm(x, w, residual, norm_w, eps, plan: Optional[G.GemmPlan] = None,
-                       out=None):
+def linear_add_rmsnorm(x, w, residual, norm_w, eps, plan: Optional[G.GemmPlan] = None):
     """residual += x @ w.T (bf16-rounded, in place); returns rmsnorm(residual) * norm_w
-    (None when norm_w is None), written into ``out`` when given (a contiguous row block).
-    Split-K GEMMs reduce their partial slabs inside the norm kernel (fused_reduce.hip), so
-    the bf16 GEMM output is never materialised.
+    (None when norm_w is None). Split-K GEMMs reduce their partial slabs inside the norm
+    kernel (fused_reduce.hip), so the bf16 GEMM output is never materialised.
     ``plan`` forces the GEMM plan (the autotuner times every candidate with its consumer)."""
     if plan is None:
         p = _splitk_plan(x, w)
@@ -172,18 +170,11 @@ def linear_add_rmsnorm(x, w, residual, norm_w, eps, plan: Optional[G.GemmPlan] =
         if norm_w is None:
             residual.add_(y)             # bf16 add computes in fp32 and rounds once
             return None
-        r = add_rmsnorm(y, residual, norm_w, eps)
-        if out is not None:
-            out.copy_(r)
-            return out
-        return r
+        return add_rmsnorm(y, residual, norm_w, eps)
     M, K = x.shape
     Nn = w.shape[0]
     ws = G.workspace(x.device, p.splits * M * Nn * 4)
-    if norm_w is None:
-        out = None
-    elif out is None:
-        out = torch.empty_like(residual)
+    out = torch.empty_like(residual) if norm_w is not None else None
     if (p.tile in G.GEMV_FUSED_NORM_TILES and M <= G.GEMV_MAX_M and p.splits in (2, 4, 8)
             and residual.is_contiguous() and _FUSED_GEMV_NORM):
         # batch-1 decode: the split-K combine + residual add + RMSNorm run inside the GEMV's
@@ -225,38 +216,27 @@ def linear_rope_cache(x, w, positions, slot_mapping, cos_sin, k_cache, v_cache, 
     return qkv
 
 
-def fused_attention_ok(x, w, k_cache, max_context: int, hkv, hd) -> bool:
-    """True where ``linear_rope_attention`` runs its fused kernel for these rows (else it
-    returns None without launching anything): see its docstring."""
-    if (os.environ.get("DLI_FUSED_ROPE_ATTN", "1") != "1" or hd != 128 or k_cache is None
-            or not _use_native(x)):
-        return False
-    p = _splitk_plan(x, w)
-    if p is not None and p.splits not in (2, 4):
-        return False
-    if decode_num_splits(x.shape[0], hkv, max_context) != 1:
-        return False
-    mode = int(N.require_native().dli_decode_get_pipe())
-    # the pipelined long-context kernel (dli_decode_attention) is not fused
-    return not (mode == 1 or (mode == 2 and -(-max_context // 32) * 32 >= 768))
-
-
 def linear_rope_attention(x, w, positions, slot_mapping, cos_sin, k_cache, v_cache,
-                          block_tables, context_lens, max_context: int, hq, hkv, hd, scale,
-                          mid=None):
+                          block_tables, context_lens, max_context: int, hq, hkv, hd, scale):
     """Decode step, one fused pass after the QKV GEMM: the split-K slabs (or, for an unsplit
     plan, the bf16 QKV rows) are reduced, q and k rotated, k/v written to the paged cache and
     attention computed by ONE kernel per layer (``dli_decode_attention_fused``) instead of
     ``linear_rope_cache`` + ``decode_attention``. Returns the attention output [B, hq*hd], or
     None where the fused kernel does not apply (the caller then runs the two-kernel path):
     split counts other than 2 / 4, KV-split attention (long contexts at small batch), the
-    pipelined long-context kernel, head dim != 128. ``DLI_FUSED_ROPE_ATTN=0`` turns it off.
-    ``mid()`` is called between the GEMM's launch and the attention kernel's (the overlapped
-    decode block records its fork event there)."""
-    if not fused_attention_ok(x, w, k_cache, max_context, hkv, hd):
+    pipelined long-context kernel, head dim != 128. ``DLI_FUSED_ROPE_ATTN=0`` turns it off."""
+    if (os.environ.get("DLI_FUSED_ROPE_ATTN", "1") != "1" or hd != 128 or k_cache is None
+            or not _use_native(x)):
         return None
     p = _splitk_plan(x, w)
+    if p is not None and p.splits not in (2, 4):
+        return None
     B, K = x.shape
+    if decode_num_splits(B, hkv, max_context) != 1:
+        return None
+    mode = int(N.require_native().dli_decode_get_pipe())
+    if mode == 1 or (mode == 2 and -(-max_context // 32) * 32 >= 768):
+        return None                       # dli_decode_attention picks the pipelined kernel
     Nn = w.shape[0]
     if p is None:                         # unsplit plan: the prologue reads the bf16 rows
         src, splits = linear(x, w), 0
@@ -264,8 +244,6 @@ def linear_rope_attention(x, w, positions, slot_mapping, cos_sin, k_cache, v_cac
         src, splits = G.workspace(x.device, p.splits * B * Nn * 4), p.splits
         _native_call("dli_gemm", _p(x), x.stride(0), _p(w), w.stride(-2), None, Nn, B, Nn, K,
                      0, p.tile, p.splits, None, _p(src), None, 1, _st())
-    if mid is not None:
-        mid()
     out = torch.empty(B, hq * hd, dtype=x.dtype, device=x.device)
     _native_call("dli_decode_attention_fused", _p(out), _p(src), splits, _p(positions),
                  _p(slot_mapping), _p(cos_sin), _p(k_cache), _p(v_cache), _p(block_tables),

@@ -130,29 +130,9 @@ def tickets(device: torch.device, n: int, stream: int = 0) -> torch.Tensor:
         return t
 
 
-_slot = threading.local()
-
-
-class ws_slot:
-    """Route ``workspace()`` calls of this thread to scratch slot ``n`` while the block runs:
-    work enqueued on a second stream that may run concurrently with the first (the decode
-    step's overlapped half batch, models/model.py) must not share split-K slabs with it."""
-
-    def __init__(self, n: int):
-        self.n = n
-
-    def __enter__(self):
-        self.old = getattr(_slot, "v", 0)
-        _slot.v = self.n
-
-    def __exit__(self, *exc):
-        _slot.v = self.old
-
-
 def workspace(device: torch.device, nbytes: int) -> torch.Tensor:
-    """Grow-only scratch (bytes) per device and slot (``ws_slot``). Never freed: see
-    ``_retired``."""
-    key = (device.type, device.index, getattr(_slot, "v", 0))
+    """Grow-only scratch (bytes) per device. Never freed: see ``_retired``."""
+    key = (device.type, device.index)
     with _ws_lock:
         ws = _workspaces.get(key)
         if ws is None or ws.numel() < nbytes:

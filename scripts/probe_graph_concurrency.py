@@ -14,10 +14,12 @@ def main():
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
     cyc = 20_000_000                       # ~10 ms at ~2 GHz
-    main_s = torch.cuda.current_stream()
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
 
     def branches():
+        # fork from the stream current at call time: inside torch.cuda.graph that is the
+        # capture stream (forking from the default stream left the graph empty)
+        main_s = torch.cuda.current_stream()
         s1.wait_stream(main_s)
         s2.wait_stream(main_s)
         with torch.cuda.stream(s1):

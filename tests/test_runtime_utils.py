@@ -370,7 +370,7 @@ def test_gemm_workspace_growth_keeps_the_replaced_buffer_alive():
     the decode graphs are captured), so the old buffer must never return to the allocator."""
     from distributed_llm_inferencing_amd.ops import gemm as G
     dev = torch.device("cpu")
-    key = (dev.type, dev.index, 0)
+    key = (dev.type, dev.index)
     saved, n_ret = G._workspaces.pop(key, None), len(G._retired)
     try:
         small = G.workspace(dev, 1024)
@@ -379,11 +379,7 @@ def test_gemm_workspace_growth_keeps_the_replaced_buffer_alive():
         big = G.workspace(dev, small.numel() + 1)
         assert big is not small and big.numel() > small.numel()
         assert any(t.data_ptr() == ptr for t in G._retired[n_ret:])
-        with G.ws_slot(1):                                    # a second stream's slot
-            other = G.workspace(dev, 256)
-        assert other.data_ptr() != big.data_ptr() and G.workspace(dev, 256) is big
     finally:
-        G._workspaces.pop((dev.type, dev.index, 1), None)
         del G._retired[n_ret:]
         if saved is not None:
             G._workspaces[key] = saved
