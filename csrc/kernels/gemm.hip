@@ -22,7 +22,8 @@
 // gate/up weight (output width N/2), 3 bias + tanh-GELU, 4 bias.
 //
 // Files: gemm_common.h (shared epilogue / split-K pieces), gemm_tiles.hip (ids 0-21, 23-25),
-// gemm8p.hip (22, 26-28), gemm4w.h + gemm4w.hip (34, 41, 45), gemv.hip (29-33 and the fused
+// gemm8p.hip (22, 26-28), gemm4w.h + gemm4w.hip (34, 41, 45), gemm4wp.hip (55: persistent
+// 45), gemv.hip (29-33 and the fused
 // batch-1 combine). The losing 4-wave A/B variants of round 4 are documented, not built
 // (profiles/r4/gemm4w/).
 #include "gemm_common.h"
@@ -51,7 +52,8 @@ extern "C" int dli_gemm_set_slab_store_family(int family, int mode) {
 // 256x256, 256x128, 128x256 (2 stages) and 256x128, 128x256 (3 stages); 18/19 = 128x96 and
 // 20/21 = 128x64 with 2/3 stages; 22 = 256x256 8-phase ping-pong; 23/24 = 128x192 (3/2
 // stages), 25 = 256x192, 8 waves; 26 = 256x224 ping-pong; 29-33 = the M <= 4 weight
-// stream (16 / 32 rows per workgroup, dispatch_gemv). ws: fp32 [splits, M, N] when splits>1.
+// stream (16 / 32 rows per workgroup, dispatch_gemv); 55 = tile 45 persistent (one workgroup
+// per CU walks its tiles, no split-K / grouped mode). ws: fp32 [splits, M, N] when splits>1.
 // group_off (nullable): int[groups+1] row offsets; M is then the max rows of any group.
 extern "C" int dli_gemm(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M,
                         int N, int K, int epi, int tile_cfg, int splits, const void* bias,
@@ -66,6 +68,7 @@ extern "C" int dli_gemm(const void* A, int lda, const void* W, int ldw, void* C,
   int r = gemm_tiles_dispatch(epi, tile_cfg, DLI_GEMM_PASS);
   if (r == DLI_NOT_MINE) r = gemm_8p_dispatch(epi, tile_cfg, DLI_GEMM_PASS);
   if (r == DLI_NOT_MINE) r = gemm_4w_dispatch(epi, tile_cfg, DLI_GEMM_PASS);
+  if (r == DLI_NOT_MINE) r = gemm_4wp_dispatch(epi, tile_cfg, DLI_GEMM_PASS);
   if (r == DLI_NOT_MINE) r = gemm_gemv_dispatch(epi, tile_cfg, DLI_GEMM_PASS);
   return r == DLI_NOT_MINE ? (int)hipErrorInvalidValue : r;
 }

@@ -223,6 +223,7 @@ constexpr int DLI_NOT_MINE = -0x4d494e45;
 int gemm_tiles_dispatch(int epi, int tile_cfg, DLI_GEMM_ARGS);
 int gemm_8p_dispatch(int epi, int tile_cfg, DLI_GEMM_ARGS);
 int gemm_4w_dispatch(int epi, int tile_cfg, DLI_GEMM_ARGS);
+int gemm_4wp_dispatch(int epi, int tile_cfg, DLI_GEMM_ARGS);
 int gemm_gemv_dispatch(int epi, int tile_cfg, DLI_GEMM_ARGS);
 int gemm_tiles_set_slab_store(int mode);
 int gemm_8p_set_slab_store(int mode);

@@ -52,9 +52,14 @@ TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256), 4: (256, 128),
          # K-tile further ahead); 45 = 34 with two barriers per K-tile (the buffer released
          # after 20 MFMAs, the next-next K-tile's DMA over 80 MFMAs). The losing A/B variants
          # 35-40 / 42-44 / 46-53 are not instantiated (profiles/r4/gemm4w/)
-         34: (256, 256), 41: (256, 256), 45: (256, 256)}
+         34: (256, 256), 41: (256, 256), 45: (256, 256),
+         # 55 = 45 persistent: one workgroup per CU walks its tiles, the next tile's first two
+         # K-tiles staged in the current tile's last two (gemm4wp.hip); no split-K / grouped
+         55: (256, 256)}
 # the 4-wave plan raced against the 8-phase one in the prefill autotune
 PREFILL_4W_TILE = int(os.environ.get("DLI_GEMM_PREFILL_4W", "45"))
+# the persistent 4-wave tile (55) raced too (DLI_GEMM_PREFILL_PERSIST=0: not a candidate)
+PREFILL_PERSIST = os.environ.get("DLI_GEMM_PREFILL_PERSIST", "1") == "1"
 # prefill-sized grouped expert GEMMs (ops.moe_mlp's eager path): Mixtral 8x7B at 32k routed
 # rows, tile 45 vs the 8-phase tile 22: down 2,895 vs 3,071-3,239 us, gate/up 5,736 vs
 # 5,898 us (profiles/r4/moe/)
@@ -468,6 +473,8 @@ def prefill_candidates(M: int, N: int, K: int, epi: str):
     base = out[0]
     if base.tile == 22 and PREFILL_4W_TILE > 0:
         out.append(GemmPlan("dli", PREFILL_4W_TILE, base.splits))
+    if base.tile == 22 and base.splits == 1 and K % 128 == 0 and PREFILL_PERSIST:
+        out.append(GemmPlan("dli", 55, 1))
     return out
 
 
@@ -482,7 +489,7 @@ def candidate_plans(M: int, N: int, K: int, epi: str):
     # isolated decode timings (M = 512 LM head 4-7 %) but cost the step 1.8 % in a same-box
     # bench A/B (42,548 without vs 41,790 / 41,653 tok/s with, profiles/r4/bench/)
     excl_env = os.environ.get("DLI_GEMM_EXCLUDE")
-    excl = {int(t) for t in (excl_env if excl_env is not None else "26,27,41,45").split(",")
+    excl = {int(t) for t in (excl_env if excl_env is not None else "26,27,41,45,55").split(",")
             if t.strip()}
     # ... except where 256x256 tiles take more than one wave of the chip and 256x224 tiles
     # land on a whole number of waves (Llama-3-70B gate/up at M = 512: N = 57344 is 448
@@ -497,6 +504,7 @@ def candidate_plans(M: int, N: int, K: int, epi: str):
     # head (several waves of 256x256 tiles), where it ran 3-7 % faster in isolation
     if excl_env is None and epi == "f32" and os.environ.get("DLI_GEMM_HEAD_4W", "0") == "1":
         excl.discard(45)
+        excl.discard(55)
     for tile, (bm, bn) in TILES.items():
         if not tile_ok(tile, epi) or tile in excl:
             continue

@@ -99,6 +99,45 @@ def test_gemm_256x224_pingpong(gpu, M, N, K, epi, tile):
         close(out, ref, rtol=2e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("M,N,K,epi", [(2048, 6144, 4096, "none"), (4096, 4096, 4096, "none"),
+                                       (8192, 28672, 4096, "silu_mul"),
+                                       (16384, 4096, 14336, "none"), (512, 28672, 4096, "silu_mul"),
+                                       (1100, 4096, 14336, "none"), (777, 50257, 4096, "f32"),
+                                       (300, 2304, 768, "bias_gelu")])
+def test_gemm_4wave_persistent(gpu, M, N, K, epi):
+    """Tile 55: the two-barrier 4-wave kernel as a persistent grid (one workgroup per CU walks
+    tiles; the next tile's first K-tiles are staged in the current tile's last two). Shapes
+    with one tile per workgroup (M = 2048 QKV: 192 tiles), many (gate/up at 8192: 3,584
+    tiles, 14 per workgroup), partial row / column tiles and every epilogue, against the fp32
+    reference; bitwise equal to tile 45 (same K order per output); odd K-tile counts and
+    split-K are refused."""
+    torch.manual_seed(11)
+    x, w = rnd(M, K, dev=gpu), rnd(N, K, dev=gpu, scale=0.05)
+    bias = rnd(N, dev=gpu) if epi == "bias_gelu" else None
+    if epi == "silu_mul":
+        ref = R.silu_mul(R.linear(x, w).float().to(BF))
+    elif epi == "bias_gelu":
+        ref = R.gelu_tanh(R.linear(x, w).float() + bias.float())
+    else:
+        ref = R.linear(x, w, out_dtype=torch.float32)
+    t45 = ops._gemm_native(x, w, epi, plan=G.GemmPlan("dli", 45, 1), bias=bias)
+    for rep in range(3):
+        out = ops._gemm_native(x, w, epi, plan=G.GemmPlan("dli", 55, 1), bias=bias)
+        err = (out.float() - ref.float()).abs()
+        bad = err > 2e-2 + 2e-2 * ref.float().abs().max()
+        assert not bool(bad.any()), (
+            f"rep {rep}: {int(bad.sum())} bad elements, rows "
+            f"{torch.unique(torch.nonzero(bad)[:, 0])[:16].tolist()}, cols "
+            f"{torch.unique(torch.nonzero(bad)[:, 1])[:16].tolist()}, max {float(err.max())}")
+        assert torch.equal(out, t45)
+    with pytest.raises(Exception):
+        ops._gemm_native(x, w, epi, plan=G.GemmPlan("dli", 55, 2), bias=bias)
+    if K % 128 == 0:
+        x2, w2 = x[:, :K - 64].contiguous(), w[:, :K - 64].contiguous()   # odd K-tile count
+        with pytest.raises(Exception):
+            ops._gemm_native(x2, w2, epi, plan=G.GemmPlan("dli", 55, 1), bias=bias)
+
+
 @pytest.mark.parametrize("tile", [int(t) for t in os.environ.get("DLI_TEST_4W_TILES",
                                                                   "34,41,45").split(",")])
 @pytest.mark.parametrize("M,N,K,epi", [(2048, 6144, 4096, "none"), (4096, 4096, 4096, "none"),

@@ -307,23 +307,25 @@ def test_prefill_gemm_plan_is_own_kernel(monkeypatch):
     G.clear_plans()
     # prefill autotune (StageRunner.autotune_prefill): our 8-phase plan vs our 4-wave plan at
     # the same split
+    # (and the persistent 4-wave tile 55 where the plan is unsplit and K an even K-tile count)
     c = G.prefill_candidates(16384, 28672, 4096, "silu_mul")
     t4 = G.PREFILL_4W_TILE
-    assert c == [G.GemmPlan("dli", 22, 1), G.GemmPlan("dli", t4, 1)]
+    assert c == [G.GemmPlan("dli", 22, 1), G.GemmPlan("dli", t4, 1), G.GemmPlan("dli", 55, 1)]
     assert G.prefill_candidates(2048, 4096, 4096, "splitk") == \
         [G.GemmPlan("dli", 22, 2), G.GemmPlan("dli", t4, 2)]
+    assert G.GemmPlan("dli", 55, 1) not in G.prefill_candidates(16384, 4096, 4160, "none")
     assert all(p.backend == "dli" for p in G.prefill_candidates(4096, 4096, 4096, "bias_gelu"))
     for env in ("DLI_TUNE_PREFILL_LIB", "DLI_GEMM_PREFILL_LIB", "DLI_GEMM_DECODE_LIB"):
         monkeypatch.setenv(env, "1")             # no switch reaches a library backend
     monkeypatch.setenv("DLI_GEMM_BACKEND", "library")
     G.clear_plans()
     assert G.plan(16384, 6144, 4096, "none") == G.GemmPlan("dli", 22, 1)
-    assert [p.backend for p in G.prefill_candidates(16384, 6144, 4096, "none")] == ["dli", "dli"]
+    assert [p.backend for p in G.prefill_candidates(16384, 6144, 4096, "none")] == ["dli"] * 3
     assert all(p.backend == "dli" for p in G.candidate_plans(512, 4096, 4096, "splitk"))
     G.clear_plans()
     # the 4-wave tiles stay out of the decode autotune (tile 41 cost the step 1.8 %)
     tiles = {p.tile for p in G.candidate_plans(512, 4096, 4096, "none")}
-    assert not tiles & {41, 45} and 34 in tiles
+    assert not tiles & {41, 45, 55} and 34 in tiles
     # decode QKV timing pins the candidate for the fused attention path, then restores
     p1, p4 = G.GemmPlan("dli", 30, 1), G.GemmPlan("dli", 32, 4)
     G.set_plan(1, 6144, 4096, "none", p4)
