@@ -23,7 +23,7 @@
 //
 // Files: gemm_common.h (shared epilogue / split-K pieces), gemm_tiles.hip (ids 0-21, 23-25),
 // gemm8p.hip (22, 26-28), gemm4w.h + gemm4w.hip (34, 41, 45), gemm4wp.hip (55: persistent
-// 45), gemm_sk.hip (60-62), gemv.hip (29-33 and the fused
+// 45), gemv.hip (29-33 and the fused
 // batch-1 combine). The losing 4-wave A/B variants of round 4 are documented, not built
 // (profiles/r4/gemm4w/).
 #include "gemm_common.h"
@@ -32,7 +32,6 @@ extern "C" int dli_gemm_set_slab_store(int mode) {
   const int old = gemm_tiles_set_slab_store(mode);
   gemm_8p_set_slab_store(mode);
   gemm_4w_set_slab_store(mode);
-  gemm_sk_set_slab_store(mode);
   return old;
 }
 
@@ -43,7 +42,6 @@ extern "C" int dli_gemm_set_slab_store_family(int family, int mode) {
     case 0: return gemm_tiles_set_slab_store(mode);
     case 1: return gemm_8p_set_slab_store(mode);
     case 2: return gemm_4w_set_slab_store(mode);
-    case 3: return gemm_sk_set_slab_store(mode);
     default: return -1;
   }
 }
@@ -55,9 +53,7 @@ extern "C" int dli_gemm_set_slab_store_family(int family, int mode) {
 // 20/21 = 128x64 with 2/3 stages; 22 = 256x256 8-phase ping-pong; 23/24 = 128x192 (3/2
 // stages), 25 = 256x192, 8 waves; 26 = 256x224 ping-pong; 29-33 = the M <= 4 weight
 // stream (16 / 32 rows per workgroup, dispatch_gemv); 55 = tile 45 persistent (one workgroup
-// per CU walks its tiles, no split-K / grouped mode); 60-62 = the skinny full-K tiles 64x128,
-// 64x96, 32x128 (gemm_sk.hip: 4 waves split a block's K range, operands straight from
-// global memory). ws: fp32 [splits, M, N] when splits>1.
+// per CU walks its tiles, no split-K / grouped mode). ws: fp32 [splits, M, N] when splits>1.
 // group_off (nullable): int[groups+1] row offsets; M is then the max rows of any group.
 extern "C" int dli_gemm(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M,
                         int N, int K, int epi, int tile_cfg, int splits, const void* bias,
@@ -73,7 +69,6 @@ extern "C" int dli_gemm(const void* A, int lda, const void* W, int ldw, void* C,
   if (r == DLI_NOT_MINE) r = gemm_8p_dispatch(epi, tile_cfg, DLI_GEMM_PASS);
   if (r == DLI_NOT_MINE) r = gemm_4w_dispatch(epi, tile_cfg, DLI_GEMM_PASS);
   if (r == DLI_NOT_MINE) r = gemm_4wp_dispatch(epi, tile_cfg, DLI_GEMM_PASS);
-  if (r == DLI_NOT_MINE) r = gemm_sk_dispatch(epi, tile_cfg, DLI_GEMM_PASS);
   if (r == DLI_NOT_MINE) r = gemm_gemv_dispatch(epi, tile_cfg, DLI_GEMM_PASS);
   return r == DLI_NOT_MINE ? (int)hipErrorInvalidValue : r;
 }

@@ -224,12 +224,10 @@ int gemm_tiles_dispatch(int epi, int tile_cfg, DLI_GEMM_ARGS);
 int gemm_8p_dispatch(int epi, int tile_cfg, DLI_GEMM_ARGS);
 int gemm_4w_dispatch(int epi, int tile_cfg, DLI_GEMM_ARGS);
 int gemm_4wp_dispatch(int epi, int tile_cfg, DLI_GEMM_ARGS);
-int gemm_sk_dispatch(int epi, int tile_cfg, DLI_GEMM_ARGS);
 int gemm_gemv_dispatch(int epi, int tile_cfg, DLI_GEMM_ARGS);
 int gemm_tiles_set_slab_store(int mode);
 int gemm_8p_set_slab_store(int mode);
 int gemm_4w_set_slab_store(int mode);
-int gemm_sk_set_slab_store(int mode);
 
 // EPI -> template argument, for a family's dispatch<EPI>(tile_cfg, ...)
 #define DLI_EPI_SWITCH(FN)                                                         \

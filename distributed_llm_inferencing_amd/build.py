@@ -68,7 +68,7 @@ def _digest(paths, flags) -> str:
 # compiler-made copy of their accumulators inside the K loop (a scratch spill, a rolled
 # epilogue indexing them dynamically) reads AGPRs an MFMA may still be writing. Such a
 # kernel must keep its accumulators in registers: a nonzero scratch size fails the build.
-ASM_MFMA_KERNELS = ("gemm4w_kernel", "gemm4wp_kernel", "gemm_sk_kernel")
+ASM_MFMA_KERNELS = ("gemm4w_kernel", "gemm4wp_kernel")
 _REMARKS = "-Rpass-analysis=kernel-resource-usage"
 
 

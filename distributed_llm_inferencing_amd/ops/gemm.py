@@ -55,11 +55,7 @@ TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256), 4: (256, 128),
          34: (256, 256), 41: (256, 256), 45: (256, 256),
          # 55 = 45 persistent: one workgroup per CU walks its tiles, the next tile's first two
          # K-tiles staged in the current tile's last two (gemm4wp.hip); no split-K / grouped
-         55: (256, 256),
-         # skinny full-K tiles for decode-sized M (gemm_sk.hip): a 4-wave workgroup splits one
-         # block's K range over its waves, fragments loaded straight from global memory, the
-         # partials summed through LDS; no split-K slabs at M = 512 on N = 4096 / 6144
-         60: (64, 128), 61: (64, 96), 62: (32, 128)}
+         55: (256, 256)}
 # the 4-wave plan raced against the 8-phase one in the prefill autotune
 PREFILL_4W_TILE = int(os.environ.get("DLI_GEMM_PREFILL_4W", "45"))
 # the persistent 4-wave tile (55) raced too (DLI_GEMM_PREFILL_PERSIST=0: not a candidate)
@@ -79,7 +75,7 @@ GEMV_MAX_M = 4
 GEMV_FUSED_NORM_TILES = (30, 31, 32, 33)
 TILE_WAVES = {13: (2, 4), 14: (4, 2), 15: (2, 4), 16: (4, 2), 17: (2, 4),
               22: (2, 4), 23: (2, 4), 24: (2, 4), 25: (4, 2),
-              26: (4, 2), 27: (2, 4), 28: (4, 2), 60: (1, 1), 61: (1, 1), 62: (1, 1)}
+              26: (4, 2), 27: (2, 4), 28: (4, 2)}
 
 
 def tile_ok(tile: int, epi: str) -> bool:
