@@ -76,6 +76,8 @@ def test_gemm_bf16_all_tiles(gpu, M, N, K):
         for splits in (1, 2, 4, 8):
             if K % (64 * splits):
                 continue
+            if tile == 55 and (splits > 1 or K % 128):      # persistent: unsplit, even K-tiles
+                continue
             out = ops._gemm_native(x, w, "none", plan=G.GemmPlan("dli", tile, splits))
             close(out, ref, rtol=1e-2, atol=1e-2)
 
@@ -759,7 +761,7 @@ def test_grouped_gemm_all_tiles_and_splitk(gpu, epi):
         refs.append(R.silu_mul(y.float().to(BF)) if epi == "silu_mul" else y)
     ref = torch.cat(refs)
     for tile in G.TILES:
-        if not G.tile_ok(tile, epi):
+        if not G.tile_ok(tile, epi) or tile == 55:         # 55 (persistent): no grouped mode
             continue
         for splits in (1, 2, 4):
             out = ops._gemm_native(x, w, epi, plan=G.GemmPlan("dli", tile, splits), groups=E,
