@@ -489,7 +489,11 @@ def candidate_plans(M: int, N: int, K: int, epi: str):
     # isolated decode timings (M = 512 LM head 4-7 %) but cost the step 1.8 % in a same-box
     # bench A/B (42,548 without vs 41,790 / 41,653 tok/s with, profiles/r4/bench/)
     excl_env = os.environ.get("DLI_GEMM_EXCLUDE")
-    excl = {int(t) for t in (excl_env if excl_env is not None else "26,27,41,45,55").split(",")
+    # 34 too (round 5): the 4-wave family wins isolated cold-weight timings within the noise
+    # but loses in the decode graph — down at M = 512 ran 70.4 us on tile 34 against 56.9 on
+    # the 8-phase tile 22, the LM head 433 vs 407 (profiles/r5/s12/wave_summary.txt vs
+    # profiles/r4/prof/llama_b512_head.wave.txt); the autotune flipped between them run to run
+    excl = {int(t) for t in (excl_env if excl_env is not None else "26,27,34,41,45,55").split(",")
             if t.strip()}
     # ... except where 256x256 tiles take more than one wave of the chip and 256x224 tiles
     # land on a whole number of waves (Llama-3-70B gate/up at M = 512: N = 57344 is 448

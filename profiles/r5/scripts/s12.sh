@@ -9,7 +9,9 @@ mkdir -p $O
 step() { local name=$1 t=$2; shift 2; echo "== $name"; timeout -k 10 $t "$@" > $O/$name.log 2>&1; local rc=$?;
          echo "rc[$name]=$rc"; tail -3 $O/$name.log; [ $rc -eq 0 ] || exit $rc; }
 rec() { echo "{\"arm\": \"$1\", \"bench\": $(grep -h '^{"metric"' $O/$1.log)}" >> $O/bench.jsonl; }
-step tests 1200 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m gpu
+step tests 900 python -u -m pytest -x -v --timeout 150 --timeout-method thread tests -m gpu --deselect tests/test_serving_gpu.py::test_serve_expert_on_gpu_through_master
+# the serve-expert test is silent while its workers start: stream their logs (autotune lines)
+echo "== serving"; timeout -k 10 600 env DLI_GEMM_AUTOTUNE_LOG=1 python -u -m pytest -x -v -s --timeout 500 --timeout-method thread tests/test_serving_gpu.py::test_serve_expert_on_gpu_through_master 2>&1 | tee $O/serving.log | grep -E "PASS|FAIL|autotune|Error|error" ; echo "rc[serving]=${PIPESTATUS[0]}"
 step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
 step bench1 300 python3 bench.py --gpus 1 --steps 20 --warmup 5
 rec bench1
