@@ -484,7 +484,7 @@ def head_logits_gmax(h, w):
 
 def _sample_gmax_ws(device, B: int):
     """Zeroed grow-only scratch of the group-max candidate sampler (overflow flags, which the
-    kernels leave zero, and B x 1024 candidate slots)."""
+    kernels leave zero, and B x 2048 candidate slots)."""
     nbytes = int(N.require_native().dli_sample_gmax_workspace_bytes(B))
     key = (device.type, device.index)
     ws = _gmax_wss.get(key)
