@@ -65,11 +65,6 @@ extern "C" int dli_gemm(const void* A, int lda, const void* W, int ldw, void* C,
   if (splits > 1 && ws == nullptr) return (int)hipErrorInvalidValue;
   if (groups < 1) groups = 1;
   const int* go = group_off;
-  // fp32 + 16-column group maxima (LM head feeding the candidate sampler): 8-phase tile 22
-  if (epi == EPI_F32_GMAX) {
-    const int r = gemm_8p_dispatch(epi, tile_cfg, DLI_GEMM_PASS);
-    return r == DLI_NOT_MINE ? (int)hipErrorInvalidValue : r;
-  }
   int r = gemm_tiles_dispatch(epi, tile_cfg, DLI_GEMM_PASS);
   if (r == DLI_NOT_MINE) r = gemm_8p_dispatch(epi, tile_cfg, DLI_GEMM_PASS);
   if (r == DLI_NOT_MINE) r = gemm_4w_dispatch(epi, tile_cfg, DLI_GEMM_PASS);

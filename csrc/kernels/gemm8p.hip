@@ -307,32 +307,6 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(
     }
     return;
   }
-  if constexpr (EPI == EPI_F32_GMAX) {
-    // fp32 logits, and each row's 16-column group maxima into ws [M][ceil(N / 16)]: the 4
-    // lanes fq = 0..3 of one fr hold a group's 16 columns (4 each), same row, so two xor
-    // shuffles give the group max; no lane-divergent exit around them
-    const int G = (N + 15) >> 4;
-    const bool v32 = out_vec<EPI_F32>(C, ldc, N, bias);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int row = wr0 + 16 * i + fr;
-      const bool rok = row < Mg;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int gcol = wc0 + 16 * j, col = gcol + 4 * fq;
-        if (rok && col < N)
-          store_quad<EPI_F32>(C, ldc, row0 + row, col, N, acc[i][j], bias, v32);
-        float mx = -INFINITY;
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (col + r < N) mx = fmaxf(mx, acc[i][j][r]);
-        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        if (fq == 0 && rok && gcol < N) ws[(long)(row0 + row) * G + (gcol >> 4)] = mx;
-      }
-    }
-    return;
-  }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int row = wr0 + 16 * i + fr;
@@ -942,14 +916,5 @@ static int dispatch_8p(int tile_cfg, DLI_GEMM_ARGS) {
   }
 }
 
-int gemm_8p_dispatch(int epi, int tile_cfg, DLI_GEMM_ARGS) {
-  if (epi == EPI_F32_GMAX) {                       // LM head + group maxima: tile 22, unsplit
-    if (tile_cfg != 22) return tile_cfg == 26 || tile_cfg == 27 || tile_cfg == 28
-                                   ? (int)hipErrorInvalidValue : DLI_NOT_MINE;
-    if (splits != 1 || ws == nullptr || go != nullptr || C == nullptr)
-      return (int)hipErrorInvalidValue;
-    return launch_8p<EPI_F32_GMAX, GEMM8P_DEFAULT>(DLI_GEMM_PASS);
-  }
-  DLI_EPI_SWITCH(dispatch_8p)
-}
+int gemm_8p_dispatch(int epi, int tile_cfg, DLI_GEMM_ARGS) { DLI_EPI_SWITCH(dispatch_8p) }
 int gemm_8p_set_slab_store(int mode) { return set_slab_store_tu(mode); }

@@ -11,10 +11,7 @@
 
 #define BK 64
 
-enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_SILU = 2, EPI_BIAS_GELU = 3, EPI_BIAS = 4,
-       // fp32 logits + the max of every 16-column group of each row into ws (the LM head
-       // feeding the sampler's candidate path; tile 22 unsplit only, gemm8p.hip)
-       EPI_F32_GMAX = 5 };
+enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_SILU = 2, EPI_BIAS_GELU = 3, EPI_BIAS = 4 };
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef const __attribute__((address_space(1))) void gbl_void;

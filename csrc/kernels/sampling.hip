@@ -501,115 +501,6 @@ __global__ void __launch_bounds__(SMP_THREADS) sample_kernel(
   if (tid == 0) out_tokens[row] = vocab_id(cidx[s_cnt]);
 }
 
-// ---------------------------------------------------------------------------------------
-// Candidate path for large batches fed by the LM head's 16-column group maxima (gemm8p.hip
-// EPI_F32_GMAX: gmax[row][g] = max of logits[row][16 g .. 16 g + 15]). At batch 512 the
-// one-workgroup-per-row sampler reads every row 1.25 times (263 MB of fp32 logits: 81 us per
-// step); here a row costs its 8k group maxima plus the 16 logits of each selected group.
-// Exactness: tau = the keff-th largest group max. The keff groups above it hold keff distinct
-// elements >= tau, so the row's keff-th largest element v >= tau, and every element >= v sits
-// in a group whose max >= tau: the candidate list (every column of every group with max >=
-// tau, in ascending column order, -inf pads) contains all of the row's top-keff with their
-// ties, and sample_kernel's two-phase consumer draws the same token as over the full row.
-// (The bound used is looser: tau = the keff-th largest of 512 slice maxima, see below.)
-// More than SMP_GCAND / 16 such groups set the row's overflow flag: full-row path.
-#define SMP_GROUP 16
-#define SMP_GCAND 2048                          // candidate slots per row (128 groups)
-#define SMP_GMAX_MAXG 8192                      // group maxima per row held in LDS
-
-template <typename LT>
-__global__ void __launch_bounds__(SMP_THREADS) sample_gmax_kernel(
-    float* __restrict__ cand_v, int* __restrict__ cand_i, int* __restrict__ overflow,
-    const LT* __restrict__ logits, long row_stride, int V, const float* __restrict__ gmax,
-    int G, const float* __restrict__ temperature, const int* __restrict__ top_k,
-    const float* __restrict__ top_p) {
-  __shared__ uint32_t keys[SMP_GMAX_MAXG];
-  __shared__ uint32_t hist[256];
-  __shared__ float tmp[16];
-  __shared__ uint32_t sel[3];
-  __shared__ int s_total;
-  const int row = blockIdx.x, tid = threadIdx.x;
-  const float T = temperature[row];
-  const int K = top_k[row];
-  if (!smp_split_ok(T, K, top_p[row])) return;        // sample_kernel reads the full row
-  const int keff = (T <= 0.f || K == 1) ? 1 : K;
-  const float* gm = gmax + (long)row * G;
-  // tau = the keff-th largest of the 512 per-thread maxima over contiguous slices of the
-  // maxima (a radix select over the G ~ 8k maxima themselves serialised on a few hot LDS
-  // histogram bins: 64.6 us per step at batch 512): keff slices hold a group max >= tau, so
-  // tau still bounds the row's keff-th largest element from below
-  const int per = (G + SMP_THREADS - 1) / SMP_THREADS;
-  const int b0 = min(G, tid * per), b1 = min(G, b0 + per);
-  uint32_t tmax = 0u;
-  for (int g = b0; g < b1; ++g) {
-    const uint32_t k = f2key(gm[g]);
-    keys[g] = k;
-    tmax = max(tmax, k);
-  }
-  __shared__ uint32_t tkeys[SMP_THREADS];
-  tkeys[tid] = tmax;
-  __syncthreads();
-  const uint32_t tau = radix_kth(tkeys, SMP_THREADS, (uint32_t)min(keff, SMP_THREADS), hist,
-                                 tmp, sel);
-  // ordered compaction of the groups >= tau over the same slices
-  int cnt = 0;
-  for (int g = b0; g < b1; ++g) cnt += keys[g] >= tau && keys[g] != 0u;
-  const int incl = (int)block_scan((float)cnt, tmp);   // exact: counts < 2^24
-  if (tid == SMP_THREADS - 1) s_total = incl;
-  __syncthreads();
-  const int total = s_total;
-  const long base = (long)row * SMP_GCAND;
-  if (total * SMP_GROUP > SMP_GCAND || tau == 0u) {
-    if (tid == 0) overflow[row] = 1;                   // sample_kernel reads the full row
-    return;
-  }
-  // slot s of the list = group #s in column order; thread t gathers its groups' columns
-  const LT* xr = logits + (long)row * row_stride;
-  int slot = incl - cnt;
-  for (int g = b0; g < b1; ++g) {
-    if (keys[g] >= tau && keys[g] != 0u) {
-#pragma unroll 4
-      for (int e = 0; e < SMP_GROUP; ++e) {
-        const int col = g * SMP_GROUP + e;
-        cand_v[base + slot * SMP_GROUP + e] = col < V ? ldv(xr, col) : -INFINITY;
-        cand_i[base + slot * SMP_GROUP + e] = col < V ? col : 0;
-      }
-      ++slot;
-    }
-  }
-  for (int e = total * SMP_GROUP + tid; e < SMP_GCAND; e += SMP_THREADS) {
-    cand_v[base + e] = -INFINITY;
-    cand_i[base + e] = 0;
-  }
-}
-
-extern "C" long dli_sample_gmax_workspace_bytes(int B) {
-  return B <= 0 ? 0 : (long)B * 4 + (long)B * SMP_GCAND * 8;
-}
-
-// Sample B rows whose LM head also produced its 16-column group maxima (gmax [B][G], G =
-// ceil(V / 16)). ws: >= dli_sample_gmax_workspace_bytes(B), its first B ints zero before the
-// first call (the kernels leave them zero). Rows the candidate path cannot take (top-k > 64,
-// plain temperature, overflowing ties) read their full row in sample_kernel as before.
-extern "C" int dli_sample_gmax(int* out_tokens, const float* logits, long row_stride, int B,
-                               int V, const float* gmax, const float* temperature,
-                               const int* top_k, const float* top_p, const long long* seeds,
-                               void* ws, hipStream_t st) {
-  if (B <= 0) return 0;
-  const int G = (V + SMP_GROUP - 1) / SMP_GROUP;
-  if (gmax == nullptr || ws == nullptr || G > SMP_GMAX_MAXG) return (int)hipErrorInvalidValue;
-  int* overflow = static_cast<int*>(ws);
-  float* cand_v = reinterpret_cast<float*>(overflow + B);
-  int* cand_i = reinterpret_cast<int*>(cand_v + (long)B * SMP_GCAND);
-  sample_gmax_kernel<float><<<B, SMP_THREADS, 0, st>>>(cand_v, cand_i, overflow, logits,
-                                                       row_stride, V, gmax, G, temperature,
-                                                       top_k, top_p);
-  sample_kernel<float><<<B, SMP_THREADS, 0, st>>>(out_tokens, logits, row_stride, V,
-                                                  temperature, top_k, top_p, seeds, cand_v,
-                                                  cand_i, overflow, SMP_GCAND);
-  DLI_RETURN_LAUNCH();
-}
-
 // Bytes of the two-phase workspace dli_sample takes for a batch of B rows (0: one phase).
 extern "C" long dli_sample_workspace_bytes(int B, int V) {
   if (B <= 0 || B > g_smp_max_b) return 0;

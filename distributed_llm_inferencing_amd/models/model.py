@@ -234,22 +234,13 @@ class TransformerLM:
         """Final norm + LM head on the last token of each sequence -> [S, V] logits."""
         return self.head_logits(self.final_hidden(hidden, b))
 
-    def logits_gmax(self, hidden: torch.Tensor, b: DeviceBatch):
-        """``logits`` plus the head's 16-column group maxima when its kernel produces them
-        (``ops.head_logits_gmax``; else None): the sampler's candidate path."""
-        p = self.params
-        w = p["embed"] if self.cfg.tie_embeddings else p["lm_head"]
-        return ops.head_logits_gmax(self.final_hidden(hidden, b), w)
-
     def head_candidates(self, h: torch.Tensor, c: int = 64):
         """This rank's slice of a vocab-parallel LM head (``params['head_slice']`` = rows
         ``[vocab_offset, vocab_offset + V_r)``): top-``c`` (fp32 values, int32 ids)."""
         return ops.head_candidates(h, self.params["head_slice"], self.vocab_offset, c)
 
-    def sample(self, logits: torch.Tensor, b: DeviceBatch, generator=None,
-               gmax=None) -> torch.Tensor:
-        return ops.sample(logits, b.temperature, b.top_k, b.top_p, b.seeds, generator=generator,
-                          gmax=gmax)
+    def sample(self, logits: torch.Tensor, b: DeviceBatch, generator=None) -> torch.Tensor:
+        return ops.sample(logits, b.temperature, b.top_k, b.top_p, b.seeds, generator=generator)
 
     def forward(self, b: DeviceBatch, kv_caches, hidden: Optional[torch.Tensor] = None,
                 return_logits: bool = False):
@@ -262,6 +253,6 @@ class TransformerLM:
             return x
         if self.vocab_parallel:          # the LM head runs sliced on every pipeline rank
             return self.final_hidden(x, b)
-        lg, gmax = self.logits_gmax(x, b)
-        tok = self.sample(lg, b, gmax=gmax)
+        lg = self.logits(x, b)
+        tok = self.sample(lg, b)
         return (tok, lg) if return_logits else tok

@@ -457,62 +457,17 @@ def _sample_ws(device, B: int, V: int):
 HEAD_EPI = "none" if os.environ.get("DLI_BF16_LOGITS", "0") == "1" else "f32"
 
 
-# LM head -> sampler through the head's 16-column group maxima (sampling.hip
-# sample_gmax_kernel): the sampler reads the maxima and the selected groups instead of every
-# logit. DLI_HEAD_GMAX=0 restores the full-row sampler (token-identical either way).
-HEAD_GMAX = os.environ.get("DLI_HEAD_GMAX", "1") == "1"
-_gmax_wss: dict = {}
-
-
-def head_logits_gmax(h, w):
-    """LM head ``h @ w.T`` in fp32 plus each row's 16-column group maxima ([B, ceil(V/16)]
-    fp32) when the head's GEMM plan is the 8-phase tile 22 unsplit (the only kernel with that
-    epilogue); else (logits, None)."""
-    if not (HEAD_GMAX and HEAD_EPI == "f32" and _use_native(h)) or h.stride(-1) != 1:
-        return linear(h, w, epi=HEAD_EPI), None
-    M, K = h.shape
-    V = w.shape[0]
-    p = G.plan(M, V, K, "f32")
-    if p.tile != 22 or p.splits != 1 or M <= 8:
-        return linear(h, w, epi=HEAD_EPI), None
-    out = torch.empty(M, V, dtype=torch.float32, device=h.device)
-    gmax = torch.empty(M, -(-V // 16), dtype=torch.float32, device=h.device)
-    _native_call("dli_gemm", _p(h), h.stride(0), _p(w), w.stride(-2), _p(out), out.stride(0),
-                 M, V, K, G.EPI["f32_gmax"], 22, 1, None, _p(gmax), None, 1, _st())
-    return out, gmax
-
-
-def _sample_gmax_ws(device, B: int):
-    """Zeroed grow-only scratch of the group-max candidate sampler (overflow flags, which the
-    kernels leave zero, and B x 2048 candidate slots)."""
-    nbytes = int(N.require_native().dli_sample_gmax_workspace_bytes(B))
-    key = (device.type, device.index)
-    ws = _gmax_wss.get(key)
-    if ws is None or ws.numel() < nbytes:
-        if ws is not None:
-            G._retired.append(ws)        # a captured graph may still hold it (ops.gemm)
-        ws = _gmax_wss[key] = torch.zeros(nbytes, dtype=torch.uint8, device=device)
-    return ws
-
-
-def sample(logits, temperature, top_k, top_p, seeds, generator=None, ids=None, gmax=None):
+def sample(logits, temperature, top_k, top_p, seeds, generator=None, ids=None):
     """logits fp32 or bf16 [B, V] -> int32 tokens [B] (every comparison on the exact fp32
     value of each logit). temperature<=0 -> greedy. With ``ids``
     [B, V] the row holds candidates (vocab-parallel LM head) in ascending token-id order,
     and the sampled column is mapped to its token id (ties then break by token id exactly
-    as over the full vocabulary). ``gmax``: the head's 16-column group maxima
-    (``head_logits_gmax``): rows then sample from the groups that can hold their top-k."""
+    as over the full vocabulary)."""
     if not _use_native(logits):
         return R.sample(logits, temperature, top_k, top_p, generator=generator, seeds=seeds,
                         ids=ids)
     B, V = logits.shape
     out = torch.empty(B, dtype=torch.int32, device=logits.device)
-    if (gmax is not None and ids is None and logits.dtype == torch.float32
-            and gmax.shape == (B, -(-V // 16)) and gmax.is_contiguous()):
-        _native_call("dli_sample_gmax", _p(out), _p(logits), logits.stride(0), B, V, _p(gmax),
-                     _p(temperature), _p(top_k), _p(top_p), _p(seeds),
-                     _p(_sample_gmax_ws(logits.device, B)), _st())
-        return out
     if logits.dtype not in (torch.float32, torch.bfloat16):
         logits = logits.float()
     fn = "dli_sample_bf16" if logits.dtype == torch.bfloat16 else "dli_sample"

@@ -53,8 +53,6 @@ _SIGS = {
     "dli_sample": [P, P, L, I, I, P, P, P, P, P, P],
     "dli_sample_workspace_bytes": [I, I],
     "dli_sample_bf16": [P, P, L, I, I, P, P, P, P, P, P],
-    "dli_sample_gmax": [P, P, L, I, I, P, P, P, P, P, P, P],
-    "dli_sample_gmax_workspace_bytes": [I],
     "dli_topk_rows_bf16": [P, P, P, L, I, I, I, I, P],
     "dli_topk_rows": [P, P, P, L, I, I, I, I, P],
     "dli_gemm": [P, I, P, I, P, I, I, I, I, I, I, I, P, P, P, I, P],

@@ -95,9 +95,7 @@ def tile_ok(tile: int, epi: str) -> bool:
 
 # "splitk": a plain GEMM whose fp32 partial slabs feed a fused reduce (ops.linear_add_rmsnorm,
 # ops.linear_rope_cache); planned/tuned separately (a non-split winner runs unfused).
-EPI = {"none": 0, "f32": 1, "silu_mul": 2, "bias_gelu": 3, "bias": 4, "splitk": 0,
-       # fp32 + 16-column group maxima of each row (LM head -> candidate sampler; tile 22)
-       "f32_gmax": 5}
+EPI = {"none": 0, "f32": 1, "silu_mul": 2, "bias_gelu": 3, "bias": 4, "splitk": 0}
 NUM_CUS = int(os.environ.get("DLI_NUM_CUS", "256"))
 
 

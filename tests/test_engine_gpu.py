@@ -140,25 +140,3 @@ def test_mixed_steps_token_identical_on_gpu(gpu, monkeypatch):
         res.append([outs[r].all_ids for r in rids])
         assert (eng.stats.mixed_steps > 0) == mixed
     assert res[0] == res[1]
-
-
-def test_lm_head_group_max_sampler_in_the_engine(gpu, monkeypatch):
-    """Decode steps whose LM head runs on tile 22 produce the 16-column group maxima and
-    sample through them: tokens identical to the full-row sampler (DLI_HEAD_GMAX off)."""
-    from distributed_llm_inferencing_amd import ops
-    from distributed_llm_inferencing_amd.ops import gemm as G
-    monkeypatch.setenv("DLI_GEMM_AUTOTUNE", "0")
-    prompts = [IDS[i % 5: i % 5 + 6] for i in range(16)]
-    sp = SamplingParams(max_length=28, temperature=0.8, top_k=50, top_p=0.95, seed=11,
-                        ignore_eos=True)
-    outs = []
-    for on in (False, True):
-        monkeypatch.setattr(ops, "HEAD_GMAX", on)
-        G.clear_plans()
-        eng = LLMEngine("llama-tiny128", device="cuda", max_batch=16, max_model_len=128,
-                        num_blocks=128, seed=3)
-        c = eng.cfg
-        G.set_plan(16, c.vocab_size, c.hidden_size, "f32", G.GemmPlan("dli", 22, 1))
-        outs.append([o.output_ids for o in eng.generate(prompts, sp)])
-    G.clear_plans()
-    assert outs[0] == outs[1]

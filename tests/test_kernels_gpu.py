@@ -1054,50 +1054,3 @@ def test_rccl_comm_module_self_exchange(gpu):
     with pytest.raises(RuntimeError):
         comm.exchange([(a, 3)], [], st)
     comm.close()
-
-
-@pytest.mark.parametrize("M,N,K", [(512, 128256, 4096), (300, 1000, 512), (37, 50257, 768)])
-def test_lm_head_group_maxima(gpu, M, N, K):
-    """EPI_F32_GMAX (8-phase tile 22): the fp32 logits are bitwise the plain fp32 epilogue's,
-    and gmax[r][g] is the max of logits[r][16 g .. 16 g + 15] (a partial last group: its
-    valid columns only)."""
-    torch.manual_seed(21)
-    x, w = rnd(M, K, dev=gpu), rnd(N, K, dev=gpu, scale=0.05)
-    ref = ops._gemm_native(x, w, "f32", plan=G.GemmPlan("dli", 22, 1))
-    G.set_plan(M, N, K, "f32", G.GemmPlan("dli", 22, 1))
-    try:
-        lg, gm = ops.head_logits_gmax(x, w)
-    finally:
-        G.clear_plans()
-    assert gm is not None and torch.equal(lg, ref)
-    Gn = -(-N // 16)
-    pad = torch.full((M, Gn * 16 - N), -float("inf"), device=gpu)
-    want = torch.cat([ref, pad], 1).view(M, Gn, 16).amax(-1)
-    assert torch.equal(gm, want)
-
-
-def test_sampler_group_max_path_is_token_identical(gpu):
-    """sample(gmax=...) draws exactly the full-row sampler's token for every warper setting:
-    top-k 50 / top-p 0.95 (the candidate path), greedy, k = 1, k = 64, k = 100 and plain
-    temperature (full-row fallback), top-p 0.5, rows of heavy ties (bf16-rounded logits) and
-    a constant row (more than 64 tied groups: overflow -> full row)."""
-    torch.manual_seed(22)
-    B, V = 96, 128256
-    lg = torch.randn(B, V, device=gpu) * 3
-    lg[8:16] = lg[8:16].to(BF).float()                  # many exact ties
-    lg[16] = 1.0                                        # every group tied
-    lg[17, 1000:1100] = 50.0                            # a block of 100 tied maxima
-    T = torch.full((B,), 0.8, device=gpu)
-    k = torch.full((B,), 50, dtype=torch.int32, device=gpu)
-    p = torch.full((B,), 0.95, device=gpu)
-    T[20], k[21], k[22], k[23], p[24] = 0.0, 1, 64, 100, 0.5
-    k[25], p[25] = 0, 1.0                               # plain temperature
-    seeds = torch.arange(B, dtype=torch.int64, device=gpu) * 7919 + 3
-    Gn = V // 16
-    gm = lg.view(B, Gn, 16).amax(-1).contiguous()
-    for rep in range(2):
-        a = ops.sample(lg, T, k, p, seeds)
-        b = ops.sample(lg, T, k, p, seeds, gmax=gm)
-        torch.cuda.synchronize()
-        assert torch.equal(a, b), (rep, torch.nonzero(a != b).flatten().tolist())
-        seeds = seeds + 1
