@@ -162,18 +162,6 @@ __device__ __forceinline__ void row_scan(const float* __restrict__ x, int V, F&&
     const int V4 = V >> 2;
     const float4* x4 = reinterpret_cast<const float4*>(x);
     int i = tid;
-    // 8 loads in flight per thread first (a 512-thread workgroup per row reads its row at
-    // the latency-bound rate of the bytes it keeps in flight), then 4, then 1
-    for (; i + 7 * nt < V4; i += 8 * nt) {
-      float4 a[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) a[u] = x4[i + u * nt];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int b = 4 * (i + u * nt);
-        f(a[u].x, b); f(a[u].y, b + 1); f(a[u].z, b + 2); f(a[u].w, b + 3);
-      }
-    }
     for (; i + 3 * nt < V4; i += 4 * nt) {
       const float4 a = x4[i], b = x4[i + nt], c = x4[i + 2 * nt], d = x4[i + 3 * nt];
       f(a.x, 4 * i); f(a.y, 4 * i + 1); f(a.z, 4 * i + 2); f(a.w, 4 * i + 3);
