@@ -33,11 +33,22 @@ __device__ __forceinline__ float dot8_acc(const bf16x8v w, const bf16x8v x, floa
 
 // The weight stream of one workgroup: res[m][wid * RW + r] = sum over this K slice of
 // A[m, :] . W[r0 + r, :] (r < RW), reduced across the wave and staged in LDS.
-template <int MB, int RW, int UNROLL>
+struct NoPrologue {
+  __device__ void issue() {}
+  __device__ void complete() {}
+};
+
+// PRE: the input rows are produced by `pro` (the RMSNorm prologue, into LDS): pro.issue()
+// requests the residual rows and norm weight, then this lane's first UNROLL weight steps are
+// requested (branch-free, clamped), then pro.complete() waits for the ROW loads only (they
+// are older than the weight loads, so the counted wait leaves the weight stream in flight),
+// normalises into LDS and synchronises. The prologue's latency (rows from the Infinity
+// Cache, a block reduction, LDS stores) thus runs under the first weight requests.
+template <int MB, int RW, int UNROLL, bool PRE = false, class Pro = NoPrologue>
 __device__ __forceinline__ void gemv_core(const u16* __restrict__ A, int lda,
                                           const u16* __restrict__ W, int ldw, int M, int N,
                                           int K, int k_split_len, int r0, int ks,
-                                          float (&res)[MB][4 * RW]) {
+                                          float (&res)[MB][4 * RW], Pro& pro) {
   // r0: this wave's first weight row (rows r0 .. r0 + RW - 1 land in res[.][wid * RW ..])
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int kb = ks * k_split_len;
@@ -59,6 +70,29 @@ __device__ __forceinline__ void gemv_core(const u16* __restrict__ A, int lda,
 #pragma unroll
     for (int r = 0; r < RW; ++r) acc[m][r] = 0.f;
   int c = lane;
+  if constexpr (PRE) {
+    pro.issue();
+    const bool first = c + 64 * (UNROLL - 1) < nchunk;
+    bf16x8v w[UNROLL][RW];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u)
+#pragma unroll
+      for (int r = 0; r < RW; ++r)
+        w[u][r] = __builtin_nontemporal_load(wrow[r] + min(c + 64 * u, nchunk - 1));
+    pro.complete();
+    if (first) {
+#pragma unroll
+      for (int m = 0; m < MB; ++m) {
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+          const bf16x8v xv = xrow[m][c + 64 * u];
+#pragma unroll
+          for (int r = 0; r < RW; ++r) acc[m][r] = dot8_acc(w[u][r], xv, acc[m][r]);
+        }
+      }
+      c += 64 * UNROLL;
+    }
+  }
   // UNROLL 64-chunk steps per iteration: UNROLL * RW weight loads in flight per lane (the
   // short projections of a batch-1 layer run only a few iterations, so depth, not
   // occupancy, hides the HBM latency)
@@ -98,27 +132,124 @@ __device__ __forceinline__ void gemv_core(const u16* __restrict__ A, int lda,
     }
 }
 
-// H16 (SiLU*up only, RW = 4): 16 rows per workgroup as 8 gate + 8 up rows of one 32-row
-// gate/up block (waves 0-1 the gate half h, waves 2-3 the matching up half), so the pairing
+// gemv-only epilogue: C is the residual, residual[m, n] = bf16(residual + bf16(acc)) (the
+// rounding of splitk_add_rmsnorm: the GEMM result is rounded before the add). Full K per
+// workgroup (splits 1): every output element has one writer and no slab round trip.
+constexpr int EPI_RES = 16;
+
+// The deferred RMSNorm of the consuming GEMV (PRO): x[m] = bf16(A[m] * rstd_m * nw) for the
+// MB input rows into LDS (xs: [MB][K] bf16), one block reduction per row. issue(): every row
+// vector and norm-weight vector of this thread requested (VPT 16-B vectors per row, indices
+// clamped, K <= 256 * 8 * VPT); complete(): sums, scales, stores, barrier. Numerics as
+// splitk_add_rmsnorm's output: (v * rstd) * w in fp32, rounded once.
+template <int MB, int VPT>
+struct NormPrologue {
+  const u16* A;
+  int lda;
+  const u16* nw;
+  float eps;
+  int M, K;
+  u16* xs;
+  float* red;
+  uint4 rv[MB][VPT], wv[VPT];
+  __device__ __forceinline__ void issue() {
+    const int nvec = K >> 3;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int vi = min((int)threadIdx.x + 256 * i, nvec - 1);
+#pragma unroll
+      for (int m = 0; m < MB; ++m)
+        rv[m][i] = *reinterpret_cast<const uint4*>(A + (long)min(m, M - 1) * lda + vi * 8);
+      wv[i] = *reinterpret_cast<const uint4*>(nw + vi * 8);
+    }
+  }
+  __device__ __forceinline__ void complete() {
+    const int nvec = K >> 3;
+#pragma unroll
+    for (int m = 0; m < MB; ++m) {
+      float v[VPT][8];
+      float ss = 0.f;
+#pragma unroll
+      for (int i = 0; i < VPT; ++i) {
+        const uint4 q = rv[m][i];
+        v[i][0] = __uint_as_float(q.x << 16); v[i][1] = __uint_as_float(q.x & 0xffff0000u);
+        v[i][2] = __uint_as_float(q.y << 16); v[i][3] = __uint_as_float(q.y & 0xffff0000u);
+        v[i][4] = __uint_as_float(q.z << 16); v[i][5] = __uint_as_float(q.z & 0xffff0000u);
+        v[i][6] = __uint_as_float(q.w << 16); v[i][7] = __uint_as_float(q.w & 0xffff0000u);
+        float s8 = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s8 += v[i][j] * v[i][j];
+        ss += ((int)threadIdx.x + 256 * i < nvec) ? s8 : 0.f;
+      }
+      const float rstd = rsqrtf(block_sum(ss, red) / K + eps);
+#pragma unroll
+      for (int i = 0; i < VPT; ++i) {
+        const int vi = (int)threadIdx.x + 256 * i;
+        const uint4 q = wv[i];
+        const float w8[8] = {__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u),
+                             __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xffff0000u),
+                             __uint_as_float(q.z << 16), __uint_as_float(q.z & 0xffff0000u),
+                             __uint_as_float(q.w << 16), __uint_as_float(q.w & 0xffff0000u)};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[i][j] = v[i][j] * rstd * w8[j];
+        if (vi < nvec) store8(xs + (long)m * K + vi * 8, v[i]);
+      }
+    }
+    __syncthreads();
+  }
+};
+
+// H16 (SiLU*up only): R = 4 RW rows per workgroup as R/2 gate + the matching R/2 up rows of
+// one 32-row gate/up block (waves 0-1 the gate rows, waves 2-3 the up rows; RW 4: 8 + 8,
+// RW 1: 2 + 2 — tile 58, 4x the workgroups of tile 29), so the pairing
 // runs at the 16-row grid (2x the workgroups of the 32-row tile; profiles/r4/b1/)
-template <int MB, int RW, int EPI, int UNROLL, bool H16 = false>
+template <int MB, int RW, int EPI, int UNROLL, bool H16 = false, bool PRO = false>
 __global__ void __launch_bounds__(256) gemv_kernel(
     const u16* __restrict__ A, int lda, const u16* __restrict__ W, int ldw,
     void* __restrict__ C, int ldc, int M, int N, int K, int k_split_len,
-    const u16* __restrict__ bias, float* __restrict__ ws) {
+    const u16* __restrict__ bias, float* __restrict__ ws, const u16* __restrict__ nw,
+    float eps) {
   constexpr int R = 4 * RW;
-  static_assert(!H16 || (EPI == EPI_SILU && RW == 4), "H16 pairs 8 gate + 8 up rows");
+  static_assert(!H16 || (EPI == EPI_SILU && RW <= 4), "H16 pairs R/2 gate + R/2 up rows");
+  constexpr int HR = R / 2, PARTS = 16 / HR;          // H16: rows per half, parts per block
   __shared__ float res[MB][R];
+  __shared__ float red[16];
+  extern __shared__ __align__(16) u16 xs_dyn[];
   const int n_base = blockIdx.x * R;
   const int ks = blockIdx.y;
   const int wid = threadIdx.x >> 6;
-  const int blk = blockIdx.x >> 1, half = blockIdx.x & 1;
+  const int blk = blockIdx.x / PARTS, half = blockIdx.x % PARTS;
   // weight row of res column j
   auto row_of = [&](int j) {
-    return H16 ? blk * 32 + (j < 8 ? half * 8 + j : 16 + half * 8 + (j - 8)) : n_base + j;
+    return H16 ? blk * 32 + (j < HR ? half * HR + j : 16 + half * HR + (j - HR)) : n_base + j;
   };
-  gemv_core<MB, RW, UNROLL>(A, lda, W, ldw, M, N, K, k_split_len, row_of(wid * RW), ks, res);
+  if constexpr (PRO) {
+    // row vectors per thread: 2 up to K = 4096 (Llama-3-8B / Mixtral hidden), 4 up to 8192
+    if (K <= 4096) {
+      NormPrologue<MB, 2> pro{A, lda, nw, eps, M, K, xs_dyn, red};
+      gemv_core<MB, RW, UNROLL, true>(xs_dyn, K, W, ldw, M, N, K, k_split_len,
+                                      row_of(wid * RW), ks, res, pro);
+    } else {
+      NormPrologue<MB, 4> pro{A, lda, nw, eps, M, K, xs_dyn, red};
+      gemv_core<MB, RW, UNROLL, true>(xs_dyn, K, W, ldw, M, N, K, k_split_len,
+                                      row_of(wid * RW), ks, res, pro);
+    }
+  } else {
+    NoPrologue pro;
+    gemv_core<MB, RW, UNROLL>(A, lda, W, ldw, M, N, K, k_split_len, row_of(wid * RW), ks, res,
+                              pro);
+  }
   __syncthreads();
+  if constexpr (EPI == EPI_RES) {
+    for (int t = threadIdx.x; t < MB * R; t += 256) {
+      const int m = t / R, j = t % R, n = n_base + j;
+      if (m < M && n < N) {
+        u16* p = (u16*)C + (long)m * ldc + n;
+        *p = f2bf(bf2f(*p) + bf2f(f2bf(res[m][j])));
+      }
+    }
+    return;
+  }
   // epilogue: one thread per (row m, output column)
   if (ws != nullptr && gridDim.y > 1) {             // fp32 partial slab of this K slice
     for (int t = threadIdx.x; t < MB * R; t += 256) {
@@ -127,12 +258,12 @@ __global__ void __launch_bounds__(256) gemv_kernel(
     }
     return;
   }
-  if (H16) {                                        // res 0-7 gate, 8-15 the matching up
-    for (int t = threadIdx.x; t < MB * 8; t += 256) {
-      const int m = t / 8, j = t % 8;
-      const int f = blk * 16 + half * 8 + j;
+  if (H16) {                                        // res 0..HR-1 gate, HR.. the matching up
+    for (int t = threadIdx.x; t < MB * HR; t += 256) {
+      const int m = t / HR, j = t % HR;
+      const int f = blk * 16 + half * HR + j;
       if (m < M && blk * 32 < N)
-        ((u16*)C)[(long)m * ldc + f] = f2bf(silu_f(res[m][j]) * res[m][j + 8]);
+        ((u16*)C)[(long)m * ldc + f] = f2bf(silu_f(res[m][j]) * res[m][j + HR]);
     }
     return;
   }
@@ -151,25 +282,33 @@ __global__ void __launch_bounds__(256) gemv_kernel(
   }
 }
 
-template <int MB, int RW, int EPI, int UNROLL = 2, bool H16 = false>
+// nw != null (PRO): A is the raw residual, normalised per row into LDS by the prologue
+// (MB * K * 2 bytes of dynamic LDS, <= 64 KB)
+template <int MB, int RW, int EPI, int UNROLL = 2, bool H16 = false, bool PRO = false>
 static int launch_gemv(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M,
-                       int N, int K, int splits, const void* bias, void* ws, hipStream_t st) {
+                       int N, int K, int splits, const void* bias, void* ws, hipStream_t st,
+                       const void* nw = nullptr, float eps = 0.f) {
   constexpr int R = 4 * RW;
   if (M > MB || (EPI == EPI_SILU && ((R != 32 && !H16) || N % 32)) || K % 8 || lda % 8 ||
       ldw % 8)
     return (int)hipErrorInvalidValue;
+  const size_t lds = PRO ? (size_t)MB * K * 2 : 0;
+  if (PRO && (nw == nullptr || K > 8192 || lds > 65536)) return (int)hipErrorInvalidValue;
+  if (EPI == EPI_RES && (splits != 1 || C == nullptr)) return (int)hipErrorInvalidValue;
   int ksl = K / splits;
   ksl = (ksl / 8) * 8;
   if (ksl * splits != K) return (int)hipErrorInvalidValue;
   dim3 grid((N + R - 1) / R, splits);
-  gemv_kernel<MB, RW, EPI, UNROLL, H16><<<grid, 256, 0, st>>>((const u16*)A, lda, (const u16*)W, ldw, C, ldc,
-                                                 M, N, K, ksl, (const u16*)bias,
-                                                 splits > 1 ? (float*)ws : nullptr);
-  if (splits > 1 && C != nullptr) {
-    const int outN = (EPI == EPI_SILU) ? N / 2 : N;
-    const long total = (long)M * outN;
-    splitk_reduce_kernel<EPI><<<(int)((total + 255) / 256), 256, 0, st>>>(
-        C, ldc, (const float*)ws, M, N, splits, (const u16*)bias);
+  gemv_kernel<MB, RW, EPI, UNROLL, H16, PRO><<<grid, 256, lds, st>>>(
+      (const u16*)A, lda, (const u16*)W, ldw, C, ldc, M, N, K, ksl, (const u16*)bias,
+      splits > 1 ? (float*)ws : nullptr, (const u16*)nw, eps);
+  if constexpr (EPI != EPI_RES) {
+    if (splits > 1 && C != nullptr) {
+      const int outN = (EPI == EPI_SILU) ? N / 2 : N;
+      const long total = (long)M * outN;
+      splitk_reduce_kernel<EPI><<<(int)((total + 255) / 256), 256, 0, st>>>(
+          C, ldc, (const float*)ws, M, N, splits, (const u16*)bias);
+    }
   }
   DLI_RETURN_LAUNCH();
 }
@@ -258,7 +397,9 @@ __global__ void __launch_bounds__(256) gemv_addnorm_kernel(
   const int n_base = blockIdx.x * R;
   const int ks = blockIdx.y, S = gridDim.y, nblk = gridDim.x;
   const int wid = threadIdx.x >> 6;
-  gemv_core<MB, RW, UNROLL>(A, lda, W, ldw, M, N, K, k_split_len, n_base + wid * RW, ks, res);
+  NoPrologue pro;
+  gemv_core<MB, RW, UNROLL>(A, lda, W, ldw, M, N, K, k_split_len, n_base + wid * RW, ks, res,
+                            pro);
   __syncthreads();
   for (int t = threadIdx.x; t < MB * R; t += 256) {
     const int m = t / R, j = t % R, n = n_base + j;
@@ -377,11 +518,45 @@ static int dispatch_gemv(int tile_cfg, const void* A, int lda, const void* W, in
                   : (int)hipErrorInvalidValue;
   // 29: SiLU*up gate/up on the 16-row grid (8 gate + 8 up rows per workgroup); 4 K-steps
   // in flight per lane at M = 1 (tile 32's depth), 2 at M = 2..4 (tile 30's)
+  // 58 / 59: the pairing with 2 + 2 / 4 + 4 rows a workgroup and 8 K-steps in flight per
+  // lane (tile 56 / 57's grid for the gate/up projection)
+  if (tile_cfg == 58 || tile_cfg == 59) {
+    if constexpr (EPI == EPI_SILU) {
+      const bool r8 = tile_cfg == 59;
+      if (M <= 1)
+        return r8 ? launch_gemv<1, 2, EPI, 8, true>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st)
+                  : launch_gemv<1, 1, EPI, 8, true>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st);
+      if (M <= 2)
+        return r8 ? launch_gemv<2, 2, EPI, 4, true>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st)
+                  : launch_gemv<2, 1, EPI, 8, true>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st);
+      if (M <= 4)
+        return r8 ? launch_gemv<4, 2, EPI, 4, true>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st)
+                  : launch_gemv<4, 1, EPI, 8, true>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st);
+    }
+    return (int)hipErrorInvalidValue;
+  }
   if (tile_cfg == 29) {
     if constexpr (EPI == EPI_SILU) {
       if (M <= 1) return launch_gemv<1, 4, EPI, 4, true>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st);
       if (M <= 2) return launch_gemv<2, 4, EPI, 2, true>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st);
       if (M <= 4) return launch_gemv<4, 4, EPI, 2, true>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st);
+    }
+    return (int)hipErrorInvalidValue;
+  }
+  // 56 / 57: 4 / 8 rows a workgroup with 8 K-steps in flight per lane (4x / 2x the
+  // workgroups of tile 30 on one projection: full-K or lightly split skinny projections)
+  if (tile_cfg == 56 || tile_cfg == 57) {
+    if constexpr (EPI != EPI_SILU) {
+      const bool r8 = tile_cfg == 57;
+      if (M <= 1)
+        return r8 ? launch_gemv<1, 2, EPI, 8>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st)
+                  : launch_gemv<1, 1, EPI, 8>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st);
+      if (M <= 2)
+        return r8 ? launch_gemv<2, 2, EPI, 4>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st)
+                  : launch_gemv<2, 1, EPI, 8>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st);
+      if (M <= 4)
+        return r8 ? launch_gemv<4, 2, EPI, 4>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st)
+                  : launch_gemv<4, 1, EPI, 8>(A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st);
     }
     return (int)hipErrorInvalidValue;
   }
@@ -398,7 +573,7 @@ static int dispatch_gemv(int tile_cfg, const void* A, int lda, const void* W, in
 }
 
 int gemm_gemv_dispatch(int epi, int tile_cfg, DLI_GEMM_ARGS) {
-  if (tile_cfg < 29 || tile_cfg > 33) return DLI_NOT_MINE;
+  if ((tile_cfg < 29 || tile_cfg > 33) && (tile_cfg < 56 || tile_cfg > 59)) return DLI_NOT_MINE;
   if (go != nullptr) return (int)hipErrorInvalidValue;     // no grouped mode
   (void)groups;
   switch (epi) {
@@ -409,4 +584,62 @@ int gemm_gemv_dispatch(int epi, int tile_cfg, DLI_GEMM_ARGS) {
     case EPI_BIAS: return dispatch_gemv<EPI_BIAS>(tile_cfg, A, lda, W, ldw, C, ldc, M, N, K, splits, bias, ws, st);
     default: return (int)hipErrorInvalidValue;
   }
+}
+
+// ---------------------------------------------------------------------------------------
+// Batch-1 decode without the split-K reduce kernels (ops.linear_residual / ops.NormedRows):
+//  * epi EPI_RES (16), nw null: residual[M, N] (= C) += A . W^T, full K per workgroup;
+//  * nw != null: A is the raw residual [M, K]; the GEMV normalises it in its prologue
+//    (x = rmsnorm(A) * nw, into LDS) and runs epi 0 (bf16 C, or fp32 slabs when C is null
+//    and splits > 1: the fused QKV consumer) or 2 (SiLU*up).
+// The O / down projections then write the residual directly and the next GEMV (gate/up,
+// the next layer's QKV) applies the norm: two kernels fewer per layer.
+// Tiles: 30 / 32 as dli_gemm (16 rows a workgroup, 2 / 4 K-steps in flight), 29 / 31 / 33
+// (SiLU), and for EPI_RES 56 (4 rows a workgroup, 8 K-steps in flight: 1024 workgroups on
+// a 4096-wide projection) and 57 (8 rows, 8 K-steps).
+extern "C" int dli_gemv_fused(const void* A, int lda, const void* nw, float eps, const void* W,
+                              int ldw, void* C, int ldc, int M, int N, int K, int epi,
+                              int tile_cfg, int splits, void* ws, hipStream_t st) {
+  if (M <= 0 || N <= 0) return 0;
+  // split K needs the fp32 slabs: the output itself (C null) or the reduce's input
+  if (M > 4 || splits < 1 || (splits > 1 && ws == nullptr) || (C == nullptr && splits < 2))
+    return (int)hipErrorInvalidValue;
+#define DLI_GF(MB, RW, E, U, H, P) \
+  return launch_gemv<MB, RW, E, U, H, P>(A, lda, W, ldw, C, ldc, M, N, K, splits, nullptr, ws, st, nw, eps)
+#define DLI_GF_M(RW, E, U1, U, H, P)           \
+  if (M <= 1) DLI_GF(1, RW, E, U1, H, P);      \
+  if (M <= 2) DLI_GF(2, RW, E, U, H, P);       \
+  DLI_GF(4, RW, E, U, H, P)
+  if (nw != nullptr) {
+    if (epi == EPI_SILU) {
+      switch (tile_cfg) {
+        case 29: DLI_GF_M(4, EPI_SILU, 4, 2, true, true);
+        case 31: DLI_GF_M(8, EPI_SILU, 2, 2, false, true);
+        case 33: if (M <= 1) DLI_GF(1, 8, EPI_SILU, 4, false, true); break;
+        case 58: DLI_GF_M(1, EPI_SILU, 8, 8, true, true);
+        case 59: DLI_GF_M(2, EPI_SILU, 8, 4, true, true);
+        default: break;
+      }
+    } else if (epi == EPI_BF16) {
+      switch (tile_cfg) {
+        case 30: DLI_GF_M(4, EPI_BF16, 2, 2, false, true);
+        case 32: if (M <= 1) DLI_GF(1, 4, EPI_BF16, 4, false, true); break;
+        case 56: DLI_GF_M(1, EPI_BF16, 8, 8, false, true);
+        case 57: DLI_GF_M(2, EPI_BF16, 8, 4, false, true);
+        default: break;
+      }
+    }
+    return (int)hipErrorInvalidValue;
+  }
+  if (epi != EPI_RES) return (int)hipErrorInvalidValue;
+  switch (tile_cfg) {
+    case 30: DLI_GF_M(4, EPI_RES, 2, 2, false, false);
+    case 32: if (M <= 1) DLI_GF(1, 4, EPI_RES, 4, false, false); break;
+    case 56: DLI_GF_M(1, EPI_RES, 8, 8, false, false);
+    case 57: DLI_GF_M(2, EPI_RES, 8, 4, false, false);
+    default: break;
+  }
+#undef DLI_GF_M
+#undef DLI_GF
+  return (int)hipErrorInvalidValue;
 }

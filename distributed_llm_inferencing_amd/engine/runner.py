@@ -178,6 +178,7 @@ class StageRunner:
 
     def gemm_shapes(self, M: int):
         """(shapes, weights) of every projection GEMM a decode step of M rows runs here."""
+        from ..ops import gemm as G
         m = self.model
         shapes, weights = [], {}
         lp = m.layers[0] if m.layers else {}
@@ -194,6 +195,11 @@ class StageRunner:
             add(lp.get("wqkv"), "splitk"), add(lp.get("wo"), "splitk")
             if not m.cfg.is_moe:
                 add(lp.get("w_gu"), "silu_mul"), add(lp.get("w_down"), "splitk")
+            # batch-1 / tiny steps: O and down add into the residual in their own epilogue
+            # (models/model.py deferred norm) — timed as that op
+            if (M <= G.GEMV_MAX_M and G.DEFER_NORM and not m.cfg.is_moe
+                    and m.tp_reduce is None):
+                add(lp.get("wo"), "res"), add(lp.get("w_down"), "res")
         if m.is_last and not m.vocab_parallel:
             head = m.params["embed"] if m.cfg.tie_embeddings else m.params.get("lm_head")
             add(head, ops.HEAD_EPI)
@@ -242,7 +248,13 @@ class StageRunner:
             shapes, weights = self.gemm_shapes(b)
             c = m.cfg
             qkv = ((c.num_heads, c.num_kv_heads, c.head_dim) if c.arch != "gpt2" else None)
-            G.autotune(shapes, weights, self.device, log=log, qkv_heads=qkv)
+            normed = ()
+            if (b <= G.GEMV_MAX_M and G.DEFER_NORM and not c.is_moe and c.arch != "gpt2"
+                    and m.tp_reduce is None and m.layers):
+                lp = m.layers[0]           # batch-1 QKV and gate/up read a deferred norm
+                normed = {(lp["wqkv"].shape[0], lp["wqkv"].shape[1], "splitk"),
+                          (lp["w_gu"].shape[0], lp["w_gu"].shape[1], "silu_mul")}
+            G.autotune(shapes, weights, self.device, log=log, qkv_heads=qkv, normed_in=normed)
             if moe:      # grouped expert GEMMs: rows = b tokens x top-k (uniform routing)
                 lp = m.layers[0]
                 rows = b * m.cfg.top_k_experts

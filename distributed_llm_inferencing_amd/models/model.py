@@ -140,6 +140,11 @@ class TransformerLM:
             return x
         h = ops.rmsnorm(x, self.layers[0]["attn_norm"], eps, residual_copy=residual)
         pending = None
+        # batch-1 / tiny decode steps: the O and down GEMVs add into the residual themselves
+        # and the next GEMV normalises its input rows in its prologue (ops.NormedRows), so no
+        # split-K reduce + RMSNorm kernel runs between them (2 kernels fewer per layer)
+        defer = (not b.is_prefill and self.tp_reduce is None and not cfg.is_moe
+                 and ops.deferred_norm_ok(x))
         for li, lp in enumerate(self.layers):
             kc, vc = kv_caches[li] if kv_caches else (None, None)
             if pending is not None:          # MoE output of the previous layer
@@ -156,18 +161,21 @@ class TransformerLM:
                                             self.cos_sin, kc, vc, cfg.num_heads,
                                             cfg.num_kv_heads, cfg.head_dim)
                 attn = self._attend(qkv, b, kc, vc)
-            h = self._proj_add_norm(attn, lp["wo"], residual, lp["mlp_norm"], eps)
+            h = self._proj_add_norm(attn, lp["wo"], residual, lp["mlp_norm"], eps, defer)
             if cfg.is_moe:
                 pending = self.moe_fn(h, lp, self.layer_start + li)
                 continue
             act = ops.linear(h, lp["w_gu"], epi="silu_mul")
             nxt = self.layers[li + 1]["attn_norm"] if li + 1 < n else None
-            h = self._proj_add_norm(act, lp["w_down"], residual, nxt, eps)
+            h = self._proj_add_norm(act, lp["w_down"], residual, nxt, eps, defer)
         if pending is not None:
             residual.add_(pending)
         return residual
 
-    def _proj_add_norm(self, x, w, residual, norm_w, eps):
+    def _proj_add_norm(self, x, w, residual, norm_w, eps, defer: bool = False):
+        if defer:
+            ops.linear_residual(x, w, residual)
+            return None if norm_w is None else ops.NormedRows(residual, norm_w, eps)
         if self.tp_reduce is None:
             return ops.linear_add_rmsnorm(x, w, residual, norm_w, eps)
         y = self.tp_reduce(ops.linear(x, w))

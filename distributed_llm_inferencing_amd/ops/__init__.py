@@ -86,6 +86,83 @@ def add_layernorm(x, residual, w, b, eps):
     return out
 
 
+class NormedRows:
+    """rmsnorm(residual) * w, not yet computed: batch-1 decode (models/model.py) hands this to
+    the consuming GEMV, whose prologue normalises the rows into LDS (``dli_gemv_fused``), so
+    the O / down projections add straight into the residual (``linear_residual``) and no
+    reduce + norm kernel runs between them. Consumers without such a prologue call
+    ``materialize()``. The residual must not change before the consumer has run."""
+    __slots__ = ("residual", "w", "eps")
+
+    def __init__(self, residual: torch.Tensor, w: torch.Tensor, eps: float):
+        self.residual, self.w, self.eps = residual, w, eps
+
+    @property
+    def shape(self):
+        return self.residual.shape
+
+    @property
+    def device(self):
+        return self.residual.device
+
+    @property
+    def dtype(self):
+        return self.residual.dtype
+
+    def materialize(self) -> torch.Tensor:
+        return rmsnorm(self.residual, self.w, self.eps)
+
+
+def deferred_norm_ok(x: torch.Tensor) -> bool:
+    """Whether a decode step of ``x.shape[0]`` rows runs the reduce-free GEMV chain."""
+    M, K = x.shape
+    return (G.DEFER_NORM and _use_native(x) and M <= G.GEMV_MAX_M and K % 8 == 0
+            and K <= 8192 and x.is_contiguous())
+
+
+def _gemv_prologue(x: NormedRows, w, epi: str, plan: Optional[G.GemmPlan], C, ldc, ws=None):
+    """Run the GEMV with the deferred norm in its prologue; False if the plan has no such
+    variant (the caller materialises the norm)."""
+    M, K = x.shape
+    p = plan or G.plan(M, w.shape[0], K, epi)
+    tiles = G.GEMV_PRO_TILES.get(epi, ())
+    if p.tile not in tiles or (p.tile in G.GEMV_PRO_M1_ONLY and M > 1) or M > G.GEMV_MAX_M:
+        return False
+    r = x.residual
+    code = G.EPI["silu_mul"] if epi == "silu_mul" else 0
+    if ws is None and p.splits > 1:      # split K into C: slabs + the reduce kernel
+        ws = G.workspace(r.device, p.splits * M * w.shape[0] * 4)
+    _native_call("dli_gemv_fused", _p(r), r.stride(0), _p(x.w), x.eps, _p(w), w.stride(-2),
+                 _p(C), ldc, M, w.shape[0], K, code, p.tile, p.splits, _p(ws), _st())
+    return True
+
+
+def linear_normed(x: NormedRows, w, epi: str, plan: G.GemmPlan):
+    """epi(rmsnorm(x) @ w.T) under a forced plan (the autotuner's timing of a prologue GEMV;
+    plans without a prologue variant materialise the norm first, as ``linear`` does)."""
+    n_out = w.shape[-2] // 2 if epi == "silu_mul" else w.shape[-2]
+    y = torch.empty(x.shape[0], n_out, dtype=x.dtype, device=x.device)
+    if plan.splits > 1 and epi == "splitk":
+        return _gemm_native(x.materialize(), w, "none", plan=plan)
+    if _gemv_prologue(x, w, epi, plan, y, y.stride(0)):
+        return y
+    return _gemm_native(x.materialize(), w, epi, plan=plan, out=y)
+
+
+def linear_residual(x, w, residual, plan: Optional[G.GemmPlan] = None):
+    """residual += x @ w.T (bf16-rounded, in place) — the O / down projection of a batch-1
+    decode layer as ONE kernel: full K per workgroup, the add in its epilogue (no split-K
+    slabs, no reduce kernel). Other shapes take ``linear_add_rmsnorm`` without a norm."""
+    M, K = x.shape
+    p = plan or G.plan(M, w.shape[0], K, "res")
+    if (not _use_native(x) or p.tile not in G.GEMV_RES_TILES or M > G.GEMV_MAX_M
+            or not residual.is_contiguous() or x.stride(-1) != 1 or w.stride(-1) != 1):
+        linear_add_rmsnorm(x, w, residual, None, 0.0)
+        return
+    _native_call("dli_gemv_fused", _p(x), x.stride(0), None, 0.0, _p(w), w.stride(-2),
+                 _p(residual), residual.stride(0), M, w.shape[0], K, 16, p.tile, 1, None, _st())
+
+
 # ----------------------------------------------------------------------------- embedding
 def embedding(ids, table, pos_table=None, positions=None):
     if not _use_native(table):
@@ -127,6 +204,15 @@ def linear(x, w, bias=None, epi: str = "none", out=None):
     silu_mul expects the 16-row interleaved gate/up weight and returns width N/2."""
     if bias is not None and epi == "none":
         epi = "bias"
+    if isinstance(x, NormedRows):
+        if (bias is None and epi in ("none", "silu_mul") and _use_native(x.residual)
+                and x.residual.is_contiguous()):
+            M = x.shape[0]
+            n_out = w.shape[-2] // 2 if epi == "silu_mul" else w.shape[-2]
+            y = out if out is not None else torch.empty(M, n_out, dtype=x.dtype, device=x.device)
+            if _gemv_prologue(x, w, epi, None, y, y.stride(0)):
+                return y
+        x = x.materialize()
     if not _use_native(x):
         if epi == "silu_mul":
             y = R.silu_mul(R.linear(x, w))
@@ -194,6 +280,8 @@ def linear_rope_cache(x, w, positions, slot_mapping, cos_sin, k_cache, v_cache, 
                       use_rope: bool = True, plan: Optional[G.GemmPlan] = None):
     """qkv = x @ w.T with RoPE applied in place to q,k and k,v written to the paged cache.
     ``plan`` forces the GEMM plan (the autotuner times QKV candidates with this consumer)."""
+    if isinstance(x, NormedRows):
+        x = x.materialize()
     if plan is None:
         p = _splitk_plan(x, w)
     else:
@@ -225,10 +313,11 @@ def linear_rope_attention(x, w, positions, slot_mapping, cos_sin, k_cache, v_cac
     None where the fused kernel does not apply (the caller then runs the two-kernel path):
     split counts other than 2 / 4, KV-split attention (long contexts at small batch), the
     pipelined long-context kernel, head dim != 128. ``DLI_FUSED_ROPE_ATTN=0`` turns it off."""
+    xr = x.residual if isinstance(x, NormedRows) else x
     if (os.environ.get("DLI_FUSED_ROPE_ATTN", "1") != "1" or hd != 128 or k_cache is None
-            or not _use_native(x)):
+            or not _use_native(xr)):
         return None
-    p = _splitk_plan(x, w)
+    p = _splitk_plan(xr, w)
     if p is not None and p.splits not in (2, 4):
         return None
     B, K = x.shape
@@ -241,9 +330,13 @@ def linear_rope_attention(x, w, positions, slot_mapping, cos_sin, k_cache, v_cac
     if p is None:                         # unsplit plan: the prologue reads the bf16 rows
         src, splits = linear(x, w), 0
     else:
-        src, splits = G.workspace(x.device, p.splits * B * Nn * 4), p.splits
-        _native_call("dli_gemm", _p(x), x.stride(0), _p(w), w.stride(-2), None, Nn, B, Nn, K,
-                     0, p.tile, p.splits, None, _p(src), None, 1, _st())
+        src, splits = G.workspace(xr.device, p.splits * B * Nn * 4), p.splits
+        if not (isinstance(x, NormedRows)
+                and _gemv_prologue(x, w, "splitk", p, None, Nn, ws=src)):
+            if isinstance(x, NormedRows):
+                x = x.materialize()
+            _native_call("dli_gemm", _p(x), x.stride(0), _p(w), w.stride(-2), None, Nn, B, Nn,
+                         K, 0, p.tile, p.splits, None, _p(src), None, 1, _st())
     out = torch.empty(B, hq * hd, dtype=x.dtype, device=x.device)
     _native_call("dli_decode_attention_fused", _p(out), _p(src), splits, _p(positions),
                  _p(slot_mapping), _p(cos_sin), _p(k_cache), _p(v_cache), _p(block_tables),

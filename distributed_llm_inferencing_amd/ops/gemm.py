@@ -67,12 +67,22 @@ MOE_PREFILL_TILE = int(os.environ.get("DLI_MOE_PREFILL_TILE", "45"))
 # weight-streaming skinny GEMM (gemm.hip gemv_kernel) for M <= GEMV_MAX_M rows: 16 / 32 output
 # rows per workgroup (31 for the SiLU*up gate/up pairing); not an MFMA tile, so kept apart
 GEMV_TILES = {30: 16, 31: 32, 32: 16, 33: 32,   # 32 / 33: 4 K-steps in flight per lane, M = 1
-              29: 16}   # 29: SiLU*up on the 16-row grid (8 gate + 8 up rows), M <= 4
+              29: 16,   # 29: SiLU*up on the 16-row grid (8 gate + 8 up rows), M <= 4
+              56: 4, 57: 8,   # 4 / 8 rows a workgroup, 8 K-steps in flight (not SiLU)
+              58: 4, 59: 8}   # SiLU*up pairing (2 + 2 / 4 + 4 rows), 8 K-steps in flight
 GEMV_M1_ONLY = (32, 33)
 GEMV_MAX_M = 4
 # weight-streaming tiles whose split-K combine + residual add + RMSNorm run in-launch
 # (ops.linear_add_rmsnorm -> dli_gemv_add_rmsnorm)
 GEMV_FUSED_NORM_TILES = (30, 31, 32, 33)
+# batch-1 decode without split-K reduces (ops.linear_residual, ops.NormedRows): the GEMVs that
+# add into the residual (epi "res", full K per workgroup) and the tiles whose prologue applies
+# a deferred RMSNorm to their input rows (gemv.hip dli_gemv_fused)
+GEMV_RES_TILES = {30: 16, 32: 16, 56: 4, 57: 8}
+GEMV_PRO_TILES = {"silu_mul": (29, 31, 33, 58, 59), "splitk": (30, 32, 56, 57),
+                  "none": (30, 32, 56, 57)}
+GEMV_PRO_M1_ONLY = (32, 33)
+DEFER_NORM = os.environ.get("DLI_DEFER_NORM", "1") == "1"
 TILE_WAVES = {13: (2, 4), 14: (4, 2), 15: (2, 4), 16: (4, 2), 17: (2, 4),
               22: (2, 4), 23: (2, 4), 24: (2, 4), 25: (4, 2),
               26: (4, 2), 27: (2, 4), 28: (4, 2)}
@@ -81,7 +91,9 @@ TILE_WAVES = {13: (2, 4), 14: (4, 2), 15: (2, 4), 16: (4, 2), 17: (2, 4),
 def tile_ok(tile: int, epi: str) -> bool:
     """The SiLU*up epilogue pairs 16-column gate/up blocks inside a wave's column range,
     which must therefore be a multiple of 32."""
-    if tile == 29:
+    if epi == "res":
+        return tile in GEMV_RES_TILES
+    if tile in (29, 58, 59):
         return epi == "silu_mul"
     if tile in GEMV_TILES:
         return epi != "silu_mul" or tile in (31, 33)
@@ -171,6 +183,10 @@ def _heuristic(M: int, N: int, K: int, epi: str) -> GemmPlan:
                    and K // (splits * 2) >= 1024 and splits < 4):
                 splits *= 2
         return GemmPlan("dli", 22, splits)
+    if epi == "res":
+        # residual-adding GEMV (full K): 4 rows a workgroup, 8 K-steps in flight per lane
+        # (1024 workgroups on a 4096-wide projection)
+        return GemmPlan("dli", 56, 1)
     if M <= GEMV_MAX_M:
         # batch-1 / tiny batches: stream the weights (gemv_kernel) with enough workgroups
         # (>= 512, two per CU) to keep ~64 KB of loads in flight per CU
@@ -308,7 +324,8 @@ def clear_plans() -> None:
 
 
 def autotune(shapes, weights: dict, device, iters: int = 6, log=None,
-             cold_bytes: int = 1 << 30, qkv_heads=None, candidates=None) -> dict:
+             cold_bytes: int = 1 << 30, qkv_heads=None, candidates=None,
+             normed_in=()) -> dict:
     """Measure every candidate plan for each (M, N, K, epi) and pin the fastest
     ("measure, don't guess"). ``weights[(N, K)]`` is a real [N, K] weight of that shape.
 
@@ -322,6 +339,8 @@ def autotune(shapes, weights: dict, device, iters: int = 6, log=None,
     RoPE, KV write), so its candidates are timed with the RoPE + cache-write kernel of the
     same input (``ops.linear_rope_cache``) instead of the add + RMSNorm one.
     ``candidates(M, N, K, epi)`` replaces the plan list (``prefill_candidates``).
+    ``normed_in``: (N, K, epi) of the GEMMs whose input at M <= GEMV_MAX_M is a deferred
+    RMSNorm (``ops.NormedRows``: the batch-1 QKV and gate/up), timed with that prologue.
     Returns {shape: (plan, ms)}."""
     from .. import ops  # local import: ops imports this module
     out = {}
@@ -333,6 +352,9 @@ def autotune(shapes, weights: dict, device, iters: int = 6, log=None,
         n_copies = max(2, min(16, -(-cold_bytes // (w0.numel() * w0.element_size()))))
         ws_ = [w0] + [w0.clone() for _ in range(n_copies - 1)]
         x = (torch.randn(M, K, device=device) * 0.5).to(w0.dtype)
+        x_in = x
+        if M <= GEMV_MAX_M and (N, K, epi) in normed_in:
+            x_in = ops.NormedRows(x, torch.ones(K, dtype=w0.dtype, device=device), 1e-5)
         is_qkv = (epi == "splitk" and qkv_heads is not None
                   and N == (qkv_heads[0] + 2 * qkv_heads[1]) * qkv_heads[2])
         if epi == "splitk":
@@ -341,6 +363,8 @@ def autotune(shapes, weights: dict, device, iters: int = 6, log=None,
             # pass; timing the unsplit GEMM alone hid that pass and biased the choice
             res = torch.zeros(M, N, dtype=w0.dtype, device=device)
             nw = torch.ones(N, dtype=w0.dtype, device=device)
+        if epi == "res":
+            res_r = torch.zeros(M, N, dtype=w0.dtype, device=device)
         if is_qkv:
             from . import reference as R
             hq, hkv, hd = qkv_heads
@@ -366,13 +390,17 @@ def autotune(shapes, weights: dict, device, iters: int = 6, log=None,
             def run(p=p):
                 for w in ws_:
                     if is_qkv and decode_qkv:
-                        _qkv_decode(ops, x, w, p, pos, slots, cs, kc, vc, bt, ctx, hq, hkv,
+                        _qkv_decode(ops, x_in, w, p, pos, slots, cs, kc, vc, bt, ctx, hq, hkv,
                                     hd, sc)
+                    elif x_in is not x:
+                        ops.linear_normed(x_in, w, epi, plan=p)
                     elif is_qkv:
                         ops.linear_rope_cache(x, w, pos, slots, cs, kc, vc, hq, hkv, hd,
                                               plan=p)
                     elif epi == "splitk":
                         ops.linear_add_rmsnorm(x, w, res, nw, 1e-5, plan=p)
+                    elif epi == "res":
+                        ops.linear_residual(x, w, res_r, plan=p)
                     else:
                         ops._gemm_native(x, w, epi, plan=p)
             try:
@@ -479,6 +507,9 @@ def prefill_candidates(M: int, N: int, K: int, epi: str):
 
 
 def candidate_plans(M: int, N: int, K: int, epi: str):
+    if epi == "res":
+        return [GemmPlan("dli", t, 1) for t in GEMV_RES_TILES
+                if M <= GEMV_MAX_M and not (t == 32 and M > 1)]
     out = []
     # tiles kept out of the autotune candidates (DLI_GEMM_EXCLUDE="..." overrides, "" = none).
     # Default: 26 (256x224). It fills all 256 CUs on the gate/up GEMM and wins the isolated

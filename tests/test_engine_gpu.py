@@ -55,6 +55,50 @@ def test_continuous_batching_is_batch_invariant(gpu):
     assert many[1].output_ids == alone
 
 
+@pytest.mark.parametrize("name", ["llama-tiny", "llama-tiny128"])
+def test_batch1_deferred_norm_decode(gpu, name, monkeypatch):
+    """Batch-1 decode on the reduce-free GEMV chain (O / down add into the residual in their
+    epilogue, the next GEMV normalises in its prologue: models/model.py ``defer``) against
+    the split-K + reduce path: every step's logits agree until the first differing token,
+    and there the reference's top two logits are a near tie (the paths differ only in fp32
+    summation order, so a token can flip only where two logits are within rounding)."""
+    from distributed_llm_inferencing_amd import ops
+    from distributed_llm_inferencing_amd.models.model import TransformerLM
+    from distributed_llm_inferencing_amd.ops import gemm as G
+    monkeypatch.setenv("DLI_GEMM_AUTOTUNE", "0")
+    calls, logits = [], []
+    real = ops.linear_residual
+    monkeypatch.setattr(ops, "linear_residual", lambda *a, **k: (calls.append(1), real(*a, **k)))
+    real_sample = TransformerLM.sample
+
+    def spy(self, lg, b, generator=None):
+        logits.append(lg.float().cpu())
+        return real_sample(self, lg, b, generator=generator)
+    monkeypatch.setattr(TransformerLM, "sample", spy)
+    sp = SamplingParams(max_length=40, do_sample=False, ignore_eos=True)
+
+    def run(defer, prompt):
+        monkeypatch.setattr(G, "DEFER_NORM", defer)
+        G.clear_plans()
+        calls.clear(), logits.clear()
+        eng = LLMEngine(name, device="cuda", max_batch=4, max_model_len=128, num_blocks=64,
+                        seed=5, use_graphs=False)
+        toks = eng.generate([prompt], sp)[0].output_ids
+        assert bool(calls) == defer
+        return toks, list(logits)
+    for prompt in (IDS[:6], IDS[2:13]):
+        t1, l1 = run(True, prompt)
+        t0, l0 = run(False, prompt)
+        assert len(t1) == len(t0) and len(l1) == len(l0) >= len(t0)
+        n = next((i for i, (a, b) in enumerate(zip(t1, t0)) if a != b), len(t0))
+        for i in range(min(n + 1, len(l0))):
+            err = (l1[i] - l0[i]).abs().max().item()
+            assert err < 0.02 * l0[i].abs().max().item() + 0.02, (i, err)
+        if n < len(t0):
+            top = l0[n][0].topk(2).values
+            assert (top[0] - top[1]).item() < 0.02 * top[0].abs().item() + 0.02, (n, top)
+
+
 def test_llama3_8b_smoke(gpu):
     eng = LLMEngine("llama3-8b", device="cuda", max_batch=4, max_model_len=256,
                     num_blocks=64, seed=0)

@@ -283,6 +283,88 @@ def test_gemv_in_launch_add_rmsnorm(gpu, M, N, K):
     ops._FUSED_GEMV_NORM = os.environ.get("DLI_GEMV_FUSED_NORM", "0") == "1"
 
 
+@pytest.mark.parametrize("M", [1, 2, 3, 4])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (4096, 14336), (1000, 768)])
+def test_gemv_residual_epilogue(gpu, M, N, K):
+    """Batch-1 decode O / down projection as one kernel (ops.linear_residual, epi "res"):
+    residual += x @ W^T with full K per workgroup == the fp32 reference rounded as
+    splitk_add_rmsnorm rounds (GEMM result to bf16, then the add); every tile (30 / 32 / 56 /
+    57) gives the same bits, since a row's K order does not depend on the row block; graph
+    replays equal eager."""
+    torch.manual_seed(5)
+    x, w, r0 = rnd(M, K, dev=gpu), rnd(N, K, dev=gpu, scale=0.05), rnd(M, N, dev=gpu)
+    ref = (r0.float() + R.linear(x, w, out_dtype=torch.float32).to(BF).float()).to(BF)
+    got = None
+    plans = G.candidate_plans(M, N, K, "res")
+    assert {p.tile for p in plans} >= {30, 56, 57} and all(p.splits == 1 for p in plans)
+    for p in plans:
+        res = r0.clone()
+        ops.linear_residual(x, w, res, plan=p)
+        close(res, ref, rtol=1e-2, atol=2e-2)
+        if got is None:
+            got = res
+        assert torch.equal(res, got), p
+    res_g = r0.clone()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        ops.linear_residual(x, w, res_g, plan=plans[-1])
+    res_g.copy_(r0)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(res_g, got)
+
+
+@pytest.mark.parametrize("M", [1, 2, 4])
+@pytest.mark.parametrize("N,K,epi", [(6144, 4096, "splitk"), (28672, 4096, "silu_mul"),
+                                     (96, 768, "silu_mul"), (1024, 2048, "none"),
+                                     (512, 8192, "none")])
+def test_gemv_norm_prologue(gpu, M, N, K, epi):
+    """A GEMV whose input is a deferred RMSNorm (ops.NormedRows): its prologue normalises
+    the raw residual rows into LDS, then streams the weights. == the fp32 reference of
+    (rmsnorm(residual) * w) @ W^T for every prologue tile: bf16 rows, SiLU*up (16-row
+    interleaved gate/up weight) and the fp32 split-K slabs the fused QKV consumer reads;
+    K = 8192 at M = 4 fills the 64 KB of LDS rows."""
+    torch.manual_seed(9)
+    r, nw, w = rnd(M, K, dev=gpu), rnd(K, dev=gpu), rnd(N, K, dev=gpu, scale=0.05)
+    xn = R.rmsnorm(r, nw, 1e-5)
+    h = ops.NormedRows(r, nw, 1e-5)
+    ran = 0
+    for tile in G.GEMV_PRO_TILES[epi]:
+        if tile in G.GEMV_PRO_M1_ONLY and M > 1:
+            continue
+        if epi == "splitk":
+            ref = R.linear(xn, w, out_dtype=torch.float32)
+            for splits in (2, 4):
+                ws = torch.empty(splits * M * N, dtype=torch.float32, device=gpu)
+                assert ops._gemv_prologue(h, w, "splitk", G.GemmPlan("dli", tile, splits), None,
+                                          N, ws=ws)
+                close(ws.view(splits, M, N).sum(0), ref, rtol=2e-2, atol=2e-2)
+                ran += 1
+            continue
+        ref = (R.silu_mul(R.linear(xn, w).float().to(BF)) if epi == "silu_mul"
+               else R.linear(xn, w, out_dtype=torch.float32))
+        for splits in (1, 2, 4):             # split K: slabs + the reduce kernel into C
+            if K % (64 * splits):
+                continue
+            G.set_plan(M, N, K, epi, G.GemmPlan("dli", tile, splits))
+            try:
+                out = ops.linear(h, w, epi=epi)
+            finally:
+                G.clear_plans()
+            close(out, ref, rtol=2e-2, atol=2e-2)
+            close(ops.linear_normed(h, w, epi, G.GemmPlan("dli", tile, splits)), ref,
+                  rtol=2e-2, atol=2e-2)
+            ran += 1
+    assert ran
+    # a plan without a prologue variant materialises the norm first: same values
+    G.set_plan(M, N, K, "none", G.GemmPlan("dli", 2, 1))
+    try:
+        out = ops.linear(h, w)
+    finally:
+        G.clear_plans()
+    close(out, R.linear(xn, w, out_dtype=torch.float32), rtol=2e-2, atol=2e-2)
+
+
 def test_prefill_autotune_pins_a_correct_plan(gpu):
     """StageRunner.autotune_prefill's measurement (ops.gemm.autotune over prefill_candidates:
     our 8-phase kernel vs hipBLASLt) pins one plan per shape, and whichever it pins computes

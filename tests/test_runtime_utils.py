@@ -409,3 +409,30 @@ def test_autotune_final_round_picks_the_lowest_median():
     assert G._final_round(FakeOps, [], 3, 1) is None
     one = [(2.0, plans["c"], lambda: "c")]
     assert G._final_round(FakeOps, one, 3, 1) == (plans["c"], 2.0)
+
+
+def test_deferred_norm_plans_and_cpu_gate():
+    """Batch-1 reduce-free decode (ops.linear_residual / ops.NormedRows): the "res" epilogue
+    is planned over the full-K GEMV tiles only; the prologue tiles are the GEMV tiles; on CPU
+    tensors the deferred path is off and a NormedRows input materialises to the reference."""
+    from distributed_llm_inferencing_amd import ops
+    from distributed_llm_inferencing_amd.ops import gemm as G
+    from distributed_llm_inferencing_amd.ops import reference as R
+    p1 = G.candidate_plans(1, 4096, 14336, "res")
+    assert {p.tile for p in p1} == {30, 32, 56, 57} and {p.splits for p in p1} == {1}
+    assert 32 not in {p.tile for p in G.candidate_plans(2, 4096, 4096, "res")}
+    assert G._heuristic(1, 4096, 4096, "res") == G.GemmPlan("dli", 56, 1)
+    assert G.tile_ok(56, "res") and G.tile_ok(57, "splitk") and not G.tile_ok(56, "silu_mul")
+    assert not G.tile_ok(29, "res") and not G.tile_ok(31, "res")
+    assert {56, 57} <= {p.tile for p in G.candidate_plans(1, 4096, 4096, "none")}
+    assert not {56, 57} & {p.tile for p in G.candidate_plans(8, 4096, 4096, "none")}
+    assert set(G.GEMV_PRO_TILES["silu_mul"]) <= set(G.GEMV_TILES)
+    torch.manual_seed(0)
+    r, nw, w = torch.randn(1, 64).bfloat16(), torch.randn(64).bfloat16(), torch.randn(96, 64).bfloat16()
+    assert not ops.deferred_norm_ok(r)
+    h = ops.NormedRows(r, nw, 1e-5)
+    assert torch.equal(ops.linear(h, w), R.linear(R.rmsnorm(r, nw, 1e-5), w))
+    res = torch.randn(1, 96).bfloat16()
+    want = res + R.linear(r, w)
+    ops.linear_residual(r, w, res)
+    assert torch.equal(res, want)
