@@ -40,7 +40,7 @@ struct NoPrologue {
 
 // PRE: the input rows are produced by `pro` (the RMSNorm prologue, into LDS): pro.issue()
 // requests the residual rows and norm weight, then this lane's first UNROLL weight steps are
-// requested (branch-free, clamped), then pro.complete() waits for the ROW loads only (they
+// requested (branch-free: clamped, the steps past the slice masked out of the sums), then pro.complete() waits for the ROW loads only (they
 // are older than the weight loads, so the counted wait leaves the weight stream in flight),
 // normalises into LDS and synchronises. The prologue's latency (rows from the Infinity
 // Cache, a block reduction, LDS stores) thus runs under the first weight requests.
@@ -72,7 +72,6 @@ __device__ __forceinline__ void gemv_core(const u16* __restrict__ A, int lda,
   int c = lane;
   if constexpr (PRE) {
     pro.issue();
-    const bool first = c + 64 * (UNROLL - 1) < nchunk;
     bf16x8v w[UNROLL][RW];
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u)
@@ -80,47 +79,42 @@ __device__ __forceinline__ void gemv_core(const u16* __restrict__ A, int lda,
       for (int r = 0; r < RW; ++r)
         w[u][r] = __builtin_nontemporal_load(wrow[r] + min(c + 64 * u, nchunk - 1));
     pro.complete();
-    if (first) {
 #pragma unroll
-      for (int m = 0; m < MB; ++m) {
+    for (int m = 0; m < MB; ++m) {
 #pragma unroll
-        for (int u = 0; u < UNROLL; ++u) {
+      for (int u = 0; u < UNROLL; ++u) {
+        if (c + 64 * u < nchunk) {
           const bf16x8v xv = xrow[m][c + 64 * u];
 #pragma unroll
           for (int r = 0; r < RW; ++r) acc[m][r] = dot8_acc(w[u][r], xv, acc[m][r]);
         }
       }
-      c += 64 * UNROLL;
     }
+    c += 64 * UNROLL;
   }
   // UNROLL 64-chunk steps per iteration: UNROLL * RW weight loads in flight per lane (the
   // short projections of a batch-1 layer run only a few iterations, so depth, not
-  // occupancy, hides the HBM latency)
-  for (; c + 64 * (UNROLL - 1) < nchunk; c += 64 * UNROLL) {
+  // occupancy, hides the HBM latency). The last, partial iteration issues all its loads at
+  // once too (indices clamped, the extra steps masked out of the sums): a step-at-a-time
+  // tail cost the K = 14336 down projection 4 serial HBM round trips (28 steps a lane at
+  // UNROLL 8). Sums stay in step order, as before.
+  for (; c < nchunk; c += 64 * UNROLL) {
     bf16x8v w[UNROLL][RW];
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u)
 #pragma unroll
-      for (int r = 0; r < RW; ++r) w[u][r] = __builtin_nontemporal_load(wrow[r] + c + 64 * u);
+      for (int r = 0; r < RW; ++r)
+        w[u][r] = __builtin_nontemporal_load(wrow[r] + min(c + 64 * u, nchunk - 1));
 #pragma unroll
     for (int m = 0; m < MB; ++m) {
 #pragma unroll
       for (int u = 0; u < UNROLL; ++u) {
-        const bf16x8v xv = xrow[m][c + 64 * u];
+        if (c + 64 * u < nchunk) {
+          const bf16x8v xv = xrow[m][c + 64 * u];
 #pragma unroll
-        for (int r = 0; r < RW; ++r) acc[m][r] = dot8_acc(w[u][r], xv, acc[m][r]);
+          for (int r = 0; r < RW; ++r) acc[m][r] = dot8_acc(w[u][r], xv, acc[m][r]);
+        }
       }
-    }
-  }
-  for (; c < nchunk; c += 64) {
-    bf16x8v w0[RW];
-#pragma unroll
-    for (int r = 0; r < RW; ++r) w0[r] = __builtin_nontemporal_load(wrow[r] + c);
-#pragma unroll
-    for (int m = 0; m < MB; ++m) {
-      const bf16x8v x0 = xrow[m][c];
-#pragma unroll
-      for (int r = 0; r < RW; ++r) acc[m][r] = dot8_acc(w0[r], x0, acc[m][r]);
     }
   }
 #pragma unroll
