@@ -83,10 +83,14 @@ __device__ __forceinline__ void gemv_core(const u16* __restrict__ A, int lda,
     for (int m = 0; m < MB; ++m) {
 #pragma unroll
       for (int u = 0; u < UNROLL; ++u) {
-        if (c + 64 * u < nchunk) {
-          const bf16x8v xv = xrow[m][c + 64 * u];
+        // branch-free mask: a branch here made the compiler sink the x loads into it, each
+        // behind a full vmcnt(0) wait (8 serial loads per iteration at UNROLL 8)
+        const bool ok = c + 64 * u < nchunk;
+        const bf16x8v xv = xrow[m][min(c + 64 * u, nchunk - 1)];
 #pragma unroll
-          for (int r = 0; r < RW; ++r) acc[m][r] = dot8_acc(w[u][r], xv, acc[m][r]);
+        for (int r = 0; r < RW; ++r) {
+          const float a = dot8_acc(w[u][r], xv, acc[m][r]);
+          acc[m][r] = ok ? a : acc[m][r];
         }
       }
     }
@@ -94,11 +98,29 @@ __device__ __forceinline__ void gemv_core(const u16* __restrict__ A, int lda,
   }
   // UNROLL 64-chunk steps per iteration: UNROLL * RW weight loads in flight per lane (the
   // short projections of a batch-1 layer run only a few iterations, so depth, not
-  // occupancy, hides the HBM latency). The last, partial iteration issues all its loads at
-  // once too (indices clamped, the extra steps masked out of the sums): a step-at-a-time
-  // tail cost the K = 14336 down projection 4 serial HBM round trips (28 steps a lane at
-  // UNROLL 8). Sums stay in step order, as before.
-  for (; c < nchunk; c += 64 * UNROLL) {
+  // occupancy, hides the HBM latency). Full iterations address by immediate offsets from one
+  // base; the last, partial one issues all its loads at once too (indices clamped, the
+  // extra steps masked out of the sums by selects — a branch let the compiler sink the x
+  // loads into it, each behind a vmcnt(0)): a step-at-a-time tail cost the K = 14336 down
+  // projection 4 serial HBM round trips (28 steps a lane at UNROLL 8). Sums stay in step
+  // order.
+  for (; c + 64 * (UNROLL - 1) < nchunk; c += 64 * UNROLL) {
+    bf16x8v w[UNROLL][RW];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u)
+#pragma unroll
+      for (int r = 0; r < RW; ++r) w[u][r] = __builtin_nontemporal_load(wrow[r] + c + 64 * u);
+#pragma unroll
+    for (int m = 0; m < MB; ++m) {
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+        const bf16x8v xv = xrow[m][c + 64 * u];
+#pragma unroll
+        for (int r = 0; r < RW; ++r) acc[m][r] = dot8_acc(w[u][r], xv, acc[m][r]);
+      }
+    }
+  }
+  if (c < nchunk) {
     bf16x8v w[UNROLL][RW];
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u)
@@ -109,10 +131,12 @@ __device__ __forceinline__ void gemv_core(const u16* __restrict__ A, int lda,
     for (int m = 0; m < MB; ++m) {
 #pragma unroll
       for (int u = 0; u < UNROLL; ++u) {
-        if (c + 64 * u < nchunk) {
-          const bf16x8v xv = xrow[m][c + 64 * u];
+        const bool ok = c + 64 * u < nchunk;
+        const bf16x8v xv = xrow[m][min(c + 64 * u, nchunk - 1)];
 #pragma unroll
-          for (int r = 0; r < RW; ++r) acc[m][r] = dot8_acc(w[u][r], xv, acc[m][r]);
+        for (int r = 0; r < RW; ++r) {
+          const float a = dot8_acc(w[u][r], xv, acc[m][r]);
+          acc[m][r] = ok ? a : acc[m][r];
         }
       }
     }
