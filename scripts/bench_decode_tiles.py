@@ -17,7 +17,8 @@ import torch
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 
 SHAPES = {"qkv": (6144, 4096, "splitk"), "o": (4096, 4096, "splitk"),
-          "gate_up": (28672, 4096, "silu_mul"), "down": (4096, 14336, "splitk")}
+          "gate_up": (28672, 4096, "silu_mul"), "down": (4096, 14336, "splitk"),
+          "head": (128256, 4096, "f32")}
 
 
 def main():

@@ -164,8 +164,17 @@ def test_real_shape_engine_decode(gpu, name, monkeypatch):
 def test_mixed_steps_token_identical_on_gpu(gpu, monkeypatch):
     """Prompts arriving while others decode: the mixed prefill+decode steps (decode rows on
     the decode kernel, prompt rows on the paged prefill kernel, one GEMM pass) produce the
-    tokens of the engine without mixed steps; graphs and lookahead on."""
+    tokens of the engine without mixed steps; graphs and lookahead on. The reduce-free
+    batch-1 chain (models/model.py ``defer``, M <= 4 decode steps only) sums in another order
+    than the split-K path a mixed step's decode rows take, so it is off here: the
+    invariant is the mixed step's own (its numerics: test_batch1_deferred_norm_decode).
+    Token identity across the two paths is itself a rounding question (a mixed step's decode
+    rows take the MFMA tiles, a decode-only step the weight-streaming GEMVs): it holds with
+    the decode plans the tier's earlier engine tests leave autotuned; run alone, on the
+    heuristic plans, one sampled token of 200 flips (profiles/r5/README.md §14)."""
+    from distributed_llm_inferencing_amd.ops import gemm as G
     monkeypatch.setenv("DLI_GEMM_AUTOTUNE", "0")
+    monkeypatch.setattr(G, "DEFER_NORM", False)
     waves = [[IDS[:5], IDS[:9], IDS[3:14]], [IDS[:2], IDS[1:4]], [IDS[2:11]]]
     sp = SamplingParams(max_length=40, seed=7, ignore_eos=True)
     res = []
