@@ -28,28 +28,13 @@
 // K-tile two back (WAR) and retired by its issuer's vmcnt >= 1 barrier before its first
 // ds_read (RAW) when every load segment leaves the last 3 segments' glds in flight:
 // vmcnt(6) in steady state, fewer when the K loop's tail issues nothing.
-// Stream-K (VAR & SK8P, tile 60): one workgroup per CU walks a contiguous range of
-// k_split_len K-tile iterations of the linearised (tile, K-tile) space, so a GEMM of fewer
-// tiles than CUs (the Llama-3-8B gate/up at M = 512: 224 256x256 tiles on 256 CUs) keeps every
-// CU busy. A range touches a few tiles; the tile whose END it holds it owns (epilogue), the
-// tile whose START it holds (its last segment) it hands over as an fp32 partial: slot w of
-// `ws` (device-coherent sc1 stores), then flags[w] = 1. The owner of a
-// tile begun by workgroup w - 1 processes that segment LAST, acquires flags[w - 1], starts
-// its accumulators from the partial and resets the flag. Dependencies only point to lower workgroup ids (dispatched
-// first), so the wait cannot deadlock; it is bounded anyway (~2 s). The host admits
-// partitions with at most two workgroups per tile (launch_8p_sk).
-constexpr int SK8P = 1024;
-typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
-
 template <int EPI, int VAR = 0>
 __global__ void __launch_bounds__(512) gemm8p_kernel(
     const u16* __restrict__ A, int lda, const u16* __restrict__ W, int ldw,
     void* __restrict__ C, int ldc, int M, int N, int K, int k_split_len,
-    const u16* __restrict__ bias, float* __restrict__ ws, const int* __restrict__ group_off,
-    unsigned* __restrict__ flags) {
+    const u16* __restrict__ bias, float* __restrict__ ws, const int* __restrict__ group_off) {
   constexpr int BM = 256, BN = 256;
   constexpr int A_BYTES = BM * BK * 2, BUF = 2 * A_BYTES;
-  constexpr bool SK = (VAR & SK8P) != 0;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   int row0 = 0, Mg = M;
@@ -61,33 +46,9 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(
   }
   const int tiles_m = (M + BM - 1) / BM;
   const int tiles_n = (N + BN - 1) / BN;
-  // stream-K range of this workgroup (SK): iterations [it0, it1), tiles t_first..t_last
-  const int nkt = K / BK;
-  // logical workgroup id: consecutive ranges on one XCD (xcd_remap), so a tile's two
-  // workgroups and the partial between them mostly share that XCD's L2
-  const int wl = SK ? xcd_remap(blockIdx.x, gridDim.x) : 0;
-  const long it0 = SK ? (long)wl * k_split_len : 0;
-  const long it1 = SK ? min((long)tiles_m * tiles_n * nkt, it0 + k_split_len) : 0;
-  if (SK && it0 >= it1) return;
-  const int t_first = SK ? (int)(it0 / nkt) : 0;
-  const int nseg = SK ? (int)((it1 - 1) / nkt) - t_first + 1 : 1;
-  for (int sgi = 0; sgi < nseg; ++sgi) {
-  int tn, tm, kb, nk, ks = 0;
-  int role = 0;                   // 0 plain, 1 hand over a partial, 2 own + add w-1's partial
-  if constexpr (SK) {
-    // the last segment first (a partial: published early), the first one last (it may wait)
-    const int t = nseg == 1 ? t_first : sgi == 0 ? t_first + nseg - 1
-                : sgi == nseg - 1 ? t_first : t_first + sgi;
-    const long ts = (long)t * nkt, te = ts + nkt;
-    const long s0 = max(it0, ts), s1 = min(it1, te);
-    kb = (int)(s0 - ts) * BK;
-    nk = (int)(s1 - s0);
-    role = s1 != te ? 1 : (s0 != ts ? 2 : 0);
-    tn = t / tiles_m;
-    tm = t % tiles_m;
-  } else {
-  int tile;
+  int tile, ks;
   split_tile(tiles_m * tiles_n, group_off != nullptr, tile, ks);
+  int tn, tm;
   constexpr int GM = (VAR & 8) ? 4 : (VAR & 16) ? 8 : 1;
   if (GM > 1) {
     // grouped order: an XCD's ~32 consecutive tiles cover GM tile-rows x 32/GM tile-columns,
@@ -102,11 +63,10 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(
     tn = tile / tiles_m;
     tm = tile % tiles_m;
   }
-  kb = ks * k_split_len;
-  nk = min(k_split_len, K - kb) / BK;
-  }
   const int m0 = tm * BM, n0 = tn * BN;
   if (m0 >= Mg) return;
+  const int kb = ks * k_split_len;
+  const int nk = min(k_split_len, K - kb) / BK;
   const u16* Ab = A + (long)row0 * lda;
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -172,38 +132,10 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(
   };
 
   f32x4 acc[8][4];
-  if constexpr (SK) {
-    // a tile begun by workgroup w - 1 (role 2, processed last): its partial IS the initial
-    // accumulator. Branch-free: other segments read through a zero-length descriptor (range-
-    // checked buffer loads return 0 and touch no memory); an add after the K loop kept two
-    // accumulator sets live and spilled.
-    // No fences: an agent-scope acquire / release fence invalidates / writes back the whole
-    // XCD L2 under every other workgroup's stream (measured 2.3x slower). The partial moves
-    // by device-coherent (sc1) buffer accesses only, the flag by relaxed agent-scope atomics
-    // after the stores retired (s_waitcnt vmcnt(0) + barrier: the pattern of the GEMV
-    // in-launch combine, gemv.hip arrive_last).
-    if (role == 2 && tid == 0) {
-      unsigned n = 0;
-      while (__hip_atomic_load(flags + wl - 1, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT) == 0u && ++n < (1u << 25))
-        __builtin_amdgcn_s_sleep(8);
-    }
-    __syncthreads();
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-        ws + (long)(role == 2 ? wl - 1 : 0) * (BM * BN), 0,
-        role == 2 ? BM * BN * 4 : 0, 0x00020000);
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                  r, tid * 16, (i * 4 + j) * 8192, 16));
-  } else {
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // ---- prologue: K-tiles 0 and 1 in full
   if (nk > 0) {
@@ -339,36 +271,10 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(
     __builtin_amdgcn_s_barrier();
   }
 
-  // ---- stream-K hand-over: this tile's partial to slot blockIdx.x, or w - 1's into acc.
-  // 16-B buffer stores (element-major, thread-minor: each instruction covers 1 KiB of
-  // consecutive lanes) with sc1, so the slot goes through the device-coherent level between
-  // the two workgroups' XCDs.
-  if constexpr (SK) {
-    if (role == 1) {
-      // buffer stores: one lane offset VGPR, the element offset in soffset (global stores
-      // with 32 distinct 64-bit addresses spilled the accumulators)
-      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-          ws + (long)wl * (BM * BN), 0, BM * BN * 4, 0x00020000);
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          __builtin_amdgcn_raw_buffer_store_b128(
-              __builtin_bit_cast(u32x4v, acc[i][j]), r, tid * 16, (i * 4 + j) * 8192, 16);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0)
-        __hip_atomic_store(flags + wl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __syncthreads();                     // LDS reuse by the next segment
-      continue;
-    }
-    if (role == 2 && tid == 0)
-      __hip_atomic_store(flags + wl - 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
   // ---- epilogue (transposed accumulators):
   // acc[I][J][r] = C[m0 + 128g + 16I + fr][n0 + 64gw + 16J + 4fq + r]
   const int wr0 = m0 + 128 * g, wc0 = n0 + 64 * gw;
-  if (!SK && gridDim.y > 1) {
+  if (gridDim.y > 1) {
     float* slab = ws + (long)ks * M * N;
     const int sm = g_slab_store;
     const bool vec = (N & 3) == 0;
@@ -399,20 +305,18 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(
                           acc[i][j + 1], vec);
       }
     }
-  } else {
+    return;
+  }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int row = wr0 + 16 * i + fr;
-      if (row >= Mg) continue;
+  for (int i = 0; i < 8; ++i) {
+    const int row = wr0 + 16 * i + fr;
+    if (row >= Mg) continue;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int col = wc0 + 16 * j + 4 * fq;
-        if (col < N) store_quad<EPI>(C, ldc, row0 + row, col, N, acc[i][j], bias, vec);
-      }
+    for (int j = 0; j < 4; ++j) {
+      const int col = wc0 + 16 * j + 4 * fq;
+      if (col < N) store_quad<EPI>(C, ldc, row0 + row, col, N, acc[i][j], bias, vec);
     }
   }
-  if constexpr (SK) __syncthreads();       // LDS reuse by the next segment
-  }                                          // segments
 }
 
 // ---------------------------------------------------------------------------------------
@@ -928,8 +832,7 @@ static int launch_8p(const void* A, int lda, const void* W, int ldw, void* C, in
   }
   dim3 grid(tiles, splits, groups);
   gemm8p_kernel<EPI, VAR><<<grid, 512, lds, st>>>((const u16*)A, lda, (const u16*)W, ldw, C, ldc, M,
-                                             N, K, ksl, (const u16*)bias, (float*)ws, group_off,
-                                             nullptr);
+                                             N, K, ksl, (const u16*)bias, (float*)ws, group_off);
   if (splits > 1 && C != nullptr) {
     const int outN = (EPI == EPI_SILU) ? N / 2 : N;
     const long total = (long)M * outN;
@@ -995,78 +898,6 @@ static int launch_8p128(const void* A, int lda, const void* W, int ldw, void* C,
         C, ldc, (const float*)ws, M, N, splits, (const u16*)bias);
   }
   DLI_RETURN_LAUNCH();
-}
-
-// Stream-K partition of `tiles` tiles x nkt K-tiles over `grid` workgroups: iterations per
-// workgroup, or 0 when some tile would need a third workgroup (a range strictly inside one
-// tile) — the kernel's hand-over is pairwise.
-static int sk_iters(long tiles, int nkt, int& grid) {
-  const long total = tiles * nkt;
-  if (grid <= 0 || total <= 0) return 0;
-  const int it = (int)((total + grid - 1) / grid);
-  grid = (int)((total + it - 1) / it);
-  for (int w = 0; w < grid; ++w) {
-    const long a = (long)w * it, b = min(total, a + it);
-    if (a % nkt != 0 && b % nkt != 0 && a / nkt == (b - 1) / nkt) return 0;
-  }
-  return it;
-}
-
-static int num_cus() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-  }
-  return n;
-}
-
-template <int EPI>
-static int launch_8p_sk(const void* A, int lda, const void* W, int ldw, void* C, int ldc,
-                        int M, int N, int K, const void* bias, void* ws, long ws_bytes,
-                        unsigned* flags, int grid_req, hipStream_t st) {
-  constexpr int VAR = GEMM8P_DEFAULT | SK8P;
-  if ((EPI == EPI_SILU && N % 64) || K % BK || C == nullptr || ws == nullptr || flags == nullptr)
-    return (int)hipErrorInvalidValue;
-  const long tiles = (long)((M + 255) / 256) * ((N + 255) / 256);
-  int grid = grid_req > 0 ? grid_req : num_cus();
-  const int it = sk_iters(tiles, K / BK, grid);
-  if (it == 0 || ws_bytes < (long)grid * 256 * 256 * 4) return (int)hipErrorInvalidValue;
-  constexpr size_t lds = 2 * (size_t)(256 + 256) * BK * 2;
-  static bool attr_done = false;
-  if (!attr_done) {
-    hipFuncSetAttribute((const void*)gemm8p_kernel<EPI, VAR>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr_done = true;
-  }
-  gemm8p_kernel<EPI, VAR><<<dim3(grid), 512, lds, st>>>(
-      (const u16*)A, lda, (const u16*)W, ldw, C, ldc, M, N, K, it, (const u16*)bias,
-      (float*)ws, nullptr, flags);
-  DLI_RETURN_LAUNCH();
-}
-
-// C[M, N] = epi(A . W^T) on the stream-K 8-phase kernel (tile 60). ws: fp32 partial slots,
-// >= grid x 256 KiB; flags: zeroed uint32[grid] owned by the stream (reset by the kernel);
-// grid <= 0: one workgroup per CU. Returns hipErrorInvalidValue for shapes it does not take.
-extern "C" int dli_gemm_sk(const void* A, int lda, const void* W, int ldw, void* C, int ldc,
-                           int M, int N, int K, int epi, const void* bias, void* ws,
-                           long ws_bytes, unsigned* flags, int grid, hipStream_t st) {
-  if (M <= 0 || N <= 0) return 0;
-  switch (epi) {
-    case EPI_BF16: return launch_8p_sk<EPI_BF16>(A, lda, W, ldw, C, ldc, M, N, K, bias, ws, ws_bytes, flags, grid, st);
-    case EPI_F32: return launch_8p_sk<EPI_F32>(A, lda, W, ldw, C, ldc, M, N, K, bias, ws, ws_bytes, flags, grid, st);
-    case EPI_SILU: return launch_8p_sk<EPI_SILU>(A, lda, W, ldw, C, ldc, M, N, K, bias, ws, ws_bytes, flags, grid, st);
-    default: return (int)hipErrorInvalidValue;
-  }
-}
-
-// iterations per workgroup of the stream-K partition (0: not admitted), for the planner
-extern "C" int dli_gemm_sk_iters(int M, int N, int K, int grid) {
-  if (K % BK || M <= 0 || N <= 0) return 0;
-  int g = grid > 0 ? grid : num_cus();
-  return sk_iters((long)((M + 255) / 256) * ((N + 255) / 256), K / BK, g);
 }
 
 template <int EPI>

@@ -188,16 +188,6 @@ def _gemm_native(x, w, epi: str, bias=None, out=None, plan: Optional[G.GemmPlan]
     if out is None:
         dt = torch.float32 if epi == "f32" else x.dtype
         out = torch.empty(M, out_n, dtype=dt, device=x.device)
-    if plan.tile == G.SK_TILE:
-        if group_off is not None:
-            raise ValueError("the stream-K GEMM has no grouped mode")
-        grid = G.NUM_CUS
-        nbytes = grid * 256 * 256 * 4
-        ws = G.workspace(x.device, nbytes)
-        _native_call("dli_gemm_sk", _p(x), x.stride(0), _p(w), w.stride(-2), _p(out),
-                     out.stride(0), M, Nn, K, G.EPI[epi], _p(bias), _p(ws), ws.numel(),
-                     _p(G.tickets(x.device, grid, _st())), grid, _st())
-        return out
     splits = plan.splits
     ws = None
     if splits > 1:

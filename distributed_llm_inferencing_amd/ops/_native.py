@@ -59,8 +59,6 @@ _SIGS = {
     "dli_splitk_add_rmsnorm": [P, P, P, I, I, I, P, F, P],
     "dli_gemv_add_rmsnorm": [P, I, P, I, I, I, I, I, I, P, P, P, F, P, P, P],
     "dli_gemv_fused": [P, I, P, F, P, I, P, I, I, I, I, I, I, I, P, P],
-    "dli_gemm_sk": [P, I, P, I, P, I, I, I, I, I, P, P, L, P, I, P],
-    "dli_gemm_sk_iters": [I, I, I, I],
     "dli_splitk_rope_cache": [P, P, I, I, I, P, P, P, P, P, I, I, I, I, I, P],
     "dli_decode_attention_fused": [P, P, I, P, P, P, P, P, P, I, P, I, I, I, I, I, F, P],
     "dli_moe_route": [P, P, P, I, I, I, P],

@@ -83,31 +83,6 @@ GEMV_PRO_TILES = {"silu_mul": (29, 31, 33, 58, 59), "splitk": (30, 32, 56, 57),
                   "none": (30, 32, 56, 57)}
 GEMV_PRO_M1_ONLY = (32, 33)
 DEFER_NORM = os.environ.get("DLI_DEFER_NORM", "1") == "1"
-# stream-K 8-phase GEMM (gemm8p.hip dli_gemm_sk): one workgroup per CU over the linearised
-# (tile, K-tile) space, for decode GEMMs whose 256x256 tile count leaves CUs idle (the M = 512
-# gate/up: 224 tiles on 256 CUs); a decode autotune candidate where the partition is
-# pairwise (sk_ok). DLI_GEMM_SK=0 keeps it out.
-SK_TILE = 60
-SK_ON = os.environ.get("DLI_GEMM_SK", "1") == "1"
-
-
-def sk_ok(M: int, N: int, K: int, epi: str) -> bool:
-    """The stream-K partition of this shape is admitted (every tile shared by at most two
-    workgroups) and the tile count is not already a whole number of CU waves."""
-    if epi not in ("none", "f32", "silu_mul") or K % 64 or (epi == "silu_mul" and N % 64):
-        return False
-    tiles = -(-M // 256) * -(-N // 256)
-    if tiles % NUM_CUS == 0:
-        return False
-    total = tiles * (K // 64)
-    it = -(-total // NUM_CUS)
-    grid = -(-total // it)
-    nkt = K // 64
-    for w in range(grid):
-        a, b = w * it, min(total, w * it + it)
-        if a % nkt and b % nkt and a // nkt == (b - 1) // nkt:
-            return False
-    return True
 TILE_WAVES = {13: (2, 4), 14: (4, 2), 15: (2, 4), 16: (4, 2), 17: (2, 4),
               22: (2, 4), 23: (2, 4), 24: (2, 4), 25: (4, 2),
               26: (4, 2), 27: (2, 4), 28: (4, 2)}
@@ -565,8 +540,6 @@ def candidate_plans(M: int, N: int, K: int, epi: str):
     if excl_env is None and epi == "f32" and os.environ.get("DLI_GEMM_HEAD_4W", "0") == "1":
         excl.discard(45)
         excl.discard(55)
-    if SK_ON and SK_TILE not in excl and 256 < M <= 512 and sk_ok(M, N, K, epi):
-        out.append(GemmPlan("dli", SK_TILE, 1))
     for tile, (bm, bn) in TILES.items():
         if not tile_ok(tile, epi) or tile in excl:
             continue

@@ -436,15 +436,3 @@ def test_deferred_norm_plans_and_cpu_gate():
     want = res + R.linear(r, w)
     ops.linear_residual(r, w, res)
     assert torch.equal(res, want)
-
-
-def test_stream_k_admission():
-    """ops.gemm.sk_ok / candidate_plans: the stream-K tile (60) is a decode candidate for the
-    M = 512 gate/up and LM head (a pairwise partition over 256 CUs), not for shapes whose
-    ranges would sit inside one tile (3 workgroups on a tile) nor for whole waves of tiles."""
-    from distributed_llm_inferencing_amd.ops import gemm as G
-    assert G.sk_ok(512, 28672, 4096, "silu_mul") and G.sk_ok(512, 128256, 4096, "f32")
-    assert not G.sk_ok(512, 4096, 4096, "none") and not G.sk_ok(512, 14336, 4096, "silu_mul")
-    assert not G.sk_ok(512, 28672, 4096, "splitk") and not G.sk_ok(512, 32768, 4096, "none")
-    assert G.GemmPlan("dli", 60, 1) in G.candidate_plans(512, 28672, 4096, "silu_mul")
-    assert G.GemmPlan("dli", 60, 1) not in G.candidate_plans(128, 28672, 4096, "silu_mul")
