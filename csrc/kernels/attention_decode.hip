@@ -263,16 +263,7 @@ __global__ void __launch_bounds__(256, MINW) decode_attn_kernel(
 // LDS (each wave's V-tile rows are reused for its O partial) and the workgroup writes the
 // GQA group's output rows. Small batches: with one item per wave most of the chip idles and
 // each wave pays one HBM round trip per tile of the whole context.
-// 16-B store that writes through to the device-coherent level (sc1): rows another
-// workgroup of the same launch reads (decode_attn_o_kernel)
-__device__ __forceinline__ void store8_sc1(u16* p, const float* f) {
-  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  const u32x4 v = {pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]),
-                   pack2bf(f[6], f[7])};
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-}
-
-template <int WPI, bool SC1 = false>
+template <int WPI>
 __device__ __forceinline__ void decode_attn_wg(
     const bf16x8 (&qf)[4], u16 (*vtile_all)[DEC_TILE * 144], float (*ml_all)[16][2], int wv,
     int lane, int b, int kvh, int G, int s_begin, int s_end, int bt_lane0,
@@ -320,8 +311,7 @@ __device__ __forceinline__ void decode_attn_wg(
   const float inv = den > 0.f ? 1.f / den : 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) acc[j] *= inv;
-  if (SC1) store8_sc1(out + ((long)b * hq + kvh * G + h) * HD + d0, acc);
-  else store8(out + ((long)b * hq + kvh * G + h) * HD + d0, acc);
+  store8(out + ((long)b * hq + kvh * G + h) * HD + d0, acc);
 }
 
 // Small-batch form of decode_attn_kernel (head dim 128, one KV split): a workgroup per item.
@@ -372,26 +362,26 @@ __global__ void __launch_bounds__(256) decode_attn_wg_kernel(
 // trip per 32-token tile): wave 0 writes the new k/v row, every wave builds the Q fragments,
 // wave w takes the w-th quarter of the context's tiles, and the four partial (m, l, O) merge
 // through LDS (the V-tile rows are reused for the O partials).
-// One (sequence, kv head) item of the fused decode attention (decode_attn_fused_kernel, and
-// the attention role of decode_attn_o_kernel).
-template <int SPL, int WPI, bool SC1 = false>
-__device__ __forceinline__ void decode_attn_fused_item(
-    int item, u16 (*vtile_all)[DEC_TILE * 144], float (*ml_all)[16][2],
+template <int SPL, int WPI>
+__global__ void __launch_bounds__(256, 4) decode_attn_fused_kernel(
     u16* __restrict__ out, const void* __restrict__ src, int N,
     const int* __restrict__ positions, const int* __restrict__ slot_mapping,
     const float* __restrict__ cos_sin, u16* __restrict__ k_cache, u16* __restrict__ v_cache,
     const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ context_lens,
     int B, int hq, int hkv, int block_size, float scale_log2) {
-  constexpr int HD = 128, HALF = 64, KK = HD / 32, DB = HD / 16;
-  (void)DB;
+  constexpr int HD = 128, HALF = 64, KK = HD / 32, VROW = HD + 16, DB = HD / 16;
   // SPL > 0: src = the QKV GEMM's fp32 split-K slabs [SPL, B, N]; SPL == 0: the bf16 QKV rows
   // [B, N] of an unsplit GEMM (the same prologue minus the slab sum)
   const float* ws = static_cast<const float*>(src);
   const u16* qkv = static_cast<const u16*>(src);
   static_assert(WPI == 1 || WPI == DEC_WAVES, "one item per wave or per workgroup");
+  __shared__ __attribute__((aligned(16))) u16 vtile_all[DEC_WAVES][DEC_TILE * VROW];
+  __shared__ float ml_all[WPI > 1 ? WPI : 1][16][2];
   const int wv = threadIdx.x >> 6;
   u16* vt = vtile_all[wv];
   const int lane = threadIdx.x & 63;
+  const int item = WPI > 1 ? (int)blockIdx.x : (int)blockIdx.x * DEC_WAVES + wv;
+  if (item >= B * hkv) return;                                 // wave-uniform exit (WPI 1)
   const int kvh = item % hkv, b = item / hkv;
   const int col = lane & 15, grp = lane >> 4;
   const int G = hq / hkv;
@@ -482,121 +472,9 @@ __device__ __forceinline__ void decode_attn_fused_item(
                          nullptr, bt0);
   } else {
     __syncthreads();                       // wave 0's cache row visible to the other waves
-    decode_attn_wg<WPI, SC1>(qf, vtile_all, ml_all, wv, lane, b, kvh, G, s_begin, s_end, bt0,
-                             out, k_cache, v_cache, block_tables, max_blocks, hq, hkv,
-                             block_size, scale_log2);
-  }
-}
-
-template <int SPL, int WPI>
-__global__ void __launch_bounds__(256, 4) decode_attn_fused_kernel(
-    u16* __restrict__ out, const void* __restrict__ src, int N,
-    const int* __restrict__ positions, const int* __restrict__ slot_mapping,
-    const float* __restrict__ cos_sin, u16* __restrict__ k_cache, u16* __restrict__ v_cache,
-    const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ context_lens,
-    int B, int hq, int hkv, int block_size, float scale_log2) {
-  __shared__ __attribute__((aligned(16))) u16 vtile_all[DEC_WAVES][DEC_TILE * 144];
-  __shared__ float ml_all[WPI > 1 ? WPI : 1][16][2];
-  const int item = WPI > 1 ? (int)blockIdx.x : (int)blockIdx.x * DEC_WAVES + (threadIdx.x >> 6);
-  if (item >= B * hkv) return;                                 // wave-uniform exit (WPI 1)
-  decode_attn_fused_item<SPL, WPI>(item, vtile_all, ml_all, out, src, N, positions,
-                                   slot_mapping, cos_sin, k_cache, v_cache, block_tables,
-                                   max_blocks, context_lens, B, hq, hkv, block_size,
-                                   scale_log2);
-}
-
-// ---------------------------------------------------------------------------------------
-// Batch-1 decode: the fused attention AND the O projection in one launch (M <= 4 rows).
-// Workgroups [0, items) are the attention items (one (sequence, kv head) per workgroup, as
-// decode_attn_fused_kernel's small-batch form); they write their output rows through to the
-// device-coherent level (sc1) and count themselves in sync[0]. Workgroups [items, items + nO)
-// are the O GEMV (one Wo row per wave, full K, tile 56's layout): each first requests its
-// whole weight row (STEPS 16-B chunks a lane — the O weights stream while the attention
-// runs), then waits for sync[0] == items, reads the attention rows with device-scope loads
-// into LDS (the attention tiles' LDS, unused in this role) and adds its dot products into
-// the residual (bf16(residual + bf16(acc)), the reduce's rounding; the same K order as
-// ops.linear_residual). Every dependency points to lower workgroup ids, which the hardware
-// dispatches first, so the waits cannot deadlock at any residency; they are bounded anyway.
-// The last O workgroup to finish resets sync[0..1] for the next launch.
-__device__ __forceinline__ float dot8_bf16(const bf16x8 w, const bf16x8 x, float acc) {
-  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(w, w, 0, 1),
-                                        __builtin_shufflevector(x, x, 0, 1), acc, false);
-  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(w, w, 2, 3),
-                                        __builtin_shufflevector(x, x, 2, 3), acc, false);
-  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(w, w, 4, 5),
-                                        __builtin_shufflevector(x, x, 4, 5), acc, false);
-  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(w, w, 6, 7),
-                                        __builtin_shufflevector(x, x, 6, 7), acc, false);
-  return acc;
-}
-
-template <int SPL, int STEPS>
-__global__ void __launch_bounds__(256, 4) decode_attn_o_kernel(
-    u16* __restrict__ attn, const void* __restrict__ src, int N,
-    const int* __restrict__ positions, const int* __restrict__ slot_mapping,
-    const float* __restrict__ cos_sin, u16* __restrict__ k_cache, u16* __restrict__ v_cache,
-    const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ context_lens,
-    int B, int hq, int hkv, int block_size, float scale_log2, const u16* __restrict__ Wo,
-    int ldw, u16* __restrict__ residual, int ldr, int No, unsigned* __restrict__ sync) {
-  __shared__ __attribute__((aligned(16))) u16 vtile_all[DEC_WAVES][DEC_TILE * 144];
-  __shared__ float ml_all[DEC_WAVES][16][2];
-  const int items = B * hkv;
-  if ((int)blockIdx.x < items) {
-    decode_attn_fused_item<SPL, DEC_WAVES, true>(
-        blockIdx.x, vtile_all, ml_all, attn, src, N, positions, slot_mapping, cos_sin, k_cache,
-        v_cache, block_tables, max_blocks, context_lens, B, hq, hkv, block_size, scale_log2);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // this thread's rows written through
-    __syncthreads();
-    if (threadIdx.x == 0)
-      __hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  const int nO = (int)gridDim.x - items;
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int n = ((int)blockIdx.x - items) * 4 + wid;       // this wave's Wo row / output column
-  const int K = hq * 128, nchunk = K >> 3;
-  const bf16x8* wr = reinterpret_cast<const bf16x8*>(Wo + (long)min(n, No - 1) * ldw);
-  bf16x8 w[STEPS];
-#pragma unroll
-  for (int s = 0; s < STEPS; ++s) w[s] = __builtin_nontemporal_load(wr + min(lane + 64 * s, nchunk - 1));
-  // one poller per workgroup, ~1 us apart: a thousand pollers at 60 ns flooded the one line
-  if (threadIdx.x == 0) {
-    unsigned spins = 0;
-    while (__hip_atomic_load(sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)items &&
-           ++spins < (1u << 20))
-      __builtin_amdgcn_s_sleep(32);
-  }
-  __syncthreads();
-  // attention rows -> LDS through device-scope (sc1) 16-B loads (written by other workgroups)
-  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  u16* xs = &vtile_all[0][0];
-  for (int i = threadIdx.x; i < B * nchunk; i += 256) {
-    u32x4 v;
-    asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)"
-                 : "=v"(v) : "v"(attn + (long)i * 8) : "memory");
-    *reinterpret_cast<u32x4*>(xs + (long)i * 8) = v;
-  }
-  __syncthreads();
-  for (int m = 0; m < B; ++m) {
-    const bf16x8* xr = reinterpret_cast<const bf16x8*>(xs + (long)m * K);
-    float acc = 0.f;
-#pragma unroll
-    for (int s = 0; s < STEPS; ++s) {
-      const bool ok = lane + 64 * s < nchunk;
-      const float a = dot8_bf16(w[s], xr[min(lane + 64 * s, nchunk - 1)], acc);
-      acc = ok ? a : acc;
-    }
-    acc = wave_sum(acc);
-    if (lane == 0 && n < No) {
-      u16* p = residual + (long)m * ldr + n;
-      *p = f2bf(bf2f(*p) + bf2f(f2bf(acc)));
-    }
-  }
-  if (threadIdx.x == 0 &&
-      __hip_atomic_fetch_add(sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-          (unsigned)nO - 1) {
-    __hip_atomic_store(sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(sync + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    decode_attn_wg<WPI>(qf, vtile_all, ml_all, wv, lane, b, kvh, G, s_begin, s_end, bt0, out,
+                        k_cache, v_cache, block_tables, max_blocks, hq, hkv, block_size,
+                        scale_log2);
   }
 }
 
@@ -995,39 +873,4 @@ extern "C" int dli_decode_attention_fused(void* out, const void* ws, int splits,
 extern "C" long dli_decode_attention_workspace_bytes(int B, int hq, int hd, int num_splits) {
   if (num_splits <= 1) return 0;
   return (long)B * hq * num_splits * (hd + 2) * (long)sizeof(float);
-}
-
-// Batch-1 decode: fused QKV reduce + RoPE + KV write + attention, then residual[B, No] +=
-// attn . Wo^T in the same launch (decode_attn_o_kernel). attn: [B, hq * 128] scratch;
-// sync: two zeroed uint32 owned by the stream (reset by the kernel). B * hq * 128 * 2 bytes
-// must fit the attention tiles' LDS (36 KiB: B <= 4 at hq * 128 = 4096).
-extern "C" int dli_decode_attention_o(void* attn, const void* ws, int splits,
-                                      const int* positions, const int* slot_mapping,
-                                      const float* cos_sin, void* k_cache, void* v_cache,
-                                      const int* block_tables, int max_blocks,
-                                      const int* context_lens, int B, int hq, int hkv, int hd,
-                                      int block_size, float scale, const void* Wo, int ldw,
-                                      void* residual, int ldr, int No, unsigned* sync,
-                                      hipStream_t st) {
-  if (B <= 0) return 0;
-  const int K = hq * 128;
-  const long items = (long)B * hkv;
-  if (hd != 128 || hq % hkv || hq / hkv > 16 || block_size % 16 ||
-      (splits != 0 && splits != 2 && splits != 4) || ldw % 8 || No <= 0 || sync == nullptr ||
-      (long)B * K * 2 > (long)DEC_WAVES * DEC_TILE * 144 * 2 || items > 256 || K > 8192)
-    return (int)hipErrorInvalidValue;
-  const int N = (hq + 2 * hkv) * hd;
-  const float scale_log2 = scale * 1.4426950408889634f;
-  dim3 grid((int)items + (No + 3) / 4);
-#define DLI_DAO(S, T) decode_attn_o_kernel<S, T><<<grid, 64 * DEC_WAVES, 0, st>>>(              \
-      (u16*)attn, ws, N, positions, slot_mapping, cos_sin, (u16*)k_cache, (u16*)v_cache,     \
-      block_tables, max_blocks, context_lens, B, hq, hkv, block_size, scale_log2,           \
-      (const u16*)Wo, ldw, (u16*)residual, ldr, No, sync)
-  if (K <= 4096) {
-    if (splits == 0) DLI_DAO(0, 8); else if (splits == 2) DLI_DAO(2, 8); else DLI_DAO(4, 8);
-  } else {
-    if (splits == 0) DLI_DAO(0, 16); else if (splits == 2) DLI_DAO(2, 16); else DLI_DAO(4, 16);
-  }
-#undef DLI_DAO
-  DLI_RETURN_LAUNCH();
 }

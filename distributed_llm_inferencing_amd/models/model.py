@@ -151,26 +151,17 @@ class TransformerLM:
                 h = ops.add_rmsnorm(pending, residual, lp["attn_norm"], eps)
                 pending = None
             attn = None
-            if defer and ops.rope_attention_o(h, lp["wqkv"], b.positions, b.slot_mapping,
-                                              self.cos_sin, kc, vc, b.block_tables,
-                                              b.context_lens, b.max_context, cfg.num_heads,
-                                              cfg.num_kv_heads, cfg.head_dim, self.scale,
-                                              lp["wo"], residual):
-                # batch 1: attention and the O projection (into the residual) in one launch
-                h = ops.NormedRows(residual, lp["mlp_norm"], eps)
-            else:
-                if not b.is_prefill:         # decode: reduce + RoPE + KV write + attention fused
-                    attn = ops.linear_rope_attention(h, lp["wqkv"], b.positions, b.slot_mapping,
-                                                     self.cos_sin, kc, vc, b.block_tables,
-                                                     b.context_lens, b.max_context,
-                                                     cfg.num_heads, cfg.num_kv_heads,
-                                                     cfg.head_dim, self.scale)
-                if attn is None:
-                    qkv = ops.linear_rope_cache(h, lp["wqkv"], b.positions, b.slot_mapping,
-                                                self.cos_sin, kc, vc, cfg.num_heads,
-                                                cfg.num_kv_heads, cfg.head_dim)
-                    attn = self._attend(qkv, b, kc, vc)
-                h = self._proj_add_norm(attn, lp["wo"], residual, lp["mlp_norm"], eps, defer)
+            if not b.is_prefill:             # decode: reduce + RoPE + KV write + attention fused
+                attn = ops.linear_rope_attention(h, lp["wqkv"], b.positions, b.slot_mapping,
+                                                 self.cos_sin, kc, vc, b.block_tables,
+                                                 b.context_lens, b.max_context, cfg.num_heads,
+                                                 cfg.num_kv_heads, cfg.head_dim, self.scale)
+            if attn is None:
+                qkv = ops.linear_rope_cache(h, lp["wqkv"], b.positions, b.slot_mapping,
+                                            self.cos_sin, kc, vc, cfg.num_heads,
+                                            cfg.num_kv_heads, cfg.head_dim)
+                attn = self._attend(qkv, b, kc, vc)
+            h = self._proj_add_norm(attn, lp["wo"], residual, lp["mlp_norm"], eps, defer)
             if cfg.is_moe:
                 pending = self.moe_fn(h, lp, self.layer_start + li)
                 continue

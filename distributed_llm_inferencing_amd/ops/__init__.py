@@ -345,51 +345,6 @@ def linear_rope_attention(x, w, positions, slot_mapping, cos_sin, k_cache, v_cac
     return out
 
 
-_ATTN_O = os.environ.get("DLI_ATTN_O", "1") == "1"
-
-
-def rope_attention_o(x, w, positions, slot_mapping, cos_sin, k_cache, v_cache, block_tables,
-                     context_lens, max_context: int, hq, hkv, hd, scale, wo, residual) -> bool:
-    """Batch-1 decode (M <= 4): the QKV GEMV, then ONE launch for the fused attention (QKV
-    reduce, RoPE, KV write, attention) AND the O projection, whose GEMV workgroups stream
-    their Wo rows while the attention runs and add into ``residual`` (``dli_decode_attention_o``).
-    False where it does not apply (the caller runs linear_rope_attention + linear_residual)."""
-    xr = x.residual if isinstance(x, NormedRows) else x
-    if (not _ATTN_O or hd != 128 or k_cache is None or not _use_native(xr)
-            or xr.shape[0] > G.GEMV_MAX_M or os.environ.get("DLI_FUSED_ROPE_ATTN", "1") != "1"
-            or not residual.is_contiguous() or wo.stride(-1) != 1
-            or xr.shape[0] * hq * hd * 2 > 4 * 32 * 144 * 2 or hq * hd > 8192):
-        return False
-    p = _splitk_plan(xr, w)
-    if p is not None and p.splits not in (2, 4):
-        return False
-    B, K = xr.shape
-    if decode_num_splits(B, hkv, max_context) != 1:
-        return False
-    mode = int(N.require_native().dli_decode_get_pipe())
-    if mode == 1 or (mode == 2 and -(-max_context // 32) * 32 >= 768):
-        return False
-    Nn = w.shape[0]
-    if p is None:
-        src, splits = linear(x, w), 0
-    else:
-        src, splits = G.workspace(xr.device, p.splits * B * Nn * 4), p.splits
-        if not (isinstance(x, NormedRows)
-                and _gemv_prologue(x, w, "splitk", p, None, Nn, ws=src)):
-            if isinstance(x, NormedRows):
-                x = x.materialize()
-            _native_call("dli_gemm", _p(x), x.stride(0), _p(w), w.stride(-2), None, Nn, B, Nn,
-                         K, 0, p.tile, p.splits, None, _p(src), None, 1, _st())
-    attn = torch.empty(B, hq * hd, dtype=xr.dtype, device=xr.device)
-    sync = G.tickets(xr.device, 2, _st(), pool="attn_o")
-    _native_call("dli_decode_attention_o", _p(attn), _p(src), splits, _p(positions),
-                 _p(slot_mapping), _p(cos_sin), _p(k_cache), _p(v_cache), _p(block_tables),
-                 block_tables.stride(0), _p(context_lens), B, hq, hkv, hd, k_cache.shape[2],
-                 scale, _p(wo), wo.stride(-2), _p(residual), residual.stride(0), wo.shape[0],
-                 _p(sync), _st())
-    return True
-
-
 def feed_ids(ids, src, feed):
     """In place: ids[i] = feed[src[i]] where src[i] >= 0 (int32 tensors; lookahead input ids
     taken from the in-flight step's sampled tokens)."""

@@ -61,8 +61,6 @@ _SIGS = {
     "dli_gemv_fused": [P, I, P, F, P, I, P, I, I, I, I, I, I, I, P, P],
     "dli_splitk_rope_cache": [P, P, I, I, I, P, P, P, P, P, I, I, I, I, I, P],
     "dli_decode_attention_fused": [P, P, I, P, P, P, P, P, P, I, P, I, I, I, I, I, F, P],
-    "dli_decode_attention_o": [P, P, I, P, P, P, P, P, P, I, P, I, I, I, I, I, F, P, I, P, I,
-                               I, P, P],
     "dli_moe_route": [P, P, P, I, I, I, P],
     "dli_moe_align": [P, P, P, P, I, I, I, I, P],
     "dli_moe_gather": [P, P, P, I, I, P, P],

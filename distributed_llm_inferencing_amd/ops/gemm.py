@@ -131,12 +131,12 @@ _retired: list = []
 _tickets: dict = {}
 
 
-def tickets(device: torch.device, n: int, stream: int = 0, pool: str = "tickets") -> torch.Tensor:
+def tickets(device: torch.device, n: int, stream: int = 0) -> torch.Tensor:
     """Zeroed uint32 arrival counters for in-launch split-K combines, one buffer per (device,
     stream) — launches on one stream never overlap — grow-only and never freed (captured
     graphs keep the pointer). Every launch's last arrivers reset the counters they used, so
     they are zero again for the next launch on the stream."""
-    key = (pool, device.type, device.index, int(stream))
+    key = (device.type, device.index, int(stream))
     with _ws_lock:
         t = _tickets.get(key)
         if t is None or t.numel() < n:
