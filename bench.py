@@ -67,6 +67,20 @@ def _like_for_like_value():
         return None
 
 
+def _heartbeat(period_s: float = 45.0):
+    """A stderr line every ``period_s`` on rank 0 (stdout keeps the one JSON line): engine
+    start-up (weights, autotune, graph capture) and an 8-stage run can stay silent for
+    minutes, which a runner's hang detector cannot tell from a stall."""
+    import threading
+    t0 = time.monotonic()
+
+    def beat():
+        while True:
+            time.sleep(period_s)
+            print(f"[bench] running, {time.monotonic() - t0:.0f} s", file=sys.stderr, flush=True)
+    threading.Thread(target=beat, daemon=True, name="bench-heartbeat").start()
+
+
 def make_prompts(n, prompt_len, vocab, seed):
     # one [n, prompt_len] draw (0.3 ms for 512 x 32) instead of n per-row draws (5.7 ms, a
     # host gap at the head of every timed wave: profiles/r5/s06/wave_summary.txt)
@@ -198,6 +212,8 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if rank == 0:
+        _heartbeat()
     if world > 1 or a.gpus > 1:
         res = run_pipeline(a, world, rank)
     else:
