@@ -93,6 +93,9 @@ __device__ __forceinline__ void gemv_core(const u16* __restrict__ A, int lda,
           acc[m][r] = ok ? a : acc[m][r];
         }
       }
+      // several rows: one row's LDS reads at a time (hoisting every row's 8 reads held
+      // 128 VGPRs at MB = 4 and dropped the prologue GEMVs to 2 waves per SIMD)
+      if constexpr (MB > 1) __builtin_amdgcn_sched_barrier(0);
     }
     c += 64 * UNROLL;
   }
@@ -212,6 +215,7 @@ struct NormPrologue {
         for (int j = 0; j < 8; ++j) v[i][j] = v[i][j] * rstd * w8[j];
         if (vi < nvec) store8(xs + (long)m * K + vi * 8, v[i]);
       }
+      if constexpr (MB > 1) __builtin_amdgcn_sched_barrier(0);   // one row's floats live
     }
     __syncthreads();
   }
@@ -221,7 +225,7 @@ struct NormPrologue {
 // one 32-row gate/up block (waves 0-1 the gate rows, waves 2-3 the up rows; RW 4: 8 + 8,
 // RW 1: 2 + 2 — tile 58, 4x the workgroups of tile 29), so the pairing
 // runs at the 16-row grid (2x the workgroups of the 32-row tile; profiles/r4/b1/)
-template <int MB, int RW, int EPI, int UNROLL, bool H16 = false, bool PRO = false>
+template <int MB, int RW, int EPI, int UNROLL, bool H16 = false, bool PRO = false, int PV = 2>
 __global__ void __launch_bounds__(256) gemv_kernel(
     const u16* __restrict__ A, int lda, const u16* __restrict__ W, int ldw,
     void* __restrict__ C, int ldc, int M, int N, int K, int k_split_len,
@@ -242,16 +246,12 @@ __global__ void __launch_bounds__(256) gemv_kernel(
     return H16 ? blk * 32 + (j < HR ? half * HR + j : 16 + half * HR + (j - HR)) : n_base + j;
   };
   if constexpr (PRO) {
-    // row vectors per thread: 2 up to K = 4096 (Llama-3-8B / Mixtral hidden), 4 up to 8192
-    if (K <= 4096) {
-      NormPrologue<MB, 2> pro{A, lda, nw, eps, M, K, xs_dyn, red};
-      gemv_core<MB, RW, UNROLL, true>(xs_dyn, K, W, ldw, M, N, K, k_split_len,
-                                      row_of(wid * RW), ks, res, pro);
-    } else {
-      NormPrologue<MB, 4> pro{A, lda, nw, eps, M, K, xs_dyn, red};
-      gemv_core<MB, RW, UNROLL, true>(xs_dyn, K, W, ldw, M, N, K, k_split_len,
-                                      row_of(wid * RW), ks, res, pro);
-    }
+    // PV row vectors per thread (launcher: 2 up to K = 4096, 4 up to 8192) — a template
+    // parameter, not a runtime branch: the unused 4-vector form's registers set the kernel's
+    // count (196 VGPRs, 2 waves per SIMD at MB = 4)
+    NormPrologue<MB, PV> pro{A, lda, nw, eps, M, K, xs_dyn, red};
+    gemv_core<MB, RW, UNROLL, true>(xs_dyn, K, W, ldw, M, N, K, k_split_len, row_of(wid * RW),
+                                    ks, res, pro);
   } else {
     NoPrologue pro;
     gemv_core<MB, RW, UNROLL>(A, lda, W, ldw, M, N, K, k_split_len, row_of(wid * RW), ks, res,
@@ -317,9 +317,14 @@ static int launch_gemv(const void* A, int lda, const void* W, int ldw, void* C, 
   ksl = (ksl / 8) * 8;
   if (ksl * splits != K) return (int)hipErrorInvalidValue;
   dim3 grid((N + R - 1) / R, splits);
-  gemv_kernel<MB, RW, EPI, UNROLL, H16, PRO><<<grid, 256, lds, st>>>(
-      (const u16*)A, lda, (const u16*)W, ldw, C, ldc, M, N, K, ksl, (const u16*)bias,
-      splits > 1 ? (float*)ws : nullptr, (const u16*)nw, eps);
+  if (PRO && K > 4096)
+    gemv_kernel<MB, RW, EPI, UNROLL, H16, PRO, 4><<<grid, 256, lds, st>>>(
+        (const u16*)A, lda, (const u16*)W, ldw, C, ldc, M, N, K, ksl, (const u16*)bias,
+        splits > 1 ? (float*)ws : nullptr, (const u16*)nw, eps);
+  else
+    gemv_kernel<MB, RW, EPI, UNROLL, H16, PRO, 2><<<grid, 256, lds, st>>>(
+        (const u16*)A, lda, (const u16*)W, ldw, C, ldc, M, N, K, ksl, (const u16*)bias,
+        splits > 1 ? (float*)ws : nullptr, (const u16*)nw, eps);
   if constexpr (EPI != EPI_RES) {
     if (splits > 1 && C != nullptr) {
       const int outN = (EPI == EPI_SILU) ? N / 2 : N;
