@@ -225,7 +225,7 @@ struct NormPrologue {
 // one 32-row gate/up block (waves 0-1 the gate rows, waves 2-3 the up rows; RW 4: 8 + 8,
 // RW 1: 2 + 2 — tile 58, 4x the workgroups of tile 29), so the pairing
 // runs at the 16-row grid (2x the workgroups of the 32-row tile; profiles/r4/b1/)
-template <int MB, int RW, int EPI, int UNROLL, bool H16 = false, bool PRO = false, int PV = 2>
+template <int MB, int RW, int EPI, int UNROLL, bool H16 = false, bool PRO = false, int PV = 0>
 __global__ void __launch_bounds__(256) gemv_kernel(
     const u16* __restrict__ A, int lda, const u16* __restrict__ W, int ldw,
     void* __restrict__ C, int ldc, int M, int N, int K, int k_split_len,
@@ -245,13 +245,25 @@ __global__ void __launch_bounds__(256) gemv_kernel(
   auto row_of = [&](int j) {
     return H16 ? blk * 32 + (j < HR ? half * HR + j : 16 + half * HR + (j - HR)) : n_base + j;
   };
-  if constexpr (PRO) {
-    // PV row vectors per thread (launcher: 2 up to K = 4096, 4 up to 8192) — a template
-    // parameter, not a runtime branch: the unused 4-vector form's registers set the kernel's
-    // count (196 VGPRs, 2 waves per SIMD at MB = 4)
+  if constexpr (PRO && PV > 0) {
+    // several rows (launcher: MB > 1): PV row vectors per thread as a template parameter
+    // (2 up to K = 4096, 4 up to 8192) — with a runtime branch the unused 4-vector form's
+    // registers set the kernel's count (196 VGPRs, 2 waves per SIMD at MB = 4)
     NormPrologue<MB, PV> pro{A, lda, nw, eps, M, K, xs_dyn, red};
     gemv_core<MB, RW, UNROLL, true>(xs_dyn, K, W, ldw, M, N, K, k_split_len, row_of(wid * RW),
                                     ks, res, pro);
+  } else if constexpr (PRO) {
+    // one row: the runtime branch. Its allocation (124 VGPRs) streams faster than the
+    // template form's (101): batch-1 p50 0.188 vs 0.194 s, same box (profiles/r5/s33)
+    if (K <= 4096) {
+      NormPrologue<MB, 2> pro{A, lda, nw, eps, M, K, xs_dyn, red};
+      gemv_core<MB, RW, UNROLL, true>(xs_dyn, K, W, ldw, M, N, K, k_split_len,
+                                      row_of(wid * RW), ks, res, pro);
+    } else {
+      NormPrologue<MB, 4> pro{A, lda, nw, eps, M, K, xs_dyn, red};
+      gemv_core<MB, RW, UNROLL, true>(xs_dyn, K, W, ldw, M, N, K, k_split_len,
+                                      row_of(wid * RW), ks, res, pro);
+    }
   } else {
     NoPrologue pro;
     gemv_core<MB, RW, UNROLL>(A, lda, W, ldw, M, N, K, k_split_len, row_of(wid * RW), ks, res,
@@ -317,12 +329,13 @@ static int launch_gemv(const void* A, int lda, const void* W, int ldw, void* C, 
   ksl = (ksl / 8) * 8;
   if (ksl * splits != K) return (int)hipErrorInvalidValue;
   dim3 grid((N + R - 1) / R, splits);
-  if (PRO && K > 4096)
-    gemv_kernel<MB, RW, EPI, UNROLL, H16, PRO, 4><<<grid, 256, lds, st>>>(
+  constexpr int PV_SMALL = (PRO && MB > 1) ? 2 : 0, PV_LARGE = (PRO && MB > 1) ? 4 : 0;
+  if (PRO && MB > 1 && K > 4096)
+    gemv_kernel<MB, RW, EPI, UNROLL, H16, PRO, PV_LARGE><<<grid, 256, lds, st>>>(
         (const u16*)A, lda, (const u16*)W, ldw, C, ldc, M, N, K, ksl, (const u16*)bias,
         splits > 1 ? (float*)ws : nullptr, (const u16*)nw, eps);
   else
-    gemv_kernel<MB, RW, EPI, UNROLL, H16, PRO, 2><<<grid, 256, lds, st>>>(
+    gemv_kernel<MB, RW, EPI, UNROLL, H16, PRO, PV_SMALL><<<grid, 256, lds, st>>>(
         (const u16*)A, lda, (const u16*)W, ldw, C, ldc, M, N, K, ksl, (const u16*)bias,
         splits > 1 ? (float*)ws : nullptr, (const u16*)nw, eps);
   if constexpr (EPI != EPI_RES) {
