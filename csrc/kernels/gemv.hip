@@ -1,5 +1,6 @@
-// Weight-streaming skinny GEMM for M <= 4 rows (tile ids 29-33) and its in-launch split-K
-// combine + residual add + RMSNorm (dli_gemv_add_rmsnorm).
+// Weight-streaming skinny GEMM for M <= 4 rows (tile ids 29-33, 56-59), its in-launch split-K
+// combine + residual add + RMSNorm (dli_gemv_add_rmsnorm), and the batch-1 reduce-free forms
+// (dli_gemv_fused: residual-adding epilogue, RMSNorm prologue).
 #include "gemm_common.h"
 
 // ---------------------------------------------------------------------------------------
@@ -31,16 +32,17 @@ __device__ __forceinline__ float dot8_acc(const bf16x8v w, const bf16x8v x, floa
   return acc;
 }
 
-// The weight stream of one workgroup: res[m][wid * RW + r] = sum over this K slice of
-// A[m, :] . W[r0 + r, :] (r < RW), reduced across the wave and staged in LDS.
 struct NoPrologue {
   __device__ void issue() {}
   __device__ void complete() {}
 };
 
+// The weight stream of one workgroup: res[m][wid * RW + r] = sum over this K slice of
+// A[m, :] . W[r0 + r, :] (r < RW), reduced across the wave and staged in LDS.
 // PRE: the input rows are produced by `pro` (the RMSNorm prologue, into LDS): pro.issue()
 // requests the residual rows and norm weight, then this lane's first UNROLL weight steps are
-// requested (branch-free: clamped, the steps past the slice masked out of the sums), then pro.complete() waits for the ROW loads only (they
+// requested (branch-free: clamped, the steps past the slice masked out of the sums), then
+// pro.complete() waits for the ROW loads only (they
 // are older than the weight loads, so the counted wait leaves the weight stream in flight),
 // normalises into LDS and synchronises. The prologue's latency (rows from the Infinity
 // Cache, a block reduction, LDS stores) thus runs under the first weight requests.
