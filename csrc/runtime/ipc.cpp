@@ -103,8 +103,10 @@ struct ErrRef {
 // The device mirror takes the read-modify-write; the pinned host word only a plain
 // system-scope store of the accumulated bits (a device atomic on host memory needs PCIe
 // AtomicOps from the root complex, which a host may not provide). Bits only ever grow, so a
-// racing store can at worst drop another raiser's bit from the host copy — never clear the
-// word: the host's per-tick poll still sees a nonzero error.
+// racing store can at worst drop another raiser's bit — or the abort bit dli_ipc_abort set on
+// the host before its flag copy reached the device mirror — from the host copy, never clear
+// the word: the host's per-tick poll still sees a nonzero error, and dli_ipc_error ORs the
+// endpoint's host-side sticky abort flag back in, so "aborted" is never lost.
 __device__ __forceinline__ void raise_err(ErrRef e, uint64_t bit) {
   const uint64_t v =
       __hip_atomic_fetch_or(e.dev, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) | bit;
@@ -304,6 +306,10 @@ struct Endpoint {
   long long khz = 100000;             // wall clock rate
   ErrRef err{nullptr, nullptr};       // device addresses of the two error words
   uint64_t* err_host = nullptr;       // pinned host error word (host address)
+  // set by dli_ipc_abort on the host only and ORed into dli_ipc_error: a device raise that
+  // lands on err_host between the abort's fetch_or and its flag copy overwrites the word with
+  // the device mirror's bits (plain store), which would drop "aborted" from the report
+  std::atomic<uint64_t> host_sticky{0};
   uint64_t* seq = nullptr;            // device: seq_out[world], seq_in[world]
   bool host_flags = false;
   int mem_kind = kUncached;
@@ -778,6 +784,7 @@ long long dli_ipc_pending(void* h, int peer) {
 int dli_ipc_abort(void* h, double timeout_s) {
   auto* e = E(h);
   const size_t n = 2 * (size_t)e->world;
+  e->host_sticky.fetch_or(kErrAbort, std::memory_order_release);
   reinterpret_cast<std::atomic<uint64_t>*>(e->err_host)->fetch_or(kErrAbort);
   if (e->host_flags) {
     for (size_t i = 0; i < n; ++i) set_word(e->flags + i * kFlagStride, 1);
@@ -801,8 +808,9 @@ int dli_ipc_abort(void* h, double timeout_s) {
 // cheap enough to poll every pipeline tick.
 int dli_ipc_error(void* h) {
   auto* e = E(h);
-  return (int)reinterpret_cast<std::atomic<uint64_t>*>(e->err_host)->load(
-      std::memory_order_acquire);
+  return (int)(reinterpret_cast<std::atomic<uint64_t>*>(e->err_host)->load(
+                   std::memory_order_acquire) |
+               e->host_sticky.load(std::memory_order_acquire));
 }
 
 // Bounded-wait budget in seconds (wait kernels enqueued after the call).

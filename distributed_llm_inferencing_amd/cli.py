@@ -44,15 +44,15 @@ import time
 
 
 def node_commands(gpus: int, base_port: int = 5000, preload: str = ""):
-    """[(argv, env)] of serve-node's workers: worker i selects GPU i with ``--gpu i`` and
-    sees every GPU of the node. (Masking each worker to its own GPU with a visibility
-    variable would leave a join-pipeline ring over them unable to open its peers' memory:
-    the IPC mailboxes and RCCL's P2P path both need the peer device visible.)"""
+    """[(argv, env)] of serve-node's workers: worker i selects GPU i of the operator's
+    visibility mask with ``--gpu i`` (the mask, if any, is passed through unchanged, so
+    ``HIP_VISIBLE_DEVICES=4,5,6,7 serve-node --gpus 4`` runs on physical GPUs 4-7) and sees
+    every GPU of that mask. (Masking each worker down to its own GPU would leave a
+    join-pipeline ring over them unable to open its peers' memory: the IPC mailboxes and
+    RCCL's P2P path both need the peer device visible.)"""
     out = []
     for i in range(gpus):
-        env = {k: v for k, v in os.environ.items()
-               if k not in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES",
-                            "CUDA_VISIBLE_DEVICES")}
+        env = dict(os.environ)
         env.update(USE_GPU="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
         cmd = [sys.executable, "-m", "distributed_llm_inferencing_amd.worker.server",
                "--port", str(base_port + i), "--gpu", str(i), "--preload", preload]

@@ -64,6 +64,10 @@ def _pdeathsig() -> None:                       # runs in the child between fork
 def start(cmd: Sequence[str], world: int, env: Optional[Dict[str, str]] = None,
           port: Optional[int] = None) -> List[subprocess.Popen]:
     """Start ``world`` copies of ``cmd``, rank r with the torchrun variables of rank r."""
+    tm = sys.modules.get("torch")
+    if tm is not None and tm.cuda.is_initialized():
+        raise RuntimeError("launch.start: this process has initialised the GPU; its ranks "
+                           "must be started before any HIP call (fork after HIP init)")
     port = port or free_port()
     base = dict(os.environ if env is None else env)
     procs = []
@@ -131,11 +135,45 @@ def spawn_self(world: int, argv: Optional[Sequence[str]] = None,
     return spawn([sys.executable, "-u", os.path.abspath(sys.argv[0]), *args], world, env=env)
 
 
-def visible_gpus() -> int:
-    """GPUs this process could hand to its children, counted without initialising HIP
-    (``torch.cuda.device_count`` reads the agent list only on this image)."""
+def _visibility_mask(n: int) -> int:
+    """Apply ROCR_VISIBLE_DEVICES, then HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES (the HIP
+    runtime's order) to ``n`` devices: how many of them a child would see."""
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is None:
+            continue
+        ids = [t.strip() for t in v.split(",") if t.strip()]
+        keep = 0
+        for t in ids:
+            if t.lstrip("-").isdigit():
+                i = int(t)
+                if i < 0 or i >= n:      # the runtime stops at the first invalid entry
+                    break
+            keep += 1                    # UUID-style entries: trust them
+        n = min(n, keep)
+    return n
+
+
+def kfd_gpus(topology: str = "/sys/class/kfd/kfd/topology/nodes") -> int:
+    """GPU agents in the KFD topology (nodes whose ``gpu_id`` is non-zero; CPU nodes have
+    0): a sysfs read, no HIP / HSA call."""
+    n = 0
     try:
-        import torch
-        return int(torch.cuda.device_count())
-    except Exception:  # noqa: BLE001
+        for node in sorted(os.listdir(topology)):
+            try:
+                with open(os.path.join(topology, node, "gpu_id")) as f:
+                    if int(f.read().strip() or "0") != 0:
+                        n += 1
+            except (OSError, ValueError):
+                continue
+    except OSError:
         return 0
+    return n
+
+
+def visible_gpus() -> int:
+    """GPUs this process could hand to its children, counted WITHOUT initialising HIP: the
+    KFD topology in sysfs under the HIP / ROCR visibility masks. (``torch.cuda.device_count``
+    reads amdsmi on this image, but falls back to ``hipGetDeviceCount`` — a HIP init in the
+    parent that then forks its ranks — when amdsmi is unavailable, so it is never used.)"""
+    return _visibility_mask(kfd_gpus())

@@ -963,6 +963,7 @@ def bench_pipeline(args, world: int, rank: int, make_prompts):
     if rank == 0:
         eng.head.host_s, eng.head.ticks = 0.0, 0
         eng.head.host_by_kind = {k: [0.0, 0] for k in eng.head.host_by_kind}
+        eng.head.phase_s = {k: 0.0 for k in eng.head.phase_s}
     for s in range(args.steps):
         n, l = wave(s)
         toks += n
@@ -985,6 +986,8 @@ def bench_pipeline(args, world: int, rank: int, make_prompts):
     snap["head_host_ms_per_tick"] = round(1e3 * eng.head.host_s / max(1, eng.head.ticks), 4)
     hd = eng.head.host_by_kind[DECODE]
     snap["head_host_ms_per_decode_tick"] = round(1e3 * hd[0] / max(1, hd[1]), 4)
+    snap["head_phase_ms_per_tick"] = {k: round(1e3 * v / max(1, eng.head.ticks), 4)
+                                      for k, v in eng.head.phase_s.items()}
     snap["control_plane"] = eng.channel.ctrl_kind
     return {"tokens": toks, "seconds": float(dt.item()), "latencies": lats,
             "global_batch": per_wave, "parallelism": f"pp{world}", "engine": snap,

@@ -32,6 +32,7 @@ import logging
 import os
 import socket
 import threading
+import time
 from datetime import timedelta
 from typing import List, Optional, Sequence, Tuple
 
@@ -231,16 +232,29 @@ class PipeChannel:
         self._wd.start()
 
     def _watch(self, period: float) -> None:
+        from ..runtime import RcclComm
+        busy_since = None
+        # an exchange enqueue holds the RCCL handle for microseconds (a lazy P2P connect for
+        # well under a second); held longer it is blocked on a peer that will never answer
+        busy_limit = float(os.environ.get("DLI_PP_TIMEOUT_S", "30"))
         while not self._wd_stop.wait(period):
             ring = self.ring
             d = ring.dead() if ring is not None else -1
             err = self.rccl.async_error() if self.rccl is not None else 0
+            if err == RcclComm.BUSY:
+                now = time.monotonic()
+                busy_since = busy_since or now
+                err = 0 if now - busy_since < busy_limit else err
+            else:
+                busy_since = None
             if d == -1 and err == 0:
                 continue
             if d == 1000:
                 self.dead_peer = "pipeline head (rank 0) exited"
             elif d >= 0:
                 self.dead_peer = f"pipeline stage {d + 1} exited"
+            elif err == RcclComm.BUSY:
+                self.dead_peer = f"RCCL exchange blocked for over {busy_limit:.0f} s"
             else:
                 self.dead_peer = f"RCCL communicator error {err}"
             self.abort_data_plane()

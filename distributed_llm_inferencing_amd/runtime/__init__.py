@@ -521,23 +521,34 @@ class RcclComm:
         if r != 0:
             raise RuntimeError(f"RCCL exchange failed: {lib().dli_comm_error_string(r).decode()}")
 
+    BUSY = 1        # async_error(): an exchange is being enqueued on another thread
+
     def async_error(self) -> int:
-        """0 while healthy, else -(ncclResult_t) of the communicator's asynchronous error."""
+        """0 while healthy, -(ncclResult_t) of the communicator's asynchronous error, or
+        ``BUSY`` while another thread holds the handle inside an exchange (the caller decides
+        how long an enqueue may stay blocked: ``PipeChannel._watch`` aborts a stuck one)."""
         if not self._lock.acquire(timeout=0.05):
-            return 0                    # an exchange is being enqueued: ask again next period
+            return self.BUSY
         try:
             return int(lib().dli_comm_async_error(self._h)) if self._h is not None else 0
         finally:
             self._lock.release()
 
-    def abort(self) -> None:
+    def abort(self, wait_s: float = 1.0) -> None:
         """ncclCommAbort: release the communicator without waiting for peers (a dead
-        neighbour); queued RCCL kernels return so the stream drains. Waits for an exchange
-        being enqueued on another thread to finish first (never frees a handle in use)."""
-        with self._lock:
+        neighbour); queued RCCL kernels return so the stream drains. An exchange being
+        enqueued on another thread gets ``wait_s`` to leave the handle; if it is still blocked
+        there (a group end waiting on the dead peer) the handle is marked dead and aborted
+        anyway — the abort is what releases that blocked call, so waiting for it would turn a
+        fast failure into a hang. Later exchanges raise instead of touching the handle."""
+        got = self._lock.acquire(timeout=max(0.0, float(wait_s)))
+        try:
             h, self._h = self._h, None
             if h is not None:
                 lib().dli_comm_abort(h)
+        finally:
+            if got:
+                self._lock.release()
 
     def close(self) -> None:
         with self._lock:
