@@ -249,9 +249,8 @@ def main():
     }
     eng = res.get("engine") or {}
     keep = ("head_host_ms_per_tick", "head_host_ms_per_decode_tick", "head_phase_ms_per_tick",
-            "control_plane",
-            "decode_steps", "prefill_steps", "steps")
-    if any(k in eng for k in keep[:2]):
+            "lockstep_ms_per_step", "control_plane", "decode_steps", "prefill_steps", "steps")
+    if any(k in eng for k in keep[:4]):
         # multi-rank pipeline: the head's host cost per tick (it schedules every microbatch)
         line["engine"] = {k: eng[k] for k in keep if k in eng}
     infos = res.get("ranks_info")

@@ -749,30 +749,28 @@ __global__ void __launch_bounds__(256) decode_reduce_kernel(u16* __restrict__ ou
   store8(out + bh * HD + d0, acc);
 }
 
-// pipelined (1), one-tile-per-round (0) or automatic (2) decode kernel for hd 128; -1 = from
-// DLI_DECODE_PIPE (default automatic)
-static int g_decode_pipe = -1;
+// pipelined (1), one-tile-per-round (0) or automatic (2, the default) decode kernel for hd 128
+static int g_decode_pipe = 2;
 extern "C" int dli_decode_set_pipe(int v) {
   const int old = g_decode_pipe;
   g_decode_pipe = v;
   return old;
 }
 
-// the mode the next dli_decode_attention call applies (the env default resolved)
-extern "C" int dli_decode_get_pipe() {
-  if (g_decode_pipe < 0) {
-    const char* e = getenv("DLI_DECODE_PIPE");
-    g_decode_pipe = e ? atoi(e) : 2;
-  }
-  return g_decode_pipe;
-}
+// the mode the next dli_decode_attention call applies
+extern "C" int dli_decode_get_pipe() { return g_decode_pipe; }
 
 // a workgroup per (sequence, kv head) item while the items alone would leave most CUs idle
-// (<= 256 items: B <= 32 at 8 kv heads); DLI_DECODE_WPI=1 / 4 forces either form
+// (<= 256 items: B <= 32 at 8 kv heads), else a wave per item; tests force either form with
+// dli_decode_set_form(1 = wave per item, DEC_WAVES = workgroup per item, 0 = automatic)
+static int g_decode_form = 0;
+extern "C" int dli_decode_set_form(int v) {
+  const int old = g_decode_form;
+  g_decode_form = v;
+  return old;
+}
 static bool wg_form(long items) {
-  const char* e = getenv("DLI_DECODE_WPI");
-  const int v = e ? atoi(e) : 0;
-  return v == DEC_WAVES || (v != 1 && items <= 256);
+  return g_decode_form == DEC_WAVES || (g_decode_form != 1 && items <= 256);
 }
 
 extern "C" int dli_decode_attention(void* out, const void* q, int q_stride, const void* k_cache,
@@ -792,10 +790,6 @@ extern "C" int dli_decode_attention(void* out, const void* q, int q_stride, cons
   float* ws_ml = ws_o ? ws_o + (long)B * hq * num_splits * hd : nullptr;
   const float scale_log2 = scale * 1.4426950408889634f;
   const long items = (long)B * hkv * num_splits;
-  if (g_decode_pipe < 0) {
-    const char* e = getenv("DLI_DECODE_PIPE");
-    g_decode_pipe = e ? atoi(e) : 2;
-  }
   // 2 = automatic: the pipelined kernel for splits of >= 768 tokens (measured: +18 % at ctx
   // 1000, B 64; within 3 % slower at ctx 33-100, B 512, where the per-item dependent loads
   // (context length -> block table -> K/V) rather than tile rounds bound the time)

@@ -6,6 +6,9 @@
 //  * fp32 accumulation everywhere; f32->bf16 through __float2bfloat16, which lowers to
 //    v_cvt_pk_bf16_f32 on gfx950 (round-to-nearest-even, NaN-preserving).
 //  * every launcher is `extern "C" int dli_*(..., hipStream_t)` returning a hipError_t.
+// Comments cite cdna_hip_programming.md and MI355X_MICROARCH.md: the CDNA4 programming guide
+// and the measured MI355X microarchitecture notes of the build image (/opt/skills/guides/),
+// not files of this repository.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>

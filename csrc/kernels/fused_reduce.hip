@@ -96,13 +96,8 @@ extern "C" int dli_splitk_add_rmsnorm(void* out, void* residual, const float* ws
   const int nvec = N / 8;
   // threads per row (one workgroup per row): 512, i.e. one 8-column vector per lane at
   // N = 4096 (same-box A/B with the GEMMs that feed it, M = 512: O + reduce 33.85-33.92 ->
-  // 33.4 us, down + reduce 70.5-70.8 -> 69.95 us; profiles/r3/reduce_threads/);
-  // DLI_REDUCE_THREADS=256 / 128 / 64 for A/Bs
-  static const int cap = [] {
-    const char* e = getenv("DLI_REDUCE_THREADS");
-    const int v = e ? atoi(e) : 512;
-    return (v == 256 || v == 128 || v == 64) ? v : 512;
-  }();
+  // 33.4 us, down + reduce 70.5-70.8 -> 69.95 us; profiles/r3/reduce_threads/)
+  constexpr int cap = 512;
   int threads = ((nvec + 63) / 64) * 64;
   if (threads > cap) threads = cap;
   const int vpt = (nvec + threads - 1) / threads;

@@ -4,7 +4,7 @@
 // Structure (cdna_hip_programming.md §5):
 //  * WM x WN waves (2x2 = 256 threads, or 2x4 / 4x2 = 512 threads for 256-wide tiles); block
 //    tile BM x BN x 64; wave tile (BM/WM) x (BN/WN) built from v_mfma_f32_16x16x32_bf16 (the bf16 shape that holds the higher clock on random
-//    data, MI355X_MICROARCH.md 'DVFS give-back' item 7).
+//    data, /opt/skills/guides/MI355X_MICROARCH.md 'DVFS give-back' item 7).
 //  * global -> LDS by global_load_lds_dwordx4 (16 B per lane, no VGPR round trip), 2 LDS
 //    buffers: the next K-tile's DMA is issued before the current tile's ds_reads + MFMAs.
 //  * LDS rows are 128 B (64 bf16); the 16-B chunk c of row r is stored at physical chunk

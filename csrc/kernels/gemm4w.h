@@ -211,7 +211,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(
   // an accumulator is read only as the next MFMA's C (no wait states) until the drain after
   // the loop. ka / kw >= 0: this half also stages those K-tiles, one LDS-DMA piece after
   // every 4th MFMA (16 pieces issued back to back held the matrix pipe for several hundred
-  // cycles: an LDS-DMA issue costs ~60 cycles among MFMAs, MI355X_MICROARCH.md constants).
+  // cycles: an LDS-DMA issue costs ~60 cycles among MFMAs, /opt/skills/guides/MI355X_MICROARCH.md constants).
   auto half = [&](const bf16x8 (&acur)[8], const bf16x8 (&bcur)[8], bf16x8 (&anext)[8],
                   bf16x8 (&bnext)[8], const char* na, const char* nw, int nkk, bool more,
                   int ka, int kw, int ws, int rw = -1, int rl = -1)
@@ -519,7 +519,7 @@ __global__ void __launch_bounds__(256, 1) gemm4w_kernel(
       for (int j = 0; j < 8; ++j) {
         const f32x4 v = vget(acc[i][j]);
         const int col = wc0 + 16 * j + 4 * fq;
-        if (row < Mg && col < N) slab_quad(srow + col, v, sm, vec, N - col);
+        if (row < Mg && col < N) slab_quad_fp32(srow + col, v, sm & 3, vec, N - col);
       }
     }
     return;

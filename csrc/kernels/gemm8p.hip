@@ -1,11 +1,11 @@
-// 8-wave "8-phase ping-pong" MFMA GEMMs (tile ids 22, 26, 27, 28): 256x256 (gemm8p_kernel),
+// 8-wave "8-phase ping-pong" MFMA GEMMs (tile ids 22, 26, 28): 256x256 (gemm8p_kernel),
 // 256x224 (gemm8p224_kernel) and 256x128 (gemm8p128_kernel) block tiles, two wave groups
 // alternating MFMA and load segments (cdna_hip_programming.md §5 'The 256² 8-phase template').
 #include "gemm_common.h"
 
 // ---------------------------------------------------------------------------------------
 // 256x256 "8-phase ping-pong" GEMM (cdna_hip_programming.md §5 'The 256² 8-phase template',
-// T3+T4+T5; MI355X_MICROARCH.md 'Two waves per SIMD' items 1, 7, 9).
+// T3+T4+T5; /opt/skills/guides/MI355X_MICROARCH.md 'Two waves per SIMD' items 1, 7, 9).
 //
 // 8 waves = 2 groups of 4 (g = wid >> 2 = the wave's 128-row half of the tile; one wave of
 // each group per SIMD). Every K-tile (BK = 64) is 4 phases; a phase is a LOAD segment
@@ -286,7 +286,7 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int col = wc0 + 16 * j + 4 * fq;
-        if (col < N) slab_quad(srow + col, acc[i][j], sm, vec, N - col);
+        if (col < N) slab_quad(srow + col, acc[i][j], sm, vec, N - col, ws);
       }
     }
     return;
@@ -521,7 +521,7 @@ __global__ void __launch_bounds__(512) gemm8p224_kernel(
 #pragma unroll
       for (int j = 0; j < 7; ++j) {
         const int col = wc0 + 16 * j + 4 * fq;
-        if (col < N) slab_quad(srow + col, acc[i][j], sm, vec, N - col);
+        if (col < N) slab_quad(srow + col, acc[i][j], sm, vec, N - col, ws);
       }
     }
     return;
@@ -767,7 +767,7 @@ __global__ void __launch_bounds__(512) gemm8p128_kernel(
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int col = wc0 + 16 * j + 4 * fq;
-        if (col < N) slab_quad(srow + col, acc[i][j], sm, vec, N - col);
+        if (col < N) slab_quad(srow + col, acc[i][j], sm, vec, N - col, ws);
       }
     }
     return;
@@ -812,7 +812,6 @@ __global__ void __launch_bounds__(512) gemm8p128_kernel(
 // (within 1 %, profiles/r2_s2/gemm8p_wait/variants.log) did the template's B-before-A read
 // order, an lgkmcnt(0) after the barrier and per-cluster priority flips
 constexpr int GEMM8P_DEFAULT = 8 | 256 | 512;
-constexpr int GEMM8P_PER_PHASE_WAITS = 8 | 256;     // round-1 schedule (tile 27, for A/Bs)
 
 template <int EPI, int VAR = 0>
 static int launch_8p(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M,
@@ -905,8 +904,6 @@ static int dispatch_8p(int tile_cfg, DLI_GEMM_ARGS) {
   switch (tile_cfg) {
     // 256x256 8-phase ping-pong (gemm8p_kernel)
     case 22: return launch_8p<EPI, GEMM8P_DEFAULT>(DLI_GEMM_PASS);
-    // 22 with the round-1 schedule (a counted vmcnt in every phase), for A/B runs
-    case 27: return launch_8p<EPI, GEMM8P_PER_PHASE_WAITS>(DLI_GEMM_PASS);
     // 256x224 ping-pong (gemm8p224_kernel): N = 28672 gate/up at M = 512 is 256 tiles
     case 26: return launch_8p224<EPI>(DLI_GEMM_PASS);
     // 256x128 ping-pong (gemm8p128_kernel): Mixtral grouped down (8 x 32 tiles), N = 4096 at

@@ -39,7 +39,7 @@ __device__ __forceinline__ void store_pair_or_one(void* C, int ldc, int row, int
 }
 
 // fp32 split-K partial stores: 0 plain (the line stays dirty in the XCD's L2 and is written
-// back at the kernel boundary, MI355X_MICROARCH.md price row 'boundary'), 1 nontemporal,
+// back at the kernel boundary, /opt/skills/guides/MI355X_MICROARCH.md price row 'boundary'), 1 nontemporal,
 // 2 sc1 (write-through: the bytes leave L2 while the GEMM still computes), 3 sc0 sc1.
 // One copy per translation unit (device code is not relocatable across files, -fno-gpu-rdc):
 // every GEMM family sets its own through set_slab_store_tu(), dli_gemm_set_slab_store sets all.
@@ -82,8 +82,9 @@ __device__ __forceinline__ void slab_store4(float* p, f32x4 v, int mode) {
   }
 }
 
-// one split-K partial quad: p = &slab[row][col]; vec = (N % 4 == 0), so col + 3 < N
-__device__ __forceinline__ void slab_quad(float* p, f32x4 v, int mode, bool vec, int left) {
+// the fp32 partial quad (store modes 0-3); the 4-wave family calls it directly (its
+// accumulator-pinned epilogue has no register room for the probe modes)
+__device__ __forceinline__ void slab_quad_fp32(float* p, f32x4 v, int mode, bool vec, int left) {
   if (vec) {
     slab_store4(p, v, mode);
   } else {
@@ -91,6 +92,29 @@ __device__ __forceinline__ void slab_quad(float* p, f32x4 v, int mode, bool vec,
     for (int r = 0; r < 4; ++r)
       if (r < left) slab_store(p + r, v[r], mode);
   }
+}
+
+// one split-K partial quad: p = &slab[row][col]; vec = (N % 4 == 0), so col + 3 < N.
+// Probe modes (dli_gemm_set_slab_store): 4 = bf16 partials at the same element index of a
+// bf16 [splits][M][N] image based at ws, 5 = no store (timing only: the consumer reads junk)
+__device__ __forceinline__ void slab_quad(float* p, f32x4 v, int mode, bool vec, int left,
+                                          const float* ws) {
+  if (mode == 5) return;
+  if (mode == 4) {
+    u16* q = (u16*)ws + (p - ws);
+    if (vec) {
+      uint2 pk;
+      pk.x = pack2bf(v[0], v[1]);
+      pk.y = pack2bf(v[2], v[3]);
+      *reinterpret_cast<uint2*>(q) = pk;
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (r < left) q[r] = f2bf(v[r]);
+    }
+    return;
+  }
+  slab_quad_fp32(p, v, mode, vec, left);
 }
 
 // four consecutive output columns [col, col + 4) of one row; vec = (N % 4 == 0 && ldc % 4

@@ -166,7 +166,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
         const int col = n0 + wn * TN + 16 * j + 4 * fq;
-        if (col < N) slab_quad(srow + col, acc[i][j], sm, vec, N - col);
+        if (col < N) slab_quad(srow + col, acc[i][j], sm, vec, N - col, ws);
       }
     }
     return;

@@ -1,6 +1,5 @@
-// Weight-streaming skinny GEMM for M <= 4 rows (tile ids 29-33, 56-59), its in-launch split-K
-// combine + residual add + RMSNorm (dli_gemv_add_rmsnorm), and the batch-1 reduce-free forms
-// (dli_gemv_fused: residual-adding epilogue, RMSNorm prologue).
+// Weight-streaming skinny GEMM for M <= 4 rows (tile ids 29-33, 56-59) and the batch-1
+// reduce-free forms (dli_gemv_fused: residual-adding epilogue, RMSNorm prologue).
 #include "gemm_common.h"
 
 // ---------------------------------------------------------------------------------------
@@ -9,7 +8,7 @@
 // kernel is a weight stream, not an MFMA tile. A workgroup (4 waves) owns R = 4 * RW output
 // rows of W over one K slice; in a wave, lane l covers the 8 K-elements [8 (l + 64 s),
 // +8) of step s for its RW rows: RW 16-B nontemporal weight loads per step (the weights are
-// read exactly once, MI355X_MICROARCH.md 'nt-weights'), two steps in flight, bf16 pairs
+// read exactly once, /opt/skills/guides/MI355X_MICROARCH.md 'nt-weights'), two steps in flight, bf16 pairs
 // accumulated by v_dot2c_f32_bf16 against x (M rows, L1/L2-resident). Lane partial sums
 // are reduced across the wave with shuffles and staged in LDS; the epilogue then writes
 // bf16 / fp32 / SiLU(gate)*up (the 16-row interleaved gate/up weight: a workgroup's 32 rows
@@ -349,194 +348,6 @@ static int launch_gemv(const void* A, int lda, const void* W, int ldw, void* C, 
     }
   }
   DLI_RETURN_LAUNCH();
-}
-
-// ---------------------------------------------------------------------------------------
-// Weight-streaming GEMV with the split-K combine, residual add and RMSNorm inside the launch
-// (M <= 4: batch-1 decode): residual += x . W^T (bf16-rounded), out = rmsnorm(residual) * w.
-// Replaces gemv (slabs) + splitk_add_rmsnorm (a second launch re-reading every slab): at
-// M = 1 a column block's slabs are S x 64 B, far below the size where an in-launch combine
-// stops paying (cdna_hip_programming.md §5 'Projection GEMM at M = 256' item 2).
-//
-// Two arrival tickets, no workgroup ever waits on another (deadlock-free at any residency):
-//  1. every K-slice workgroup publishes its partial column block with agent-scope (sc1)
-//     stores -> s_waitcnt vmcnt(0) in every wave -> barrier -> one relaxed agent fetch_add on
-//     cnt[block]; the workgroup drawing S - 1 reduces the block: partials summed in slice
-//     order 0..S-1 from 0 (splitk_add_rmsnorm's order, so residual is bit-identical), read
-//     with agent-scope (sc1) loads, residual updated with sc1 stores;
-//  2. the same publish -> ticket on cnt[nblk]; the column-block reducer drawing nblk - 1
-//     normalises every row (ss over the row in a fixed order: deterministic, one workgroup).
-// The last arriver of each ticket resets its counter (counters start zeroed: allocated once,
-// never shared by two launches in flight — every user runs on one stream).
-__device__ __forceinline__ void st_agent_f32(float* p, float v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float ld_agent_f32(const float* p) {
-  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_agent_u32(uint32_t* p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t ld_agent_u32(const uint32_t* p) {
-  return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-}
-// every wave's stores retired, then the workgroup; lane 0 draws a ticket on *c: true in the
-// workgroup that drew n - 1 (which also resets *c)
-__device__ __forceinline__ bool arrive_last(unsigned* c, unsigned n, int* flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned t = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const bool last = t == n - 1;
-    if (last) __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag = last;
-  }
-  __syncthreads();
-  return *flag != 0;
-}
-
-// the column-block combine of gemv_addnorm_kernel with the slice count known at compile
-// time: every partial of a thread is loaded before the first add (no per-slice select:
-// cdna_hip_programming.md §5 item 4(c)), summed in slice order 0..S-1 from 0
-template <int MB, int R, int S>
-__device__ __forceinline__ void combine_block(const float* __restrict__ ws, int M, int N,
-                                              int n_base, u16* __restrict__ residual) {
-  for (int t = threadIdx.x; t < MB * (R / 2); t += 256) {
-    const int m = t / (R / 2), j = 2 * (t % (R / 2)), n = n_base + j;
-    if (m >= M || n >= N) continue;
-    float p0[S], p1[S];
-#pragma unroll
-    for (int s = 0; s < S; ++s) {
-      const float* p = ws + ((long)s * M + m) * N + n;
-      p0[s] = ld_agent_f32(p);
-      p1[s] = ld_agent_f32(p + 1);
-    }
-    uint32_t* rp = reinterpret_cast<uint32_t*>(residual + (long)m * N + n);
-    const uint32_t r2 = *rp;
-    float acc0 = 0.f, acc1 = 0.f;
-#pragma unroll
-    for (int s = 0; s < S; ++s) { acc0 += p0[s]; acc1 += p1[s]; }
-    const float v0 = bf2f(f2bf(bf2f((u16)(r2 & 0xffffu)) + bf2f(f2bf(acc0))));
-    const float v1 = bf2f(f2bf(bf2f((u16)(r2 >> 16)) + bf2f(f2bf(acc1))));
-    st_agent_u32(rp, pack2bf(v0, v1));
-  }
-}
-
-template <int MB, int RW, int UNROLL>
-__global__ void __launch_bounds__(256) gemv_addnorm_kernel(
-    const u16* __restrict__ A, int lda, const u16* __restrict__ W, int ldw, int M, int N,
-    int K, int k_split_len, u16* __restrict__ residual, u16* __restrict__ out,
-    const u16* __restrict__ nw, float eps, float* __restrict__ ws, unsigned* __restrict__ cnt) {
-  constexpr int R = 4 * RW;
-  __shared__ float res[MB][R];
-  __shared__ float red[16];
-  __shared__ int flag;
-  const int n_base = blockIdx.x * R;
-  const int ks = blockIdx.y, S = gridDim.y, nblk = gridDim.x;
-  const int wid = threadIdx.x >> 6;
-  NoPrologue pro;
-  gemv_core<MB, RW, UNROLL>(A, lda, W, ldw, M, N, K, k_split_len, n_base + wid * RW, ks, res,
-                            pro);
-  __syncthreads();
-  for (int t = threadIdx.x; t < MB * R; t += 256) {
-    const int m = t / R, j = t % R, n = n_base + j;
-    if (m < M && n < N) st_agent_f32(ws + ((long)ks * M + m) * N + n, res[m][j]);
-  }
-  if (!arrive_last(cnt + blockIdx.x, (unsigned)S, &flag)) return;
-  // ---- column-block reducer (the launcher admits S in {2, 4, 8})
-  if (S == 2) combine_block<MB, R, 2>(ws, M, N, n_base, residual);
-  else if (S == 4) combine_block<MB, R, 4>(ws, M, N, n_base, residual);
-  else combine_block<MB, R, 8>(ws, M, N, n_base, residual);
-  if (nw == nullptr) return;                          // a stage's last layer: residual only
-  if (!arrive_last(cnt + nblk, (unsigned)nblk, &flag)) return;
-  // ---- the last column block: RMSNorm of every row. A thread owns bf16 pairs
-  // i = tid + 256 q (q < 8 per pass): all 8 loads issued before any use, indices clamped
-  // (duplicates masked out of the sum) instead of a per-element bounds branch
-  const int pairs = N >> 1;
-  const uint32_t* wrow = reinterpret_cast<const uint32_t*>(nw);
-  for (int m = 0; m < M; ++m) {
-    const uint32_t* rrow = reinterpret_cast<const uint32_t*>(residual + (long)m * N);
-    uint32_t* orow = reinterpret_cast<uint32_t*>(out + (long)m * N);
-    float ss = 0.f;
-    for (int b = 0; b < pairs; b += 256 * 8) {
-      uint32_t r2[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) r2[q] = ld_agent_u32(rrow + min(b + (int)threadIdx.x + 256 * q, pairs - 1));
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const float a = bf2f((u16)(r2[q] & 0xffffu)), c = bf2f((u16)(r2[q] >> 16));
-        ss += (b + (int)threadIdx.x + 256 * q < pairs) ? a * a + c * c : 0.f;
-      }
-    }
-    const float rstd = rsqrtf(block_sum(ss, red) / N + eps);
-    for (int b = 0; b < pairs; b += 256 * 8) {
-      uint32_t r2[8], w2[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int i = min(b + (int)threadIdx.x + 256 * q, pairs - 1);
-        r2[q] = ld_agent_u32(rrow + i);
-        w2[q] = wrow[i];
-      }
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int i = b + (int)threadIdx.x + 256 * q;
-        if (i < pairs)
-          orow[i] = pack2bf(bf2f((u16)(r2[q] & 0xffffu)) * rstd * bf2f((u16)(w2[q] & 0xffffu)),
-                            bf2f((u16)(r2[q] >> 16)) * rstd * bf2f((u16)(w2[q] >> 16)));
-      }
-    }
-    __syncthreads();                                  // red[] reused by the next row
-  }
-}
-
-template <int MB, int RW, int UNROLL>
-static int launch_gemv_addnorm(const void* A, int lda, const void* W, int ldw, int M, int N,
-                               int K, int splits, void* residual, void* out, const void* nw,
-                               float eps, void* ws, unsigned* cnt, hipStream_t st) {
-  constexpr int R = 4 * RW;
-  if (M > MB || K % 8 || lda % 8 || ldw % 8 || N % 2 ||
-      (splits != 2 && splits != 4 && splits != 8))
-    return (int)hipErrorInvalidValue;
-  int ksl = K / splits;
-  ksl = (ksl / 8) * 8;
-  if (ksl * splits != K) return (int)hipErrorInvalidValue;
-  dim3 grid((N + R - 1) / R, splits);
-  gemv_addnorm_kernel<MB, RW, UNROLL><<<grid, 256, 0, st>>>(
-      (const u16*)A, lda, (const u16*)W, ldw, M, N, K, ksl, (u16*)residual, (u16*)out,
-      (const u16*)nw, eps, (float*)ws, cnt);
-  DLI_RETURN_LAUNCH();
-}
-
-// residual[M, N] += A[M, K] . W[N, K]^T; out = rmsnorm(residual) * nw (nw null: residual
-// only). tile_cfg 30 / 31 / 32 / 33 as dli_gemm's weight-streaming tiles; cnt: zeroed
-// uint32[>= N / 16 + 1] owned by the caller's stream; ws: fp32 [splits, M, N].
-extern "C" int dli_gemv_add_rmsnorm(const void* A, int lda, const void* W, int ldw, int M,
-                                    int N, int K, int tile_cfg, int splits, void* residual,
-                                    void* out, const void* nw, float eps, void* ws,
-                                    unsigned* cnt, hipStream_t st) {
-  if (M <= 0 || N <= 0) return 0;
-  if (ws == nullptr || cnt == nullptr || residual == nullptr || (nw != nullptr && out == nullptr))
-    return (int)hipErrorInvalidValue;
-#define DLI_GA(MB, RW, U) \
-  return launch_gemv_addnorm<MB, RW, U>(A, lda, W, ldw, M, N, K, splits, residual, out, nw, eps, ws, cnt, st)
-  switch (tile_cfg) {
-    case 32: if (M <= 1) DLI_GA(1, 4, 4); break;
-    case 33: if (M <= 1) DLI_GA(1, 8, 4); break;
-    case 30:
-      if (M <= 1) DLI_GA(1, 4, 2);
-      if (M <= 2) DLI_GA(2, 4, 2);
-      if (M <= 4) DLI_GA(4, 4, 2);
-      break;
-    case 31:
-      if (M <= 1) DLI_GA(1, 8, 2);
-      if (M <= 2) DLI_GA(2, 8, 2);
-      if (M <= 4) DLI_GA(4, 8, 2);
-      break;
-    default: break;
-  }
-#undef DLI_GA
-  return (int)hipErrorInvalidValue;
 }
 
 template <int EPI>

@@ -291,8 +291,7 @@ class StageRunner:
         prompt tokens admitted with them: 512 < M <= 1024 for a full 512-row batch). They run
         eagerly, and without these buckets their GEMMs took the fitted heuristic's 128-row
         tiles, not the tuned decode plans."""
-        if (os.environ.get("DLI_GEMM_AUTOTUNE", "1") != "1" or self.device.type != "cuda"
-                or os.environ.get("DLI_TUNE_MIXED", "1") != "1"):
+        if os.environ.get("DLI_GEMM_AUTOTUNE", "1") != "1" or self.device.type != "cuda":
             return
         top = min(1024, max_rows)
         buckets = [m for m in range(640, top + 128, 128) if m > self.max_batch and m <= 1024]

@@ -7,7 +7,6 @@ All functions take/return torch tensors and launch on torch's current stream.
 from __future__ import annotations
 
 import math
-import os
 import time
 from typing import Optional
 
@@ -19,17 +18,13 @@ from . import reference as R
 
 _native_call = N.call
 _p = N.ptr
-_FUSED_OFF = __import__("os").environ.get("DLI_NO_FUSED_REDUCE", "0") == "1"   # A/B switch
-# batch-1: split-K combine + add + RMSNorm inside the GEMV launch (DLI_GEMV_FUSED_NORM=1). Off by
-# default: its serial tail (two arrival tickets, one workgroup normalising the row) measured
-# 0.8 % slower per token than GEMV + splitk_add_rmsnorm (profiles/r5/s03/bench.jsonl)
-_FUSED_GEMV_NORM = os.environ.get("DLI_GEMV_FUSED_NORM", "0") == "1"
 # rows per expert from which eager (prefill) MoE GEMMs take the grouped 256x256 tile
-_MOE_PREFILL_ROWS = int(__import__("os").environ.get("DLI_MOE_PREFILL_ROWS", "1024"))
+_MOE_PREFILL_ROWS = 1024
 
 
 def _use_native(t: torch.Tensor) -> bool:
-    return t.is_cuda and N.native_enabled()
+    """GPU tensors always run the HIP kernels (no switch reroutes them to torch ops)."""
+    return t.is_cuda
 
 
 def _st():
@@ -235,8 +230,6 @@ def _splitk_plan(x, w):
     """A split-K plan for a GEMM whose partial sums feed a fused reduce, or None."""
     if not _use_native(x) or x.stride(-1) != 1 or w.stride(-1) != 1:
         return None
-    if _FUSED_OFF:
-        return None
     M, K = x.shape
     p = G.plan(M, w.shape[0], K, "splitk")
     return p if p.splits > 1 else None
@@ -261,14 +254,6 @@ def linear_add_rmsnorm(x, w, residual, norm_w, eps, plan: Optional[G.GemmPlan] =
     Nn = w.shape[0]
     ws = G.workspace(x.device, p.splits * M * Nn * 4)
     out = torch.empty_like(residual) if norm_w is not None else None
-    if (p.tile in G.GEMV_FUSED_NORM_TILES and M <= G.GEMV_MAX_M and p.splits in (2, 4, 8)
-            and residual.is_contiguous() and _FUSED_GEMV_NORM):
-        # batch-1 decode: the split-K combine + residual add + RMSNorm run inside the GEMV's
-        # own launch (arrival tickets; gemm.hip gemv_addnorm_kernel), no second kernel
-        _native_call("dli_gemv_add_rmsnorm", _p(x), x.stride(0), _p(w), w.stride(-2), M, Nn,
-                     K, p.tile, p.splits, _p(residual), _p(out), _p(norm_w), eps, _p(ws),
-                     _p(G.tickets(x.device, Nn // 16 + 2, _st())), _st())
-        return out
     _native_call("dli_gemm", _p(x), x.stride(0), _p(w), w.stride(-2), None, Nn, M, Nn, K,
                  0, p.tile, p.splits, None, _p(ws), None, 1, _st())
     _native_call("dli_splitk_add_rmsnorm", _p(out), _p(residual), _p(ws), p.splits, M, Nn,
@@ -312,10 +297,9 @@ def linear_rope_attention(x, w, positions, slot_mapping, cos_sin, k_cache, v_cac
     ``linear_rope_cache`` + ``decode_attention``. Returns the attention output [B, hq*hd], or
     None where the fused kernel does not apply (the caller then runs the two-kernel path):
     split counts other than 2 / 4, KV-split attention (long contexts at small batch), the
-    pipelined long-context kernel, head dim != 128. ``DLI_FUSED_ROPE_ATTN=0`` turns it off."""
+    pipelined long-context kernel, head dim != 128."""
     xr = x.residual if isinstance(x, NormedRows) else x
-    if (os.environ.get("DLI_FUSED_ROPE_ATTN", "1") != "1" or hd != 128 or k_cache is None
-            or not _use_native(xr)):
+    if hd != 128 or k_cache is None or not _use_native(xr):
         return None
     p = _splitk_plan(xr, w)
     if p is not None and p.splits not in (2, 4):
@@ -429,10 +413,17 @@ def prefill_attention(qkv, cu_seqlens, max_seqlen: int, hq, hkv, hd, scale, out=
 
 
 def decode_pipelined(v: int) -> int:
-    """Select the pipelined (1), one-tile-per-round (0) or automatic (2: pipelined for KV
-    splits of >= 768 tokens) decode attention kernel for head_dim 128 (-1: from
-    DLI_DECODE_PIPE, default 2). Returns the previous setting."""
+    """Select the pipelined (1), one-tile-per-round (0) or automatic (2, the default: pipelined
+    for KV splits of >= 768 tokens) decode attention kernel for head_dim 128. Returns the
+    previous setting (tests force either kernel with it)."""
     return int(N.require_native().dli_decode_set_pipe(int(v)))
+
+
+def decode_form(v: int) -> int:
+    """Force the unsplit decode attention's form: 1 = a wave per (sequence, kv head), 4 = a
+    workgroup per item, 0 = automatic (workgroup per item for <= 256 items). Returns the
+    previous setting (tests force either form with it)."""
+    return int(N.require_native().dli_decode_set_form(int(v)))
 
 
 def prefill_long_min_len(n: int = 0) -> int:
@@ -515,7 +506,6 @@ def decode_attention(qkv, k_cache, v_cache, block_tables, context_lens, max_cont
 
 
 # ----------------------------------------------------------------------------- sampling
-_SAMPLE_SPLIT = __import__("os").environ.get("DLI_SAMPLE_SPLIT", "1") == "1"   # A/B switch
 _sample_wss: dict = {}
 
 
@@ -523,8 +513,6 @@ def _sample_ws(device, B: int, V: int):
     """Zero-initialised scratch of the two-phase small-batch sampler (sampling.hip
     sample_chunk_kernel: B <= 8 rows split over up to 64 workgroups each), or None. One buffer
     per device, sized for the largest batch; the kernels leave its overflow flags zero."""
-    if not _SAMPLE_SPLIT:
-        return None
     lib = N.require_native()
     if int(lib.dli_sample_workspace_bytes(B, V)) == 0:
         return None
@@ -541,13 +529,11 @@ def _sample_ws(device, B: int, V: int):
     return ws
 
 
-# LM-head output dtype. Default fp32 (the head GEMM accumulates in fp32 and stores it).
-# DLI_BF16_LOGITS=1 stores the model dtype instead, as HF's ``lm_head(h).float()`` rounds it:
-# same-box A/B at batch 512 (profiles/r5/s05/ab.jsonl) gave no gain — the head GEMM is
-# MFMA-bound at the same 407 us either way and only the sampler got 20 us faster — while a
-# request's tokens then depend on which GEMM plan (batch size) computed its logits (one
-# bf16 rounding flip changes a draw), which breaks batch-invariant seeded sampling.
-HEAD_EPI = "none" if os.environ.get("DLI_BF16_LOGITS", "0") == "1" else "f32"
+# LM-head output dtype: fp32 (the head GEMM accumulates in fp32 and stores it). bf16 logits
+# were measured without a gain at batch 512 (profiles/r5/s05/ab.jsonl: the head GEMM is
+# MFMA-bound at the same 407 us either way) and make a request's draws depend on which GEMM
+# plan (batch size) rounded its logits, which breaks batch-invariant seeded sampling.
+HEAD_EPI = "f32"
 
 
 def sample(logits, temperature, top_k, top_p, seeds, generator=None, ids=None):

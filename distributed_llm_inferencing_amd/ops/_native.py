@@ -47,6 +47,7 @@ _SIGS = {
     "dli_sample_set_split_max_b": [I],
     "dli_decode_set_pipe": [I],
     "dli_decode_get_pipe": [],
+    "dli_decode_set_form": [I],
     "dli_gemm_set_slab_store": [I],
     "dli_gemm_set_slab_store_family": [I, I],
     "dli_prefill_attention_paged": [P, I, P, I, P, P, P, P, P, I, I, I, I, I, I, I, F, P],
@@ -57,7 +58,6 @@ _SIGS = {
     "dli_topk_rows": [P, P, P, L, I, I, I, I, P],
     "dli_gemm": [P, I, P, I, P, I, I, I, I, I, I, I, P, P, P, I, P],
     "dli_splitk_add_rmsnorm": [P, P, P, I, I, I, P, F, P],
-    "dli_gemv_add_rmsnorm": [P, I, P, I, I, I, I, I, I, P, P, P, F, P, P, P],
     "dli_gemv_fused": [P, I, P, F, P, I, P, I, I, I, I, I, I, I, P, P],
     "dli_splitk_rope_cache": [P, P, I, I, I, P, P, P, P, P, I, I, I, I, I, P],
     "dli_decode_attention_fused": [P, P, I, P, P, P, P, P, P, I, P, I, I, I, I, I, F, P],
@@ -100,16 +100,6 @@ def _load():
                 fn = getattr(lib, name)
                 fn.argtypes = args
                 fn.restype = ctypes.c_long if name.endswith("_bytes") else ctypes.c_int
-            if os.environ.get("DLI_PREFILL_PACK", "1") == "0":   # A/B: unpacked prefill
-                lib.dli_prefill_set_pack(0)
-            if os.environ.get("DLI_SAMPLE_SPLIT_MAX_B"):         # A/B: two-phase sampler
-                lib.dli_sample_set_split_max_b(int(os.environ["DLI_SAMPLE_SPLIT_MAX_B"]))
-            # split-K slab store per GEMM family (A/B: DLI_SLAB_STORE_TILES / _8P / _4W =
-            # 0 plain, 1 nt, 2 sc1 write-through, 3 sc0 sc1)
-            for fam, var in enumerate(("DLI_SLAB_STORE_TILES", "DLI_SLAB_STORE_8P",
-                                       "DLI_SLAB_STORE_4W")):
-                if os.environ.get(var):
-                    lib.dli_gemm_set_slab_store_family(fam, int(os.environ[var]))
             _lib = lib
         except Exception as e:  # noqa: BLE001 - surfaced by require_native()
             _load_error = e
@@ -167,6 +157,3 @@ def loaded_path() -> str | None:
     return str(LIB_PATH) if _lib is not None else None
 
 
-def native_enabled() -> bool:
-    """False only when explicitly disabled for debugging (DLI_FORCE_TORCH=1)."""
-    return os.environ.get("DLI_FORCE_TORCH", "0") != "1"

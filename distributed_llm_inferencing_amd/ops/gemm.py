@@ -42,8 +42,6 @@ TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256), 4: (256, 128),
          23: (128, 192), 24: (128, 192), 25: (256, 192),
          # 256x224 ping-pong: N = 28672 (Llama-3 gate/up) at M = 512 = 256 tiles on 256 CUs
          26: (256, 224),
-         # 22 with the round-1 schedule (a vmcnt wait every phase), for A/B runs only
-         27: (256, 256),
          # 256x128 ping-pong: Mixtral grouped down (N = 4096: 32 column tiles per expert),
          # N = 4096 at M = 512 with split-K 4
          28: (256, 128),
@@ -57,13 +55,13 @@ TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256), 4: (256, 128),
          # K-tiles staged in the current tile's last two (gemm4wp.hip); no split-K / grouped
          55: (256, 256)}
 # the 4-wave plan raced against the 8-phase one in the prefill autotune
-PREFILL_4W_TILE = int(os.environ.get("DLI_GEMM_PREFILL_4W", "45"))
-# the persistent 4-wave tile (55) raced too (DLI_GEMM_PREFILL_PERSIST=0: not a candidate)
-PREFILL_PERSIST = os.environ.get("DLI_GEMM_PREFILL_PERSIST", "1") == "1"
+PREFILL_4W_TILE = 45
+# the persistent 4-wave tile (55) raced too
+PREFILL_PERSIST = True
 # prefill-sized grouped expert GEMMs (ops.moe_mlp's eager path): Mixtral 8x7B at 32k routed
 # rows, tile 45 vs the 8-phase tile 22: down 2,895 vs 3,071-3,239 us, gate/up 5,736 vs
 # 5,898 us (profiles/r4/moe/)
-MOE_PREFILL_TILE = int(os.environ.get("DLI_MOE_PREFILL_TILE", "45"))
+MOE_PREFILL_TILE = 45
 # weight-streaming skinny GEMM (gemm.hip gemv_kernel) for M <= GEMV_MAX_M rows: 16 / 32 output
 # rows per workgroup (31 for the SiLU*up gate/up pairing); not an MFMA tile, so kept apart
 GEMV_TILES = {30: 16, 31: 32, 32: 16, 33: 32,   # 32 / 33: 4 K-steps in flight per lane, M = 1
@@ -72,9 +70,6 @@ GEMV_TILES = {30: 16, 31: 32, 32: 16, 33: 32,   # 32 / 33: 4 K-steps in flight p
               58: 4, 59: 8}   # SiLU*up pairing (2 + 2 / 4 + 4 rows), 8 K-steps in flight
 GEMV_M1_ONLY = (32, 33)
 GEMV_MAX_M = 4
-# weight-streaming tiles whose split-K combine + residual add + RMSNorm run in-launch
-# (ops.linear_add_rmsnorm -> dli_gemv_add_rmsnorm)
-GEMV_FUSED_NORM_TILES = (30, 31, 32, 33)
 # batch-1 decode without split-K reduces (ops.linear_residual, ops.NormedRows): the GEMVs that
 # add into the residual (epi "res", full K per workgroup) and the tiles whose prologue applies
 # a deferred RMSNorm to their input rows (gemv.hip dli_gemv_fused)
@@ -85,7 +80,7 @@ GEMV_PRO_M1_ONLY = (32, 33)
 DEFER_NORM = os.environ.get("DLI_DEFER_NORM", "1") == "1"
 TILE_WAVES = {13: (2, 4), 14: (4, 2), 15: (2, 4), 16: (4, 2), 17: (2, 4),
               22: (2, 4), 23: (2, 4), 24: (2, 4), 25: (4, 2),
-              26: (4, 2), 27: (2, 4), 28: (4, 2)}
+              26: (4, 2), 28: (4, 2)}
 
 
 def tile_ok(tile: int, epi: str) -> bool:
@@ -108,7 +103,7 @@ def tile_ok(tile: int, epi: str) -> bool:
 # "splitk": a plain GEMM whose fp32 partial slabs feed a fused reduce (ops.linear_add_rmsnorm,
 # ops.linear_rope_cache); planned/tuned separately (a non-split winner runs unfused).
 EPI = {"none": 0, "f32": 1, "silu_mul": 2, "bias_gelu": 3, "bias": 4, "splitk": 0}
-NUM_CUS = int(os.environ.get("DLI_NUM_CUS", "256"))
+NUM_CUS = 256
 
 
 @dataclass(frozen=True)
@@ -160,7 +155,7 @@ def workspace(device: torch.device, nbytes: int) -> torch.Tensor:
         return ws
 
 
-LARGE_M = int(os.environ.get("DLI_GEMM_LARGE_M", "1024"))
+LARGE_M = 1024
 
 
 def _heuristic(M: int, N: int, K: int, epi: str) -> GemmPlan:
@@ -377,8 +372,7 @@ def autotune(shapes, weights: dict, device, iters: int = 6, log=None,
             # kernel where the plan's split count allows it (ops.linear_rope_attention), else
             # the RoPE/cache kernel + attention; time each plan with the path it will run
             # (one-token contexts: the launch and dependency structure, not the KV stream)
-            decode_qkv = (M <= 512 and candidates is None
-                          and os.environ.get("DLI_TUNE_QKV_ATTN", "1") == "1")
+            decode_qkv = M <= 512 and candidates is None
             if decode_qkv:
                 bt = (slots // 16).to(torch.int32).unsqueeze(1).contiguous()
                 ctx = torch.ones(M, dtype=torch.int32, device=device)
@@ -428,9 +422,9 @@ def autotune(shapes, weights: dict, device, iters: int = 6, log=None,
 # candidate order let drift and noise pick among plans a few % apart: two runs of the same
 # tree on one box pinned different QKV plans (128x192 split 2 vs 128x96 unsplit,
 # profiles/r4/prof vs profiles/r5/s06 wave summaries)
-FINAL_BAND = float(os.environ.get("DLI_TUNE_FINAL_BAND", "0.06"))
-FINAL_N = int(os.environ.get("DLI_TUNE_FINAL_N", "4"))
-FINAL_ROUNDS = int(os.environ.get("DLI_TUNE_FINAL_ROUNDS", "3"))
+FINAL_BAND = 0.06
+FINAL_N = 4
+FINAL_ROUNDS = 3
 
 
 def _final_round(ops, timed, iters: int, n_copies: int):
@@ -487,8 +481,8 @@ class _forced_plan:
 
 
 _tuned: set = set()
-# candidates timed as graph replays (ops.benchmark graph=True); DLI_GEMM_TUNE_GRAPH=0: eager
-_GRAPH_TUNE = os.environ.get("DLI_GEMM_TUNE_GRAPH", "1") == "1"
+# candidates timed as graph replays (ops.benchmark graph=True)
+_GRAPH_TUNE = True
 
 
 def prefill_candidates(M: int, N: int, K: int, epi: str):
@@ -515,7 +509,7 @@ def candidate_plans(M: int, N: int, K: int, epi: str):
     # Default: 26 (256x224). It fills all 256 CUs on the gate/up GEMM and wins the isolated
     # autotune (98.8 vs ~106 us), but in the decode step it ran 97.9 vs 99.0 us per call and
     # the bench 0.3-0.7 % lower in three same-box A/B runs (profiles/r2_s2/README.md)
-    # 27 is tile 22 with the round-1 wait schedule (A/B reference only); 45 stays
+    # 45 stays
     # prefill-only too (no gain in a same-box bench A/B, profiles/r4/bench/s18_*); 41 won
     # isolated decode timings (M = 512 LM head 4-7 %) but cost the step 1.8 % in a same-box
     # bench A/B (42,548 without vs 41,790 / 41,653 tok/s with, profiles/r4/bench/)
@@ -524,7 +518,7 @@ def candidate_plans(M: int, N: int, K: int, epi: str):
     # but loses in the decode graph — down at M = 512 ran 70.4 us on tile 34 against 56.9 on
     # the 8-phase tile 22, the LM head 433 vs 407 (profiles/r5/s12/wave_summary.txt vs
     # profiles/r4/prof/llama_b512_head.wave.txt); the autotune flipped between them run to run
-    excl = {int(t) for t in (excl_env if excl_env is not None else "26,27,34,41,45,55").split(",")
+    excl = {int(t) for t in (excl_env if excl_env is not None else "26,34,41,45,55").split(",")
             if t.strip()}
     # ... except where 256x256 tiles take more than one wave of the chip and 256x224 tiles
     # land on a whole number of waves (Llama-3-70B gate/up at M = 512: N = 57344 is 448
@@ -535,11 +529,6 @@ def candidate_plans(M: int, N: int, K: int, epi: str):
         t224 = -(-M // 256) * -(-N // 224)
         if t256 > NUM_CUS and t224 % NUM_CUS == 0:
             excl.discard(26)
-    # DLI_GEMM_HEAD_4W=1 (A/B): the two-barrier 4-wave tile competes for the fp32-output LM
-    # head (several waves of 256x256 tiles), where it ran 3-7 % faster in isolation
-    if excl_env is None and epi == "f32" and os.environ.get("DLI_GEMM_HEAD_4W", "0") == "1":
-        excl.discard(45)
-        excl.discard(55)
     for tile, (bm, bn) in TILES.items():
         if not tile_ok(tile, epi) or tile in excl:
             continue

@@ -336,6 +336,56 @@ class ExpertParallelEngine:
         # from the lockstep exchange and leaves the loop once no rank has work
         self.stop_requested = False
         self.stopping = False
+        # lockstep control plane: the shared-memory board when every rank is on this host
+        # (the single-node deployment), else the gloo all_gather; host seconds spent in it
+        self.board = self._open_board()
+        self.control_plane = "shm" if self.board is not None else "gloo"
+        self.lockstep_s = 0.0
+
+    def _open_board(self):
+        """A ``LockstepBoard`` shared by every rank of the group, or None when the ranks span
+        hosts (or the runtime library is unavailable)."""
+        import socket
+        hosts = [None] * self.world
+        dist.all_gather_object(hosts, socket.gethostname(), group=self.ctrl_group)
+        # DLI_EP_CTRL=gloo keeps the socket all_gather (A/B of the control plane, like
+        # DLI_PP_CTRL for the pipeline)
+        if (self.world == 1 or len(set(hosts)) != 1
+                or os.environ.get("DLI_EP_CTRL", "auto") == "gloo"):
+            return None
+        try:
+            from ..runtime import LockstepBoard
+            name = [f"/dli_ep_board_{os.environ.get('MASTER_PORT', '0')}_{os.getpid()}"
+                    if self.rank == 0 else None]
+            board = LockstepBoard.create(name[0], self.world) if self.rank == 0 else None
+            dist.broadcast_object_list(name, src=0, group=self.ctrl_group)
+            if board is None:
+                board = LockstepBoard.open(name[0])
+            board.join(self.rank)
+            dist.barrier(group=self.ctrl_group)
+            if self.rank == 0:
+                board.unlink()
+            return board
+        except (OSError, RuntimeError) as e:
+            _log.warning("expert-parallel rank %d: shared-memory lockstep board unavailable "
+                         "(%s); the lockstep exchange uses gloo", self.rank, e)
+            return None
+
+    def ring_bell(self) -> None:
+        """Wake every rank sleeping in ``wait_bell`` (a request arrived, or a stop)."""
+        if self.board is not None:
+            self.board.ring()
+
+    def bell(self) -> int:
+        return self.board.bell() if self.board is not None else 0
+
+    def wait_bell(self, seen: int, timeout_s: float) -> None:
+        """Idle: sleep until some rank rings the doorbell (without the board: ``timeout_s``
+        capped at a short poll period)."""
+        if self.board is not None:
+            self.board.wait_bell(seen, timeout_s)
+        else:
+            time.sleep(min(timeout_s, 0.002))
 
     def warmup(self):
         """Capture the decode graphs (every rank, same bucket order: the warm-up forwards
@@ -362,12 +412,17 @@ class ExpertParallelEngine:
         RCCL all-gather read back with ``.tolist()`` would drain this rank's stream (the
         in-flight step included) before the next step could even be planned, defeating
         lookahead; the routing itself stays on the device (mailbox headers)."""
-        mine = torch.tensor([1 if work else 0, tokens, 1 if self.stop_requested else 0],
-                            dtype=torch.int64)
-        allv = [torch.empty_like(mine) for _ in range(self.world)]
-        dist.all_gather(allv, mine, group=self.ctrl_group)
+        t0 = time.perf_counter()
+        words = [1 if work else 0, tokens, 1 if self.stop_requested else 0]
+        if self.board is not None:
+            rows = self.board.exchange(words).tolist()
+        else:
+            mine = torch.tensor(words, dtype=torch.int64)
+            allv = [torch.empty_like(mine) for _ in range(self.world)]
+            dist.all_gather(allv, mine, group=self.ctrl_group)
+            rows = torch.stack(allv).tolist()
         self.lockstep_syncs += 1
-        rows = torch.stack(allv).tolist()
+        self.lockstep_s += time.perf_counter() - t0
         if any(r[2] for r in rows):
             self.stopping = True
         return [r[:2] for r in rows]
@@ -446,6 +501,8 @@ class ExpertParallelEngine:
 
     def close(self) -> None:
         self.moe.close()
+        if self.board is not None:
+            self.board.close()
 
 
 def _dir_config(model_dir: str, name: str):
@@ -523,6 +580,7 @@ def bench_expert_parallel(args, world, rank, make_prompts):
     dist.barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
+    eng.lockstep_s, eng.lockstep_syncs = 0.0, 0
     t0 = time.perf_counter()
     toks, lats = 0, []
     for s in range(args.steps):
@@ -550,4 +608,8 @@ def bench_expert_parallel(args, world, rank, make_prompts):
     return {"tokens": int(tt.item()), "seconds": float(dt.item()),
             "latencies": torch.cat(gathered).tolist(), "global_batch": args.batch * world,
             "parallelism": f"dp{world}-ep{world}", "data_plane": eng.data_plane,
-            "ranks_info": infos}
+            "ranks_info": infos,
+            "engine": {"control_plane": eng.control_plane,
+                       "lockstep_ms_per_step": round(1e3 * eng.lockstep_s
+                                                     / max(1, eng.lockstep_syncs), 4),
+                       "steps": eng.lockstep_syncs}}

@@ -135,6 +135,7 @@ class StageWorker:
                           self.device, dtype)
         self.runner = StageRunner(self.model, self.kv, max_batch, table_width, use_graphs)
         self.tick_counts: Dict[int, int] = {}     # non-head ranks: steps run, by kind
+        self._samp = None                         # pinned staging ring of _sampling
 
     @property
     def is_last(self) -> bool:
@@ -148,11 +149,40 @@ class StageWorker:
         return self.runner.run(meta, hidden=data)
 
     def _sampling(self, meta: StepMeta):
+        """(temperature, top_k, top_p, seeds) of ``meta`` on the device. On a GPU they go
+        through a ring of pinned staging buffers with async copies: a copy from pageable
+        memory waits for everything queued on the stream, which put the head's host in
+        lockstep with its GPU on every tick of the vocab-parallel head (rank 0's host time
+        per decode tick was ~the whole tick, profiles/r6/README.md)."""
         d = self.device
-        return (torch.from_numpy(np.ascontiguousarray(meta.temperature, np.float32)).to(d),
-                torch.from_numpy(np.ascontiguousarray(meta.top_k, np.int32)).to(d),
-                torch.from_numpy(np.ascontiguousarray(meta.top_p, np.float32)).to(d),
-                torch.from_numpy(np.ascontiguousarray(meta.seeds, np.int64)).to(d))
+        if d.type != "cuda":
+            return (torch.from_numpy(np.ascontiguousarray(meta.temperature, np.float32)),
+                    torch.from_numpy(np.ascontiguousarray(meta.top_k, np.int32)),
+                    torch.from_numpy(np.ascontiguousarray(meta.top_p, np.float32)),
+                    torch.from_numpy(np.ascontiguousarray(meta.seeds, np.int64)))
+        S, B = meta.num_seqs, self.max_batch
+        if self._samp is None:
+            # layout (int32 words): seeds (2B, first: an int64 view needs an even offset) |
+            # temperature (B) | top_k (B) | top_p (B)
+            ring = [torch.zeros(5 * B, dtype=torch.int32).pin_memory() for _ in range(8)]
+            self._samp = {"host": ring, "np": [t.numpy() for t in ring],
+                          "ev": [torch.cuda.Event() for _ in ring], "used": [False] * 8,
+                          "j": 0, "dev": torch.zeros(5 * B, dtype=torch.int32, device=d)}
+        R = self._samp
+        j = R["j"] = (R["j"] + 1) % len(R["host"])
+        if R["used"][j]:
+            R["ev"][j].synchronize()          # its copy 8 calls back: long done
+        h = R["np"][j]
+        h[:2 * S] = np.ascontiguousarray(meta.seeds, np.int64).view(np.int32)
+        h[2 * B:2 * B + S] = np.ascontiguousarray(meta.temperature, np.float32).view(np.int32)
+        h[3 * B:3 * B + S] = np.ascontiguousarray(meta.top_k, np.int32)
+        h[4 * B:4 * B + S] = np.ascontiguousarray(meta.top_p, np.float32).view(np.int32)
+        dev = R["dev"]
+        dev.copy_(R["host"][j], non_blocking=True)
+        R["ev"][j].record()
+        R["used"][j] = True
+        return (dev[2 * B:2 * B + S].view(torch.float32), dev[3 * B:3 * B + S],
+                dev[4 * B:4 * B + S].view(torch.float32), dev[:2 * S].view(torch.int64))
 
     def candidates(self, hf: torch.Tensor) -> torch.Tensor:
         """This rank's top-CAND of its vocab slice, packed int32 [S, 2*CAND] (values | ids)."""
@@ -469,7 +499,6 @@ def install_piped(stage: StageWorker, channel) -> bool:
     r, N = channel.rank, channel.world
     run = stage.runner
     if (channel.ipc is None or r == 0 or not run.use_graphs or run.hidden_in is None
-            or os.environ.get("DLI_PP_PIPED_GRAPHS", "1") != "1"
             or os.environ.get("DLI_PP_SCHEDULE", "piped") == "grouped"):
         return False
     tail = r == N - 1
@@ -939,7 +968,12 @@ def bench_pipeline(args, world: int, rank: int, make_prompts):
                                                            4096),
                                     shard_dir=getattr(args, "shard_dir", None))
     world = eng.world
+    t_w = time.perf_counter()
     eng.warmup()
+    if rank == 0:
+        import sys as _sys
+        print(f"[bench] pp{world} engine warm-up (autotune + capture): "
+              f"{time.perf_counter() - t_w:.1f} s", file=_sys.stderr, flush=True)
     sp = SamplingParams(max_length=args.max_length, temperature=0.8, top_k=50, top_p=0.95,
                         ignore_eos=True)
     per_wave = args.batch * eng.microbatches       # M microbatches of --batch requests
@@ -953,8 +987,16 @@ def bench_pipeline(args, world: int, rank: int, make_prompts):
         serve_session(eng.stage, eng.channel, bufs)
         return 0, []
 
+    def progress(what, i, n, t):
+        if rank == 0:
+            import sys as _sys
+            print(f"[bench] pp{world} {what} wave {i + 1}/{n}: {time.perf_counter() - t:.2f} s",
+                  file=_sys.stderr, flush=True)
+
     for w in range(args.warmup):
+        tw = time.perf_counter()
         wave(10_000 + w)
+        progress("warmup", w, args.warmup, tw)
     dist.barrier()
     if device.type == "cuda":
         torch.cuda.synchronize(device)
@@ -965,9 +1007,11 @@ def bench_pipeline(args, world: int, rank: int, make_prompts):
         eng.head.host_by_kind = {k: [0.0, 0] for k in eng.head.host_by_kind}
         eng.head.phase_s = {k: 0.0 for k in eng.head.phase_s}
     for s in range(args.steps):
+        tw = time.perf_counter()
         n, l = wave(s)
         toks += n
         lats += l
+        progress("timed", s, args.steps, tw)
     if device.type == "cuda":
         torch.cuda.synchronize(device)
     dist.barrier()

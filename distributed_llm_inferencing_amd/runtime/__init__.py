@@ -72,6 +72,18 @@ _SIGS = {
     "dli_ring_dead": ([_P], _I),
     "dli_ring_close": ([_P], None),
     "dli_ring_destroy": ([_P], None),
+    "dli_board_create": ([ctypes.c_char_p, _I], _P),
+    "dli_board_open": ([ctypes.c_char_p], _P),
+    "dli_board_join": ([_P, _I], _I),
+    "dli_board_unlink": ([_P], _I),
+    "dli_board_world": ([_P], _I),
+    "dli_board_exchange": ([_P, _P, _P, ctypes.c_double], _I),
+    "dli_board_bell": ([_P], ctypes.c_uint),
+    "dli_board_ring": ([_P], None),
+    "dli_board_wait_bell": ([_P, ctypes.c_uint, ctypes.c_double], ctypes.c_uint),
+    "dli_board_dead": ([_P], _I),
+    "dli_board_close": ([_P], None),
+    "dli_board_destroy": ([_P], None),
     "dli_comm_available": ([], _I),
     "dli_comm_async_error": ([_P], _I),
     "dli_comm_abort": ([_P], _I),
@@ -456,6 +468,95 @@ class ShmRing:
         h, self._h = self._h, None
         if h and _lib is not None:
             _lib.dli_ring_destroy(h)
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+class LockstepBoard:
+    """Per-step all-gather of a few int64 words between the processes of one node, in POSIX
+    shared memory (``csrc/runtime/lockstep.cpp``), plus a doorbell idle ranks sleep on. The
+    expert-parallel ranks' lockstep control plane: ``create`` on rank 0, ``open`` on the
+    others (after the name was shared), ``join(rank)`` on every rank, ``unlink`` once all
+    joined. Waits fail with ``TimeoutError`` / ``PeerGone`` instead of hanging."""
+
+    VALS = 4
+
+    class PeerGone(RuntimeError):
+        pass
+
+    def __init__(self, handle, name: str):
+        self._h, self.name = handle, name
+        self.world = int(lib().dli_board_world(handle))
+        self._out = np.zeros(self.world * self.VALS, dtype=np.int64)
+        self._in = np.zeros(self.VALS, dtype=np.int64)
+
+    @classmethod
+    def create(cls, name: str, world: int) -> "LockstepBoard":
+        h = lib().dli_board_create(name.encode(), int(world))
+        if not h:
+            raise OSError(f"cannot create lockstep board {name}")
+        return cls(h, name)
+
+    @classmethod
+    def open(cls, name: str, timeout_s: float = 60.0) -> "LockstepBoard":
+        import time
+        t0 = time.monotonic()
+        while True:
+            h = lib().dli_board_open(name.encode())
+            if h:
+                return cls(h, name)
+            if time.monotonic() - t0 > timeout_s:
+                raise OSError(f"cannot open lockstep board {name}")
+            time.sleep(0.01)
+
+    def join(self, rank: int) -> None:
+        if lib().dli_board_join(self._h, int(rank)) != 0:
+            raise ValueError(f"rank {rank} outside the board's {self.world} ranks")
+
+    def unlink(self) -> None:
+        lib().dli_board_unlink(self._h)
+
+    def exchange(self, words: Sequence[int], timeout_s: float = 120.0) -> np.ndarray:
+        """Publish ``words`` (<= 4 ints), return every rank's words [world, 4] (a view of a
+        buffer the next exchange overwrites)."""
+        self._in[:] = 0
+        self._in[:len(words)] = words
+        r = lib().dli_board_exchange(self._h, _np_ptr(self._in), _np_ptr(self._out),
+                                     float(timeout_s))
+        if r == -2:
+            raise self.PeerGone(f"lockstep peer rank {self.dead()} exited")
+        if r == -1:
+            raise TimeoutError(f"lockstep exchange timed out after {timeout_s} s")
+        if r != 0:
+            raise RuntimeError(f"lockstep board closed or not joined ({r})")
+        return self._out.reshape(self.world, self.VALS)
+
+    def bell(self) -> int:
+        return int(lib().dli_board_bell(self._h))
+
+    def ring(self) -> None:
+        lib().dli_board_ring(self._h)
+
+    def wait_bell(self, seen: int, timeout_s: float) -> int:
+        """Sleep (futex) until the doorbell moves past ``seen`` or ``timeout_s`` passes."""
+        return int(lib().dli_board_wait_bell(self._h, int(seen) & 0xffffffff,
+                                             float(timeout_s)))
+
+    def dead(self) -> int:
+        return int(lib().dli_board_dead(self._h)) if self._h else -1
+
+    def close(self) -> None:
+        if self._h:
+            lib().dli_board_close(self._h)
+
+    def destroy(self) -> None:
+        h, self._h = self._h, None
+        if h and _lib is not None:
+            _lib.dli_board_destroy(h)
 
     def __del__(self):
         try:

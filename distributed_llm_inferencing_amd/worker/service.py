@@ -231,13 +231,16 @@ class ExpertService:
     every rank is a worker node of its own (DP attention, its own requests and KV) whose MoE
     layers exchange rows with the other ranks every step. The ranks step in lockstep, so
     this thread keeps stepping while ANY rank has work — an idle rank joins every exchange
-    with an empty forward — and all ranks idle together (one lockstep exchange every
-    ``idle_s``) when none has. ``close`` raises the stop bit of the exchange: every rank
-    leaves its loop once no rank has work. A failed exchange (a peer died) fails every
-    pending request and sets ``error`` (the worker answers 503, the master's dispatcher
-    retries on another node)."""
+    with an empty forward — and when none has, every rank sleeps on the group's shared
+    doorbell (``ExpertParallelEngine.wait_bell``: a futex in the lockstep board) until a
+    submit on any rank rings it, re-checking the group once every ``idle_s`` (no CPU while
+    the group idles). ``close`` raises the stop bit of the exchange and rings: every rank
+    leaves its loop once no rank has work, and requests still queued then fail ("group
+    stopped"); submits after ``close`` fail at once. A failed exchange (a peer died) fails
+    every pending request and sets ``error`` (the worker answers 503, the master's
+    dispatcher retries on another node)."""
 
-    def __init__(self, ep_engine, name: str = "expert", idle_s: float = 0.002):
+    def __init__(self, ep_engine, name: str = "expert", idle_s: float = 1.0):
         self.engine = ep_engine
         self.name = name
         self.idle_s = idle_s
@@ -252,13 +255,17 @@ class ExpertService:
 
     def submit(self, prompt, params=None) -> Future:
         fut: Future = Future()
-        if self.error is not None or self.stopped.is_set():
-            fut.set_exception(PipelineFailed(f"expert group {self.name} is down: {self.error}"))
+        ep = self.engine
+        if (self.error is not None or self.stopped.is_set() or ep.stop_requested
+                or ep.stopping):
+            why = self.error if self.error is not None else "stopping"
+            fut.set_exception(PipelineFailed(f"expert group {self.name} is down: {why}"))
             return fut
         with self._lock:
             self._ids += 1
             rid = f"{self.name}-r{self.engine.rank}-{self._ids}"
         self._inbox.put((rid, prompt, params, fut))
+        ep.ring_bell()                      # wake the group if it sleeps
         return fut
 
     def generate(self, prompt, params=None, timeout=None):
@@ -292,8 +299,10 @@ class ExpertService:
 
     def _run(self):
         ep = self.engine
+        self.idle_waits = 0
         try:
             while True:
+                bell = ep.bell()                # read before looking for work (no lost ring)
                 self._admit()
                 outs, more = ep.step()
                 for o in outs:
@@ -302,8 +311,11 @@ class ExpertService:
                         f.set_result(o)
                 if ep.stopping and not more:
                     break
-                if not more:
-                    time.sleep(self.idle_s)     # every rank saw the same "no work"
+                if not more and self._inbox.empty():
+                    # every rank saw the same "no work": sleep until a submit on any rank
+                    self.idle_waits += 1
+                    ep.wait_bell(bell, self.idle_s)
+            self._fail_all(RuntimeError("group stopped"))   # submits that raced the stop
         except BaseException as e:  # noqa: BLE001 — a peer died or the data plane broke
             self.error = e
             self._fail_all(e)
@@ -320,4 +332,5 @@ class ExpertService:
     def close(self, timeout: float = 30.0) -> None:
         """Ask the whole group to stop (collective: every rank's service leaves its loop)."""
         self.engine.stop_requested = True
+        self.engine.ring_bell()
         self.stopped.wait(timeout)

@@ -1,0 +1,152 @@
+"""The expert-parallel lockstep control plane: the shared-memory board
+(``csrc/runtime/lockstep.cpp``) replaces the per-step gloo all_gather, and idle ranks sleep on
+its doorbell instead of exchanging every 2 ms. CPU, spawned processes."""
+from __future__ import annotations
+
+import os
+import resource
+import socket
+import time
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from distributed_llm_inferencing_amd.engine import SamplingParams
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _board_worker(rank, name, q, die):
+    from distributed_llm_inferencing_amd.runtime import LockstepBoard
+    b = LockstepBoard.create(name, 2) if rank == 0 else LockstepBoard.open(name)
+    b.join(rank)
+    for i in range(200):
+        rows = b.exchange([rank, i, 7 * rank + i])
+        assert rows[:, 0].tolist() == [0, 1] and rows[:, 1].tolist() == [i, i], rows
+        assert rows[1, 2] == 7 + i
+    if rank == 0:
+        b.unlink()
+    # doorbell: rank 1 sleeps, rank 0 rings after 0.3 s
+    if rank == 1:
+        seen = b.bell()
+        b.exchange([0])                     # rank 0 starts its clock after this
+        t0 = time.monotonic()
+        c0 = time.process_time()
+        b.wait_bell(seen, 10.0)
+        q.put(("bell", (time.monotonic() - t0, time.process_time() - c0)))
+        q.close()
+        q.join_thread()                     # flushed before the os._exit below
+    else:
+        b.exchange([0])
+        time.sleep(0.3)
+        b.ring()
+    if die:
+        b.exchange([1])
+        if rank == 1:
+            os._exit(0)                     # leaves without the next exchange
+        t0 = time.monotonic()
+        try:
+            b.exchange([2], timeout_s=30.0)
+            q.put(("dead", None))
+        except LockstepBoard.PeerGone as e:
+            q.put(("dead", (time.monotonic() - t0, str(e))))
+    b.close()
+
+
+def test_lockstep_board_exchange_bell_and_dead_peer():
+    name = f"/dli_test_board_{os.getpid()}"
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_board_worker, args=(r, name, q, True)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(2))
+    for p in ps:
+        p.join(60)
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+    waited, cpu = got["bell"]
+    assert 0.2 < waited < 2.0                # woken by the ring, not the 10 s timeout
+    assert cpu < 0.05                        # slept, did not spin
+    dt, msg = got["dead"]
+    assert dt < 5.0 and "rank 1" in msg
+
+
+def _service_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), DLI_EP_COMM="torch")
+    torch.set_num_threads(1)
+    import torch.distributed as dist
+    from distributed_llm_inferencing_amd.parallel.expert import ExpertParallelEngine
+    from distributed_llm_inferencing_amd.worker.service import ExpertService, PipelineFailed
+    eng = ExpertParallelEngine("mixtral-tiny", "cpu", max_batch=8, max_model_len=64,
+                               num_blocks=64, dtype=torch.float32)
+    assert eng.control_plane == "shm"
+    # the test's own sync: a group of its own (the torch all-to-all of the service thread runs
+    # on the default group, which two threads must not drive at once)
+    sync = dist.new_group(backend="gloo")
+    svc = ExpertService(eng, name="t")
+    sp = SamplingParams(max_length=12, do_sample=False, ignore_eos=True)
+    out = None
+    if rank == 0:
+        out = svc.generate([5, 6, 7], sp, timeout=120).all_ids
+    dist.barrier(group=sync)                # rank 0's request is done on both ranks
+    time.sleep(0.5)                         # both ranks go idle
+    w0 = svc.idle_waits
+    r0 = resource.getrusage(resource.RUSAGE_SELF)
+    t0 = time.monotonic()
+    time.sleep(2.0)
+    r1 = resource.getrusage(resource.RUSAGE_SELF)
+    cpu = (r1.ru_utime + r1.ru_stime) - (r0.ru_utime + r0.ru_stime)
+    frac = cpu / (time.monotonic() - t0)
+    waits = svc.idle_waits - w0
+    # a request on rank 1 wakes the sleeping group at once
+    t1 = time.monotonic()
+    if rank == 1:
+        out = svc.generate([9, 10], sp, timeout=120).all_ids
+    lat = time.monotonic() - t1
+    dist.barrier(group=sync)
+    svc.close()
+    late = svc.submit([1, 2], sp)
+    with pytest.raises(PipelineFailed):
+        late.result(timeout=5)
+    q.put((rank, out, frac, waits, lat, eng.lockstep_syncs))
+    eng.close()
+    dist.destroy_process_group()
+
+
+def test_expert_service_idles_on_the_doorbell_and_stops_cleanly():
+    """Idle EP ranks use < 5 % of a core (they sleep on the board's doorbell, re-checking
+    about once a second); a submit on another rank wakes the group; after ``close`` (every
+    rank) further submits fail at once. Outputs equal one dense engine."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_service_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = {}
+    try:
+        for _ in range(2):
+            r = q.get(timeout=300)
+            res[r[0]] = r[1:]
+    finally:
+        for p in ps:
+            p.join(60)
+            if p.is_alive():
+                p.kill()
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+    from distributed_llm_inferencing_amd.engine.llm_engine import LLMEngine
+    dense = LLMEngine("mixtral-tiny", device="cpu", dtype=torch.float32, max_batch=8,
+                      max_model_len=64, num_blocks=64)
+    sp = SamplingParams(max_length=12, do_sample=False, ignore_eos=True)
+    assert res[0][0] == dense.generate([[5, 6, 7]], sp)[0].all_ids
+    assert res[1][0] == dense.generate([[9, 10]], sp)[0].all_ids
+    for rank, (_, frac, waits, lat, syncs) in res.items():
+        assert frac < 0.05, (rank, frac)
+        assert waits <= 6, (rank, waits)     # ~1 per second of idling, not one per 2 ms
+        assert syncs < 200, (rank, syncs)

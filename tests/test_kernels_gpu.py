@@ -216,73 +216,6 @@ def test_gemv_skinny(gpu, M, N, K, epi):
         G.clear_plans()
 
 
-@pytest.mark.parametrize("M,N,K", [(1, 4096, 4096), (1, 4096, 14336), (2, 1024, 2048),
-                                   (4, 2048, 1536), (3, 1000, 1024)])
-def test_gemv_in_launch_add_rmsnorm(gpu, M, N, K):
-    """Batch-1 decode: split-K combine + residual add + RMSNorm inside the GEMV launch
-    (arrival tickets, gemm.hip gemv_addnorm_kernel) == the fp32 reference; the residual is
-    bit-identical to the two-kernel path (same slice order); the tickets reset themselves
-    (20 back-to-back launches, then graph replays, all equal)."""
-    torch.manual_seed(21)
-    ops._FUSED_GEMV_NORM = True
-    x, w = rnd(M, K, dev=gpu), rnd(N, K, dev=gpu, scale=0.05)
-    r0, nw = rnd(M, N, dev=gpu), rnd(N, dev=gpu)
-    ref_out, ref_res = R.fused_add_rmsnorm(R.linear(x, w), r0, nw, 1e-5)
-    for tile in G.GEMV_FUSED_NORM_TILES:
-        if tile in G.GEMV_M1_ONLY and M > 1:
-            continue
-        for splits in (2, 4, 8):
-            if K % (8 * splits):
-                continue
-            G.set_plan(M, N, K, "splitk", G.GemmPlan("dli", tile, splits))
-            res = r0.clone()
-            out = ops.linear_add_rmsnorm(x, w, res, nw, 1e-5)
-            close(out, ref_out, rtol=2e-2, atol=3e-2)
-            close(res, ref_res, rtol=1e-2, atol=2e-2)
-            # the two-kernel path (gemv slabs + splitk_add_rmsnorm): same residual bits
-            ops._FUSED_GEMV_NORM = False
-            try:
-                res2 = r0.clone()
-                out2 = ops.linear_add_rmsnorm(x, w, res2, nw, 1e-5)
-            finally:
-                ops._FUSED_GEMV_NORM = True
-            assert torch.equal(res, res2), (tile, splits)
-            close(out, out2, rtol=1e-2, atol=1e-2)
-            # add-only (a stage's last layer)
-            res3 = r0.clone()
-            assert ops.linear_add_rmsnorm(x, w, res3, None, 1e-5) is None
-            assert torch.equal(res3, res)
-            # back-to-back launches on one stream: every launch sees zeroed tickets
-            outs = []
-            for _ in range(20):
-                rr = r0.clone()
-                outs.append((ops.linear_add_rmsnorm(x, w, rr, nw, 1e-5), rr))
-            torch.cuda.synchronize()
-            assert all(torch.equal(o, out) and torch.equal(rr, res) for o, rr in outs)
-    # captured and replayed (the decode step's form)
-    G.set_plan(M, N, K, "splitk", G.GemmPlan("dli", 30, 2))
-    res_g = r0.clone()
-    st = torch.cuda.Stream()
-    st.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(st):
-        ops.linear_add_rmsnorm(x, w, res_g.clone(), nw, 1e-5)       # warm the workspace
-    torch.cuda.current_stream().wait_stream(st)
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        out_g = ops.linear_add_rmsnorm(x, w, res_g, nw, 1e-5)
-    want_out, want_res = None, None
-    for _ in range(5):
-        res_g.copy_(r0)
-        g.replay()
-        torch.cuda.synchronize()
-        if want_out is None:
-            want_out, want_res = out_g.clone(), res_g.clone()
-        assert torch.equal(out_g, want_out) and torch.equal(res_g, want_res)
-    close(want_out, ref_out, rtol=2e-2, atol=3e-2)
-    G.clear_plans()
-    ops._FUSED_GEMV_NORM = os.environ.get("DLI_GEMV_FUSED_NORM", "0") == "1"
-
-
 @pytest.mark.parametrize("M", [1, 2, 3, 4])
 @pytest.mark.parametrize("N,K", [(4096, 4096), (4096, 14336), (1000, 768)])
 def test_gemv_residual_epilogue(gpu, M, N, K):
@@ -588,9 +521,9 @@ def test_decode_attention_paged(gpu, hq, hkv, hd, bs, lens):
     ref = R.decode_attention(q, kc, vc, tables, ctx, scale).reshape(len(lens), -1)
     # pipelined and one-tile-per-round kernels; the latter unsplit at hd 128 as a workgroup
     # per (sequence, kv head) (small batches, WPI 4) or a wave per item (WPI 1)
-    for pipe, wpi in ((1, "0"), (0, "4"), (0, "1")):
+    for pipe, wpi in ((1, 0), (0, 4), (0, 1)):
         old = ops.decode_pipelined(pipe)
-        os.environ["DLI_DECODE_WPI"] = wpi
+        old_form = ops.decode_form(wpi)
         try:
             for splits in (1, 2, 4):
                 out = ops.decode_attention(qkv, kc, vc, tables, ctx, max(lens), hq, hkv, hd,
@@ -598,19 +531,20 @@ def test_decode_attention_paged(gpu, hq, hkv, hd, bs, lens):
                 close(out, ref, rtol=2e-2, atol=2e-2)
         finally:
             ops.decode_pipelined(old)
-            del os.environ["DLI_DECODE_WPI"]
+            ops.decode_form(old_form)
 
 
-@pytest.mark.parametrize("wpi", ["1", "4"])
+@pytest.mark.parametrize("wpi", [1, 4])
 @pytest.mark.parametrize("splits", [1, 2, 4])
 @pytest.mark.parametrize("hq,hkv", [(32, 8), (8, 1)])
-def test_fused_rope_attention(gpu, monkeypatch, hq, hkv, splits, wpi):
+def test_fused_rope_attention(gpu, request, hq, hkv, splits, wpi):
     """dli_decode_attention_fused (split-K QKV reduce + RoPE + KV write + attention in one
     kernel) == linear_rope_cache + decode_attention: the same cache bytes, the same output,
     and the output matches the fp32 reference. splits 1: an unsplit QKV plan (the prologue
     reads the bf16 QKV rows). wpi 1 = a wave per (sequence, kv head), 4 = a
     workgroup per item with the context split over its waves and merged in LDS."""
-    monkeypatch.setenv("DLI_DECODE_WPI", wpi)
+    old_form = ops.decode_form(wpi)
+    request.addfinalizer(lambda: ops.decode_form(old_form))
     hd, bs = 128, 16
     lens = [1, 5, 33, 100, 200, 17, 130]
     B = len(lens)
@@ -630,7 +564,6 @@ def test_fused_rope_attention(gpu, monkeypatch, hq, hkv, splits, wpi):
         kc1, vc1 = kc.clone(), vc.clone()
         qkv = ops.linear_rope_cache(x, w, pos, slots, cs, kc1, vc1, hq, hkv, hd)
         ref2 = ops.decode_attention(qkv, kc1, vc1, tables, ctx, max(lens), hq, hkv, hd, scale)
-        monkeypatch.setenv("DLI_FUSED_ROPE_ATTN", "1")
         kc2, vc2 = kc.clone(), vc.clone()
         out = ops.linear_rope_attention(x, w, pos, slots, cs, kc2, vc2, tables, ctx,
                                         max(lens), hq, hkv, hd, scale)
