@@ -362,7 +362,7 @@ __global__ void __launch_bounds__(256) decode_attn_wg_kernel(
 // trip per 32-token tile): wave 0 writes the new k/v row, every wave builds the Q fragments,
 // wave w takes the w-th quarter of the context's tiles, and the four partial (m, l, O) merge
 // through LDS (the V-tile rows are reused for the O partials).
-template <int SPL, int WPI>
+template <int SPL, int WPI, bool S16 = false>
 __global__ void __launch_bounds__(256, 4) decode_attn_fused_kernel(
     u16* __restrict__ out, const void* __restrict__ src, int N,
     const int* __restrict__ positions, const int* __restrict__ slot_mapping,
@@ -372,8 +372,10 @@ __global__ void __launch_bounds__(256, 4) decode_attn_fused_kernel(
   constexpr int HD = 128, HALF = 64, KK = HD / 32, VROW = HD + 16, DB = HD / 16;
   // SPL > 0: src = the QKV GEMM's fp32 split-K slabs [SPL, B, N]; SPL == 0: the bf16 QKV rows
   // [B, N] of an unsplit GEMM (the same prologue minus the slab sum)
+  // S16: the slabs are fp16 x 1/16 (EPI_SLAB16), read as 16-bit words
   const float* ws = static_cast<const float*>(src);
   const u16* qkv = static_cast<const u16*>(src);
+  const u16* ws16 = static_cast<const u16*>(src);
   static_assert(WPI == 1 || WPI == DEC_WAVES, "one item per wave or per workgroup");
   __shared__ __attribute__((aligned(16))) u16 vtile_all[DEC_WAVES][DEC_TILE * VROW];
   __shared__ float ml_all[WPI > 1 ? WPI : 1][16][2];
@@ -404,8 +406,25 @@ __global__ void __launch_bounds__(256, 4) decode_attn_fused_kernel(
         load8(qr + d1, x1);
         load8(qr + HALF + d1, x2);
       }
+      if constexpr (S16) {
+        const u16* qh = ws16 + rowoff + (long)(kvh * G + col) * HD;
+        uint4 ua[SPL], uc[SPL];
 #pragma unroll
-      for (int s = 0; s < SPL; ++s) {
+        for (int s = 0; s < SPL; ++s) {
+          ua[s] = *reinterpret_cast<const uint4*>(qh + s * splitstride + d1);
+          uc[s] = *reinterpret_cast<const uint4*>(qh + s * splitstride + HALF + d1);
+        }
+#pragma unroll
+        for (int s = 0; s < SPL; ++s) {
+          float fa[8], fc[8];
+          unpack8h(ua[s], fa);
+          unpack8h(uc[s], fc);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) { x1[j] += fa[j]; x2[j] += fc[j]; }
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < (S16 ? 0 : SPL); ++s) {
         const float4* a = reinterpret_cast<const float4*>(qp + s * splitstride + d1);
         const float4* c = reinterpret_cast<const float4*>(qp + s * splitstride + HALF + d1);
         const float4 a0 = a[0], a1 = a[1], c0 = c[0], c1 = c[1];
@@ -440,7 +459,17 @@ __global__ void __launch_bounds__(256, 4) decode_attn_fused_kernel(
     const float* kp = ws + rowoff + (long)(hq + kvh) * HD;
     const float* vp = ws + rowoff + (long)(hq + hkv + kvh) * HD;
     float k1 = 0.f, k2 = 0.f, v1 = 0.f, v2 = 0.f;
-    if constexpr (SPL > 0) {
+    if constexpr (S16) {
+      const u16* kh = ws16 + rowoff + (long)(hq + kvh) * HD;
+      const u16* vh = ws16 + rowoff + (long)(hq + hkv + kvh) * HD;
+#pragma unroll
+      for (int s = 0; s < SPL; ++s) {
+        k1 += h2f(kh[s * splitstride + lane]) * SLAB16_UNSCALE;
+        k2 += h2f(kh[s * splitstride + HALF + lane]) * SLAB16_UNSCALE;
+        v1 += h2f(vh[s * splitstride + lane]) * SLAB16_UNSCALE;
+        v2 += h2f(vh[s * splitstride + HALF + lane]) * SLAB16_UNSCALE;
+      }
+    } else if constexpr (SPL > 0) {
 #pragma unroll
       for (int s = 0; s < SPL; ++s) {
         k1 += kp[s * splitstride + lane];
@@ -833,32 +862,35 @@ extern "C" int dli_decode_attention(void* out, const void* q, int q_stride, cons
 // Fused split-K QKV reduce + RoPE + KV-cache write + decode attention (one KV split, head
 // dim 128, RoPE models): ws = the QKV GEMM's fp32 slabs [splits, B, (hq + 2 hkv) * 128], or
 // with splits == 0 the bf16 QKV rows [B, (hq + 2 hkv) * 128] of an unsplit GEMM.
+// fmt: 0 = fp32 slabs (or the bf16 rows when splits == 0), 1 = fp16 x 1/16 slabs (EPI_SLAB16)
 extern "C" int dli_decode_attention_fused(void* out, const void* ws, int splits,
                                           const int* positions, const int* slot_mapping,
                                           const float* cos_sin, void* k_cache, void* v_cache,
                                           const int* block_tables, int max_blocks,
                                           const int* context_lens, int B, int hq, int hkv,
-                                          int hd, int block_size, float scale, hipStream_t st) {
+                                          int hd, int block_size, float scale, int fmt,
+                                          hipStream_t st) {
   if (B <= 0) return 0;
   if (hd != 128 || hq % hkv || hq / hkv > 16 || block_size % 16 ||
-      (splits != 0 && splits != 2 && splits != 4))
+      (splits != 0 && splits != 2 && splits != 4) || fmt < 0 || fmt > 1 ||
+      (fmt == 1 && splits == 0))
     return (int)hipErrorInvalidValue;
   const int N = (hq + 2 * hkv) * hd;
   const float scale_log2 = scale * 1.4426950408889634f;
   const long items = (long)B * hkv;
   const bool per_wg = wg_form(items);
   dim3 grid((int)(per_wg ? items : (items + DEC_WAVES - 1) / DEC_WAVES));
-#define DLI_DAF(S, W) decode_attn_fused_kernel<S, W><<<grid, 64 * DEC_WAVES, 0, st>>>(          \
+#define DLI_DAF(S, W, F) decode_attn_fused_kernel<S, W, F><<<grid, 64 * DEC_WAVES, 0, st>>>(   \
       (u16*)out, ws, N, positions, slot_mapping, cos_sin, (u16*)k_cache, (u16*)v_cache,      \
       block_tables, max_blocks, context_lens, B, hq, hkv, block_size, scale_log2)
   if (per_wg) {
-    if (splits == 0) DLI_DAF(0, DEC_WAVES);
-    else if (splits == 2) DLI_DAF(2, DEC_WAVES);
-    else DLI_DAF(4, DEC_WAVES);
+    if (splits == 0) DLI_DAF(0, DEC_WAVES, false);
+    else if (splits == 2) { if (fmt) DLI_DAF(2, DEC_WAVES, true); else DLI_DAF(2, DEC_WAVES, false); }
+    else { if (fmt) DLI_DAF(4, DEC_WAVES, true); else DLI_DAF(4, DEC_WAVES, false); }
   } else {
-    if (splits == 0) DLI_DAF(0, 1);
-    else if (splits == 2) DLI_DAF(2, 1);
-    else DLI_DAF(4, 1);
+    if (splits == 0) DLI_DAF(0, 1, false);
+    else if (splits == 2) { if (fmt) DLI_DAF(2, 1, true); else DLI_DAF(2, 1, false); }
+    else { if (fmt) DLI_DAF(4, 1, true); else DLI_DAF(4, 1, false); }
   }
 #undef DLI_DAF
   DLI_RETURN_LAUNCH();

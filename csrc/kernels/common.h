@@ -84,3 +84,25 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 }
 
 #define DLI_RETURN_LAUNCH() return (int)hipGetLastError()
+
+// fp16 split-K partials (the EPI_SLAB16 GEMM epilogue and its consumers): value x 1/16 in
+// fp16 (RNE), read back x 16 — half the bytes of fp32 slabs, |partial| up to ~1e6 in range
+constexpr float SLAB16_SCALE = 0.0625f, SLAB16_UNSCALE = 16.f;
+__device__ __forceinline__ uint32_t pack2h(float a, float b) {
+  const _Float16 ha = (_Float16)a, hb = (_Float16)b;
+  return (uint32_t)__builtin_bit_cast(uint16_t, ha) |
+         ((uint32_t)__builtin_bit_cast(uint16_t, hb) << 16);
+}
+__device__ __forceinline__ float h2f(uint32_t bits16) {
+  return (float)__builtin_bit_cast(_Float16, (uint16_t)bits16);
+}
+// 8 fp16 slab values (one 16-B load) -> fp32, unscaled
+__device__ __forceinline__ void unpack8h(const uint4 u, float* f) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = h2f(w[i] & 0xffffu) * SLAB16_UNSCALE;
+    f[2 * i + 1] = h2f(w[i] >> 16) * SLAB16_UNSCALE;
+  }
+}
+

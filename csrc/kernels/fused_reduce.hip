@@ -5,16 +5,17 @@
 //                           (w == null: residual += sum_s P_s only, for a stage's last layer)
 //  dli_splitk_rope_cache  : qkv = bf16(sum_s P_s); RoPE on q,k in place; k,v -> paged cache
 //
-// P_s are the fp32 [M, N] slabs written by gemm_bf16_kernel when called with C == nullptr.
-// Numerics equal the unfused path: the GEMM result is rounded to bf16 before the residual add
-// / rotation, exactly as the bf16 GEMM output would be.
+// P_s are the [M, N] slabs written by a GEMM called with C == nullptr: fp32, or (fmt 1, the
+// EPI_SLAB16 epilogue of the MFMA families) fp16 scaled by 1/16. The sum is fp32 in slab
+// order 0..S-1 and rounded to bf16 before the residual add / rotation, exactly as the bf16
+// GEMM output would be.
 #include "common.h"
 #include <stdlib.h>
 
 // SPL > 0: the split count is a compile-time constant, so every partial of a thread is
 // loaded before the first add (SPL x VPT x 2 16-B loads in flight per lane instead of 2 x VPT);
 // SPL == 0 reads `splits` partials in a runtime loop.
-template <int VPT, int SPL>
+template <int VPT, int SPL, bool S16 = false>
 __global__ void __launch_bounds__(512) splitk_add_rmsnorm_kernel(
     u16* __restrict__ out, u16* __restrict__ residual, const float* __restrict__ ws, int splits,
     int M, int N, const u16* __restrict__ w, float eps) {
@@ -28,7 +29,20 @@ __global__ void __launch_bounds__(512) splitk_add_rmsnorm_kernel(
     const int vi = threadIdx.x + i * blockDim.x;
     if (vi < nvec) {
       float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      if constexpr (SPL > 0) {
+      if constexpr (S16) {                        // fp16 slabs: one 16-B load per slab
+        const u16* ws16 = reinterpret_cast<const u16*>(ws);
+        uint4 pu[SPL];
+#pragma unroll
+        for (int s = 0; s < SPL; ++s)
+          pu[s] = *reinterpret_cast<const uint4*>(ws16 + ((long)s * M + row) * N + vi * 8);
+#pragma unroll
+        for (int s = 0; s < SPL; ++s) {
+          float f[8];
+          unpack8h(pu[s], f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[j] += f[j];
+        }
+      } else if constexpr (SPL > 0) {
         float4 pa[SPL], pb[SPL];
 #pragma unroll
         for (int s = 0; s < SPL; ++s) {
@@ -76,7 +90,16 @@ __global__ void __launch_bounds__(512) splitk_add_rmsnorm_kernel(
 
 template <int VPT>
 static int launch_add_rmsnorm(u16* o, u16* r, const float* ws, int splits, int M, int N,
-                              const u16* wp, float eps, int threads, hipStream_t st) {
+                              const u16* wp, float eps, int threads, int fmt, hipStream_t st) {
+  if (fmt == 1) {                                  // fp16 slabs: the planner's 2 / 4 / 8 splits
+    switch (splits) {
+      case 2: splitk_add_rmsnorm_kernel<VPT, 2, true><<<M, threads, 0, st>>>(o, r, ws, 2, M, N, wp, eps); break;
+      case 4: splitk_add_rmsnorm_kernel<VPT, 4, true><<<M, threads, 0, st>>>(o, r, ws, 4, M, N, wp, eps); break;
+      case 8: splitk_add_rmsnorm_kernel<VPT, 8, true><<<M, threads, 0, st>>>(o, r, ws, 8, M, N, wp, eps); break;
+      default: return (int)hipErrorInvalidValue;
+    }
+    DLI_RETURN_LAUNCH();
+  }
   // the register-resident partials of SPL x VPT cap the unrolled variants at 8 slabs, so
   // they exist for rows up to 4096 wide (VPT <= 2) and the split counts the planner offers
   // (2/4/8); wider rows and other counts take the runtime-split loop (SPL = 0)
@@ -89,10 +112,12 @@ static int launch_add_rmsnorm(u16* o, u16* r, const float* ws, int splits, int M
   DLI_RETURN_LAUNCH();
 }
 
+// fmt: 0 = fp32 slabs, 1 = fp16 x 1/16 slabs (EPI_SLAB16)
 extern "C" int dli_splitk_add_rmsnorm(void* out, void* residual, const float* ws, int splits,
-                                      int M, int N, const void* w, float eps, hipStream_t st) {
+                                      int M, int N, const void* w, float eps, int fmt,
+                                      hipStream_t st) {
   if (M <= 0) return 0;
-  if (N % 8) return (int)hipErrorInvalidValue;
+  if (N % 8 || fmt < 0 || fmt > 1) return (int)hipErrorInvalidValue;
   const int nvec = N / 8;
   // threads per row (one workgroup per row): 512, i.e. one 8-column vector per lane at
   // N = 4096 (same-box A/B with the GEMMs that feed it, M = 512: O + reduce 33.85-33.92 ->
@@ -103,11 +128,11 @@ extern "C" int dli_splitk_add_rmsnorm(void* out, void* residual, const float* ws
   const int vpt = (nvec + threads - 1) / threads;
   auto o = (u16*)out; auto r = (u16*)residual; auto wp = (const u16*)w;
   switch (vpt) {
-    case 1: return launch_add_rmsnorm<1>(o, r, ws, splits, M, N, wp, eps, threads, st);
-    case 2: return launch_add_rmsnorm<2>(o, r, ws, splits, M, N, wp, eps, threads, st);
-    case 3: case 4: return launch_add_rmsnorm<4>(o, r, ws, splits, M, N, wp, eps, threads, st);
+    case 1: return launch_add_rmsnorm<1>(o, r, ws, splits, M, N, wp, eps, threads, fmt, st);
+    case 2: return launch_add_rmsnorm<2>(o, r, ws, splits, M, N, wp, eps, threads, fmt, st);
+    case 3: case 4: return launch_add_rmsnorm<4>(o, r, ws, splits, M, N, wp, eps, threads, fmt, st);
     case 5: case 6: case 7: case 8:
-      return launch_add_rmsnorm<8>(o, r, ws, splits, M, N, wp, eps, threads, st);
+      return launch_add_rmsnorm<8>(o, r, ws, splits, M, N, wp, eps, threads, fmt, st);
     default: return (int)hipErrorInvalidValue;
   }
 }
@@ -115,7 +140,7 @@ extern "C" int dli_splitk_add_rmsnorm(void* out, void* residual, const float* ws
 // one lane: 8 dims of the first half of a head + the matching 8 of the second half. SPL > 0:
 // compile-time split count, every partial's loads issued before the first add (and the
 // position / cos-sin loads ahead of them); SPL == 0: runtime loop.
-template <int SPL>
+template <int SPL, bool S16 = false>
 __global__ void __launch_bounds__(256) splitk_rope_cache_kernel(
     u16* __restrict__ qkv, const float* __restrict__ ws, int splits, int T, int N,
     const int* __restrict__ positions, const int* __restrict__ slot_mapping,
@@ -140,7 +165,24 @@ __global__ void __launch_bounds__(256) splitk_rope_cache_kernel(
     x[0] += a.x; x[1] += a.y; x[2] += a.z; x[3] += a.w;
     x[4] += b.x; x[5] += b.y; x[6] += b.z; x[7] += b.w;
   };
-  if constexpr (SPL > 0) {
+  if constexpr (S16) {                             // fp16 slabs: one 16-B load per half-row
+    const u16* ws16 = reinterpret_cast<const u16*>(ws);
+    uint4 pu[SPL], pv[SPL];
+#pragma unroll
+    for (int s = 0; s < SPL; ++s) {
+      const u16* base = ws16 + ((long)s * T + t) * N;
+      pu[s] = *reinterpret_cast<const uint4*>(base + col1);
+      pv[s] = *reinterpret_cast<const uint4*>(base + col2);
+    }
+#pragma unroll
+    for (int s = 0; s < SPL; ++s) {
+      float f1[8], f2[8];
+      unpack8h(pu[s], f1);
+      unpack8h(pv[s], f2);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { x1[j] += f1[j]; x2[j] += f2[j]; }
+    }
+  } else if constexpr (SPL > 0) {
     float4 pa[SPL], pb[SPL], pe[SPL], pf[SPL];
 #pragma unroll
     for (int s = 0; s < SPL; ++s) {
@@ -189,19 +231,29 @@ __global__ void __launch_bounds__(256) splitk_rope_cache_kernel(
 extern "C" int dli_splitk_rope_cache(void* qkv, const float* ws, int splits, int T, int N,
                                      const int* positions, const int* slot_mapping,
                                      const float* cos_sin, void* k_cache, void* v_cache, int hq,
-                                     int hkv, int hd, int block_size, int use_rope,
+                                     int hkv, int hd, int block_size, int use_rope, int fmt,
                                      hipStream_t st) {
   if (T <= 0) return 0;
-  if (hd % 16 || N != (hq + 2 * hkv) * hd) return (int)hipErrorInvalidValue;
+  if (hd % 16 || N != (hq + 2 * hkv) * hd || fmt < 0 || fmt > 1 ||
+      (fmt == 1 && splits != 2 && splits != 4 && splits != 8))
+    return (int)hipErrorInvalidValue;
   const long total = (long)T * (hq + 2 * hkv) * (hd / 16);
   const int blocks = (int)((total + 255) / 256);
-#define DLI_SRC(S) splitk_rope_cache_kernel<S><<<blocks, 256, 0, st>>>(                   \
+#define DLI_SRC(S, F) splitk_rope_cache_kernel<S, F><<<blocks, 256, 0, st>>>(             \
       (u16*)qkv, ws, splits, T, N, positions, slot_mapping, cos_sin, (u16*)k_cache,        \
       (u16*)v_cache, hq, hkv, hd, block_size, use_rope)
-  switch (splits) {
-    case 2: DLI_SRC(2); break;
-    case 4: DLI_SRC(4); break;
-    default: DLI_SRC(0);
+  if (fmt == 1) {
+    switch (splits) {
+      case 2: DLI_SRC(2, true); break;
+      case 4: DLI_SRC(4, true); break;
+      default: DLI_SRC(8, true);
+    }
+  } else {
+    switch (splits) {
+      case 2: DLI_SRC(2, false); break;
+      case 4: DLI_SRC(4, false); break;
+      default: DLI_SRC(0, false);
+    }
   }
 #undef DLI_SRC
   DLI_RETURN_LAUNCH();

@@ -286,7 +286,9 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int col = wc0 + 16 * j + 4 * fq;
-        if (col < N) slab_quad(srow + col, acc[i][j], sm, vec, N - col, ws);
+        if (col >= N) continue;
+        if (EPI == EPI_SLAB16) slab_quad16(srow + col, acc[i][j], vec, N - col, ws);
+        else slab_quad(srow + col, acc[i][j], sm, vec, N - col, ws);
       }
     }
     return;
@@ -521,7 +523,9 @@ __global__ void __launch_bounds__(512) gemm8p224_kernel(
 #pragma unroll
       for (int j = 0; j < 7; ++j) {
         const int col = wc0 + 16 * j + 4 * fq;
-        if (col < N) slab_quad(srow + col, acc[i][j], sm, vec, N - col, ws);
+        if (col >= N) continue;
+        if (EPI == EPI_SLAB16) slab_quad16(srow + col, acc[i][j], vec, N - col, ws);
+        else slab_quad(srow + col, acc[i][j], sm, vec, N - col, ws);
       }
     }
     return;
@@ -767,7 +771,9 @@ __global__ void __launch_bounds__(512) gemm8p128_kernel(
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int col = wc0 + 16 * j + 4 * fq;
-        if (col < N) slab_quad(srow + col, acc[i][j], sm, vec, N - col, ws);
+        if (col >= N) continue;
+        if (EPI == EPI_SLAB16) slab_quad16(srow + col, acc[i][j], vec, N - col, ws);
+        else slab_quad(srow + col, acc[i][j], sm, vec, N - col, ws);
       }
     }
     return;
@@ -913,5 +919,5 @@ static int dispatch_8p(int tile_cfg, DLI_GEMM_ARGS) {
   }
 }
 
-int gemm_8p_dispatch(int epi, int tile_cfg, DLI_GEMM_ARGS) { DLI_EPI_SWITCH(dispatch_8p) }
+int gemm_8p_dispatch(int epi, int tile_cfg, DLI_GEMM_ARGS) { DLI_EPI_SWITCH_S16(dispatch_8p) }
 int gemm_8p_set_slab_store(int mode) { return set_slab_store_tu(mode); }

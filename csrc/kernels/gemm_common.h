@@ -11,7 +11,11 @@
 
 #define BK 64
 
-enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_SILU = 2, EPI_BIAS_GELU = 3, EPI_BIAS = 4 };
+enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_SILU = 2, EPI_BIAS_GELU = 3, EPI_BIAS = 4,
+       // slab-only split-K call (C == nullptr, splits > 1) whose partials are stored as fp16
+       // scaled by 1/16 instead of fp32 (half the bytes the GEMM writes and its consumer
+       // reads; the scale keeps |partial| up to ~1e6 in range). Tiles and 8-phase families.
+       EPI_SLAB16 = 5 };
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef const __attribute__((address_space(1))) void gbl_void;
@@ -91,6 +95,23 @@ __device__ __forceinline__ void slab_quad_fp32(float* p, f32x4 v, int mode, bool
 #pragma unroll
     for (int r = 0; r < 4; ++r)
       if (r < left) slab_store(p + r, v[r], mode);
+  }
+}
+
+// fp16 (x 1/16) partial quad of the EPI_SLAB16 slab image: p = &fp32-indexed slab[row][col]
+// (the element index into a [splits][M][N] image based at ws), one 8-B store
+__device__ __forceinline__ void slab_quad16(float* p, f32x4 v, bool vec, int left,
+                                            const float* ws) {
+  u16* q = (u16*)ws + (p - ws);
+  if (vec) {
+    uint2 pk;
+    pk.x = pack2h(v[0] * SLAB16_SCALE, v[1] * SLAB16_SCALE);
+    pk.y = pack2h(v[2] * SLAB16_SCALE, v[3] * SLAB16_SCALE);
+    *reinterpret_cast<uint2*>(q) = pk;
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (r < left) q[r] = (u16)(pack2h(v[r] * SLAB16_SCALE, 0.f) & 0xffffu);
   }
 }
 
@@ -253,7 +274,15 @@ int gemm_tiles_set_slab_store(int mode);
 int gemm_8p_set_slab_store(int mode);
 int gemm_4w_set_slab_store(int mode);
 
-// EPI -> template argument, for a family's dispatch<EPI>(tile_cfg, ...)
+// EPI -> template argument, for a family's dispatch<EPI>(tile_cfg, ...); the families with
+// an fp16 slab store (tiles, 8-phase) take DLI_EPI_SWITCH_S16
+#define DLI_EPI_SWITCH_S16(FN)                                                     \
+  if (epi == EPI_SLAB16) {                                                         \
+    if (C != nullptr || splits < 2) return (int)hipErrorInvalidValue;              \
+    return FN<EPI_SLAB16>(tile_cfg, DLI_GEMM_PASS);                                \
+  }                                                                                \
+  DLI_EPI_SWITCH(FN)
+
 #define DLI_EPI_SWITCH(FN)                                                         \
   switch (epi) {                                                                   \
     case EPI_BF16: return FN<EPI_BF16>(tile_cfg, DLI_GEMM_PASS);                   \

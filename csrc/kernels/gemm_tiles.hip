@@ -166,7 +166,9 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
         const int col = n0 + wn * TN + 16 * j + 4 * fq;
-        if (col < N) slab_quad(srow + col, acc[i][j], sm, vec, N - col, ws);
+        if (col >= N) continue;
+        if (EPI == EPI_SLAB16) slab_quad16(srow + col, acc[i][j], vec, N - col, ws);
+        else slab_quad(srow + col, acc[i][j], sm, vec, N - col, ws);
       }
     }
     return;
@@ -255,5 +257,5 @@ static int dispatch_tiles(int tile_cfg, DLI_GEMM_ARGS) {
   }
 }
 
-int gemm_tiles_dispatch(int epi, int tile_cfg, DLI_GEMM_ARGS) { DLI_EPI_SWITCH(dispatch_tiles) }
+int gemm_tiles_dispatch(int epi, int tile_cfg, DLI_GEMM_ARGS) { DLI_EPI_SWITCH_S16(dispatch_tiles) }
 int gemm_tiles_set_slab_store(int mode) { return set_slab_store_tu(mode); }

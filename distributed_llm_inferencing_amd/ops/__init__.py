@@ -226,6 +226,18 @@ def linear(x, w, bias=None, epi: str = "none", out=None):
     return _gemm_native(x, w, epi, bias=bias, out=out)
 
 
+def _slab_gemm(x, w, p: G.GemmPlan, ws) -> int:
+    """x @ w.T as ``p.splits`` split-K partial slabs in ``ws`` (no output tensor: a fused
+    consumer reduces them). Returns the slab format the consumer must read: 1 = fp16 x 1/16
+    (the MFMA families' EPI "slab16" store, half the bytes), 0 = fp32."""
+    M, K = x.shape
+    Nn = w.shape[0]
+    fmt = 1 if (G.SLAB16 and p.tile in G.SLAB16_TILES and p.splits in (2, 4, 8)) else 0
+    _native_call("dli_gemm", _p(x), x.stride(0), _p(w), w.stride(-2), None, Nn, M, Nn, K,
+                 G.EPI["slab16"] if fmt else 0, p.tile, p.splits, None, _p(ws), None, 1, _st())
+    return fmt
+
+
 def _splitk_plan(x, w):
     """A split-K plan for a GEMM whose partial sums feed a fused reduce, or None."""
     if not _use_native(x) or x.stride(-1) != 1 or w.stride(-1) != 1:
@@ -254,10 +266,9 @@ def linear_add_rmsnorm(x, w, residual, norm_w, eps, plan: Optional[G.GemmPlan] =
     Nn = w.shape[0]
     ws = G.workspace(x.device, p.splits * M * Nn * 4)
     out = torch.empty_like(residual) if norm_w is not None else None
-    _native_call("dli_gemm", _p(x), x.stride(0), _p(w), w.stride(-2), None, Nn, M, Nn, K,
-                 0, p.tile, p.splits, None, _p(ws), None, 1, _st())
+    fmt = _slab_gemm(x, w, p, ws)
     _native_call("dli_splitk_add_rmsnorm", _p(out), _p(residual), _p(ws), p.splits, M, Nn,
-                 _p(norm_w), eps, _st())
+                 _p(norm_w), eps, fmt, _st())
     return out
 
 
@@ -279,13 +290,12 @@ def linear_rope_cache(x, w, positions, slot_mapping, cos_sin, k_cache, v_cache, 
     M, K = x.shape
     Nn = w.shape[0]
     ws = G.workspace(x.device, p.splits * M * Nn * 4)
-    _native_call("dli_gemm", _p(x), x.stride(0), _p(w), w.stride(-2), None, Nn, M, Nn, K,
-                 0, p.tile, p.splits, None, _p(ws), None, 1, _st())
+    fmt = _slab_gemm(x, w, p, ws)
     qkv = torch.empty(M, Nn, dtype=x.dtype, device=x.device)
     bs = k_cache.shape[2] if k_cache is not None else 16
     _native_call("dli_splitk_rope_cache", _p(qkv), _p(ws), p.splits, M, Nn, _p(positions),
                  _p(slot_mapping), _p(cos_sin), _p(k_cache), _p(v_cache), hq, hkv, hd, bs,
-                 int(use_rope), _st())
+                 int(use_rope), fmt, _st())
     return qkv
 
 
@@ -311,6 +321,7 @@ def linear_rope_attention(x, w, positions, slot_mapping, cos_sin, k_cache, v_cac
     if mode == 1 or (mode == 2 and -(-max_context // 32) * 32 >= 768):
         return None                       # dli_decode_attention picks the pipelined kernel
     Nn = w.shape[0]
+    fmt = 0
     if p is None:                         # unsplit plan: the prologue reads the bf16 rows
         src, splits = linear(x, w), 0
     else:
@@ -319,13 +330,12 @@ def linear_rope_attention(x, w, positions, slot_mapping, cos_sin, k_cache, v_cac
                 and _gemv_prologue(x, w, "splitk", p, None, Nn, ws=src)):
             if isinstance(x, NormedRows):
                 x = x.materialize()
-            _native_call("dli_gemm", _p(x), x.stride(0), _p(w), w.stride(-2), None, Nn, B, Nn,
-                         K, 0, p.tile, p.splits, None, _p(src), None, 1, _st())
+            fmt = _slab_gemm(x, w, p, src)
     out = torch.empty(B, hq * hd, dtype=x.dtype, device=x.device)
     _native_call("dli_decode_attention_fused", _p(out), _p(src), splits, _p(positions),
                  _p(slot_mapping), _p(cos_sin), _p(k_cache), _p(v_cache), _p(block_tables),
                  block_tables.stride(0), _p(context_lens), B, hq, hkv, hd, k_cache.shape[2],
-                 scale, _st())
+                 scale, fmt, _st())
     return out
 
 

@@ -57,10 +57,10 @@ _SIGS = {
     "dli_topk_rows_bf16": [P, P, P, L, I, I, I, I, P],
     "dli_topk_rows": [P, P, P, L, I, I, I, I, P],
     "dli_gemm": [P, I, P, I, P, I, I, I, I, I, I, I, P, P, P, I, P],
-    "dli_splitk_add_rmsnorm": [P, P, P, I, I, I, P, F, P],
+    "dli_splitk_add_rmsnorm": [P, P, P, I, I, I, P, F, I, P],
     "dli_gemv_fused": [P, I, P, F, P, I, P, I, I, I, I, I, I, I, P, P],
-    "dli_splitk_rope_cache": [P, P, I, I, I, P, P, P, P, P, I, I, I, I, I, P],
-    "dli_decode_attention_fused": [P, P, I, P, P, P, P, P, P, I, P, I, I, I, I, I, F, P],
+    "dli_splitk_rope_cache": [P, P, I, I, I, P, P, P, P, P, I, I, I, I, I, I, P],
+    "dli_decode_attention_fused": [P, P, I, P, P, P, P, P, P, I, P, I, I, I, I, I, F, I, P],
     "dli_moe_route": [P, P, P, I, I, I, P],
     "dli_moe_align": [P, P, P, P, I, I, I, I, P],
     "dli_moe_gather": [P, P, P, I, I, P, P],

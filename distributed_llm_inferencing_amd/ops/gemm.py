@@ -102,7 +102,13 @@ def tile_ok(tile: int, epi: str) -> bool:
 
 # "splitk": a plain GEMM whose fp32 partial slabs feed a fused reduce (ops.linear_add_rmsnorm,
 # ops.linear_rope_cache); planned/tuned separately (a non-split winner runs unfused).
-EPI = {"none": 0, "f32": 1, "silu_mul": 2, "bias_gelu": 3, "bias": 4, "splitk": 0}
+EPI = {"none": 0, "f32": 1, "silu_mul": 2, "bias_gelu": 3, "bias": 4, "splitk": 0,
+       "slab16": 5}
+# tiles whose slab-only split-K call can store fp16 partials (EPI "slab16": the generic tile
+# family and the 8-phase kernels); the fused consumers then read half the bytes. The
+# weight-streaming GEMVs and the 4-wave family keep fp32 slabs.
+SLAB16_TILES = frozenset(list(range(0, 22)) + [22, 23, 24, 25, 26, 28])
+SLAB16 = os.environ.get("DLI_SLAB_FP32", "0") != "1"      # A/B: fp32 partials everywhere
 NUM_CUS = 256
 
 

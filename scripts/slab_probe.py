@@ -47,7 +47,7 @@ for sp in (8, 4, 2):
     slab = G.workspace(dev, 8 * M * 4096 * 4)
     def red():
         N.call("dli_splitk_add_rmsnorm", out.data_ptr(), res.data_ptr(), slab.data_ptr(), sp, M,
-               4096, nw.data_ptr(), 1e-5, N.stream_ptr())
+               4096, nw.data_ptr(), 1e-5, 0, N.stream_ptr())
     us = ops.benchmark(red, iters=20, warmup=3, graph=True) * 1e3
     print(json.dumps({"reduce": "add_rmsnorm", "splits_fp32": sp, "us": round(us, 2)}),
           flush=True)

@@ -161,24 +161,48 @@ def test_real_shape_engine_decode(gpu, name, monkeypatch):
     assert outs[0] == outs[1]
 
 
+def _fp32_top2(eng, prefix):
+    """Top-2 logits of the next token after ``prefix`` under the fp32 CPU reference of
+    ``eng``'s weights (the same bf16 parameters, computed exactly in fp32)."""
+    from distributed_llm_inferencing_amd.models.model import TransformerLM
+    params = {k: v.float().cpu() for k, v in eng.model.params.items()}
+    lm = TransformerLM(eng.cfg, params, device="cpu")
+    ref = LLMEngine(eng.cfg, device="cpu", dtype=torch.float32, max_batch=1, max_model_len=128,
+                    num_blocks=16, lm=lm)
+    seen = []
+    real = TransformerLM.sample
+
+    def spy(self, lg, b, generator=None):
+        seen.append(lg.float())
+        return real(self, lg, b, generator=generator)
+    TransformerLM.sample = spy
+    try:
+        ref.generate([prefix], SamplingParams(max_length=len(prefix) + 1, do_sample=False,
+                                              ignore_eos=True))
+    finally:
+        TransformerLM.sample = real
+    return seen[0][0].topk(2).values
+
+
 def test_mixed_steps_token_identical_on_gpu(gpu, monkeypatch):
     """Prompts arriving while others decode: the mixed prefill+decode steps (decode rows on
-    the decode kernel, prompt rows on the paged prefill kernel, one GEMM pass) produce the
-    tokens of the engine without mixed steps; graphs and lookahead on. The reduce-free
-    batch-1 chain (models/model.py ``defer``, M <= 4 decode steps only) sums in another order
-    than the split-K path a mixed step's decode rows take, so it is off here: the
-    invariant is the mixed step's own (its numerics: test_batch1_deferred_norm_decode).
-    Token identity across the two paths is itself a rounding question (a mixed step's decode
-    rows take the MFMA tiles, a decode-only step the weight-streaming GEMVs): it holds with
-    the decode plans the tier's earlier engine tests leave autotuned; run alone, on the
-    heuristic plans, one sampled token of 200 flips (profiles/r5/README.md §14)."""
+    the decode kernel, prompt rows on the paged prefill kernel, one GEMM pass) give the
+    tokens of the engine without mixed steps — greedy, graphs, lookahead and the reduce-free
+    batch-1 chain (``DEFER_NORM``) all on, heuristic plans (no autotune), so the result does
+    not depend on what an earlier test left in the plan cache. The two engines run the
+    same math in different fp32 summation orders (a mixed step's decode rows take the MFMA
+    tiles; a decode-only step of <= 4 rows the weight-streaming GEMVs), so a request may
+    differ only where the exact model is undecided: at its first differing token the fp32
+    reference's top-two logits are a near tie; and at most one request of the eight differs.
+    (token identity held only on plans earlier tests had autotuned.)"""
     from distributed_llm_inferencing_amd.ops import gemm as G
     monkeypatch.setenv("DLI_GEMM_AUTOTUNE", "0")
-    monkeypatch.setattr(G, "DEFER_NORM", False)
+    assert G.DEFER_NORM
     waves = [[IDS[:5], IDS[:9], IDS[3:14]], [IDS[:2], IDS[1:4]], [IDS[2:11]]]
-    sp = SamplingParams(max_length=40, seed=7, ignore_eos=True)
-    res = []
+    sp = SamplingParams(max_length=40, do_sample=False, ignore_eos=True)
+    res, engs = [], []
     for mixed in (False, True):
+        G.clear_plans()
         eng = LLMEngine("llama-tiny", device="cuda", max_batch=8, max_model_len=128,
                         num_blocks=64, seed=2, mixed_steps=mixed)
         outs, rids = {}, []
@@ -192,4 +216,11 @@ def test_mixed_steps_token_identical_on_gpu(gpu, monkeypatch):
                 outs[o.request_id] = o
         res.append([outs[r].all_ids for r in rids])
         assert (eng.stats.mixed_steps > 0) == mixed
-    assert res[0] == res[1]
+        engs.append(eng)
+    G.clear_plans()
+    differ = [(a, b) for a, b in zip(res[0], res[1]) if a != b]
+    assert len(differ) <= 1, len(differ)
+    for a, b in differ:
+        n = next(i for i, (x, y) in enumerate(zip(a, b)) if x != y)
+        top = _fp32_top2(engs[0], a[:n])
+        assert (top[0] - top[1]).item() < 0.01 * top[0].abs().item() + 0.01, (n, top)

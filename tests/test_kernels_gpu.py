@@ -386,6 +386,56 @@ def test_gemm_epilogues(gpu, epi, M, N, K):
                 assert out.dtype == torch.float32
 
 
+@pytest.mark.parametrize("tile,splits", [(22, 8), (28, 4), (23, 2), (25, 4), (0, 2)])
+@pytest.mark.parametrize("scale", [1.0, 3e4])
+def test_fp16_slabs_match_fp32_reference(gpu, monkeypatch, tile, splits, scale):
+    """EPI "slab16": the split-K partials of the MFMA families stored as fp16 x 1/16 (half
+    the bytes of fp32 slabs) and reduced in fp32 by the fused consumers == the fp32 reference
+    within bf16 tolerance, at the M = 512 decode shapes; scale 3e4 puts partial sums at
+    1e4-1e5 — beyond fp16's 65504 without the 1/16 scale — and everything stays finite."""
+    from distributed_llm_inferencing_amd.ops import reference as RR
+    torch.manual_seed(12)
+    M, N, K = 512, 4096, 4096
+    x, w = rnd(M, K, dev=gpu) * scale, rnd(N, K, dev=gpu, scale=0.02)
+    r0, nw = rnd(M, N, dev=gpu) * scale, rnd(N, dev=gpu)
+    y = R.linear(x, w)
+    ref_out, ref_res = R.fused_add_rmsnorm(y, r0, nw, 1e-5)
+    outs = {}
+    for s16 in (True, False):
+        monkeypatch.setattr(G, "SLAB16", s16)
+        G.set_plan(M, N, K, "splitk", G.GemmPlan("dli", tile, splits))
+        res = r0.clone()
+        out = ops.linear_add_rmsnorm(x, w, res, nw, 1e-5)
+        assert torch.isfinite(out).all() and torch.isfinite(res.float()).all()
+        close(out, ref_out, rtol=2e-2, atol=3e-2)
+        close(res, ref_res, rtol=1e-2, atol=2e-2 * scale)
+        outs[s16] = res
+    G.clear_plans()
+    # fp16 partials differ from fp32 partials by at most a few bf16 ulps of the residual
+    d = (outs[True].float() - outs[False].float()).abs()
+    assert d.max().item() <= 2 ** -6 * outs[False].float().abs().max().item() + 1e-3
+    # the QKV consumer (RoPE + paged KV write) on the same slab format
+    hq, hkv, hd = 32, 8, 128
+    Nq = (hq + 2 * hkv) * hd
+    wq = rnd(Nq, K, dev=gpu, scale=0.02)
+    pos = torch.arange(M, device=gpu, dtype=torch.int32) % 100
+    slots = torch.arange(M, device=gpu, dtype=torch.int32)
+    kc = torch.zeros(M // 16, hkv, 16, hd, dtype=BF, device=gpu)
+    vc = torch.zeros_like(kc)
+    cs = RR.rope_cos_sin(128, hd, 500000.0, device=gpu)
+    if Nq % (splits * 64) == 0 and K % (splits * 64) == 0:
+        monkeypatch.setattr(G, "SLAB16", True)
+        G.set_plan(M, Nq, K, "splitk", G.GemmPlan("dli", tile, splits))
+        qkv = ops.linear_rope_cache(x, wq, pos, slots, cs, kc, vc, hq, hkv, hd)
+        G.clear_plans()
+        qkv_r = R.linear(x, wq)
+        kc_r, vc_r = torch.zeros_like(kc), torch.zeros_like(vc)
+        R.rope_and_cache(qkv_r, pos, slots, cs, kc_r, vc_r, hq, hkv, hd)
+        close(qkv, qkv_r, rtol=2e-2, atol=3e-2 * scale)
+        close(kc, kc_r, rtol=2e-2, atol=3e-2 * scale)
+        close(vc, vc_r, rtol=2e-2, atol=3e-2 * scale)
+
+
 @pytest.mark.parametrize("M,N,K", [(3, 512, 1024), (256, 4096, 4096), (77, 4096, 14336),
                                    (64, 8192, 3072), (5, 2000, 1024), (1, 4096, 4096),
                                    (4, 4096, 14336), (2, 5120, 3072)])

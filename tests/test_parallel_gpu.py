@@ -199,3 +199,49 @@ def test_expert_parallel_over_ipc_graphs_on_gpu(gpu, world):
             assert graph_steps > 0 and uploads == graph_steps   # one H2D + one replay
     finally:
         del os.environ["DLI_GEMM_AUTOTUNE"]
+
+
+def _register_16l():
+    from dataclasses import replace
+    from distributed_llm_inferencing_amd.models.configs import get_config, register
+    register(replace(get_config("llama3-8b"), name="llama3-8b-16l", num_layers=16))
+
+
+def _pp8_worker(rank, world, port, q):
+    _env(rank, world, port)
+    os.environ.pop("DLI_PP_COMM", None)          # the default plane: the IPC mailboxes
+    os.environ.pop("DLI_PP_VOCAB_PARALLEL", None)  # the default head at N >= 4: vocab-parallel
+    _register_16l()
+    import torch.distributed as dist
+    from distributed_llm_inferencing_amd.parallel.pipeline import DistributedPipelineEngine
+    eng = DistributedPipelineEngine("llama3-8b-16l", "cuda", max_batch=8, max_model_len=64,
+                                    num_blocks=64)
+    assert eng.channel.comm == "ipc" and eng.vocab_parallel
+    assert eng.stage.plan.end_layer - eng.stage.plan.start_layer == 2
+    eng.warmup()
+    if rank == 0:
+        q.put([o.all_ids for o in eng.generate(PROMPTS, GREEDY)])
+        eng.shutdown()
+    else:
+        eng.serve()
+    dist.barrier()
+    eng.channel.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(420)
+def test_pipeline_pp8_real_shape_stages_match_single_engine(gpu):
+    """The driver's 8-rank pipeline form at the real Llama-3-8B layer shapes (d 4096, 32 q /
+    8 kv heads, FFN 14336, vocab 128256), 2 layers per stage, all 8 ranks on cuda:0: default
+    data plane (IPC mailboxes), vocab-parallel head, M = 11 microbatches, decode graphs with
+    the captured receive / send — greedy tokens identical to one engine holding all 16
+    layers."""
+    (res,) = _run(_pp8_worker, 8)
+    _register_16l()
+    os.environ["DLI_GEMM_AUTOTUNE"] = "0"
+    try:
+        eng = LLMEngine("llama3-8b-16l", device="cuda", max_batch=8, max_model_len=64,
+                        num_blocks=64)
+        assert res == [o.all_ids for o in eng.generate(PROMPTS, GREEDY)]
+    finally:
+        del os.environ["DLI_GEMM_AUTOTUNE"]
