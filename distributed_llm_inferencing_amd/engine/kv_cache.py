@@ -26,18 +26,21 @@ def blocks_for_budget(cfg: ModelConfig, num_layers: int, block_size: int, budget
 
 def auto_num_blocks(cfg: ModelConfig, num_layers: int, block_size: int, device,
                     fraction: float = 0.85, reserve_bytes: Optional[int] = None,
-                    cap_tokens: int = 0) -> int:
+                    cap_tokens: int = 0, pending_bytes: int = 0) -> int:
     """Blocks that fit in ``fraction`` of the HBM still free (weights already resident)
     minus a reserve for activations, GEMM workspaces and graph pools: the KV pool is sized
     for the 288 GB of an MI355X (Llama-3-8B: ~1.7M tokens of context on one GPU), not for
     max_batch x max_model_len. ``cap_tokens`` / ``DLI_KV_MAX_TOKENS`` cap it (0 = no cap).
-    Ranks sharing one device (``DLI_SAME_DEVICE=1`` rehearsals) split it by
-    ``LOCAL_WORLD_SIZE``."""
+    ``pending_bytes``: weights that will land on this device after the pool is sized (a
+    pipeline stage sizes its pool before it loads its layers; ranks sharing one device pass
+    every rank's). Ranks sharing one device (``DLI_SAME_DEVICE=1`` rehearsals) split the rest
+    by ``LOCAL_WORLD_SIZE``."""
     dev = torch.device(device)
     env_cap = int(os.environ.get("DLI_KV_MAX_TOKENS", "0") or 0)
     cap_tokens = env_cap or cap_tokens
     if dev.type == "cuda":
         free, total = torch.cuda.mem_get_info(dev)
+        free = max(0, free - int(pending_bytes))
         if reserve_bytes is None:
             reserve_bytes = max(8 << 30, int(0.03 * total))
         if os.environ.get("DLI_SAME_DEVICE", "0") == "1":

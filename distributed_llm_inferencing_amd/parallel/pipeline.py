@@ -222,9 +222,40 @@ def vp_ok(meta: Optional[StepMeta]) -> bool:
 H_VP = 13          # ctrl header word: 1 = vocab-parallel head for this step
 
 
-def _stage_capacity_blocks(cfg, plan, block_size, device, kv_fraction, cap_tokens):
+def _stage_capacity_blocks(cfg, plan, block_size, device, kv_fraction, cap_tokens,
+                           vocab_slice: Optional[Tuple[int, int]] = None,
+                           loaded: bool = False):
+    """KV blocks of this stage's pool, sized before its weights are loaded: the stage's own
+    parameter bytes (plus its vocab-parallel head slice) are still to come, and with every
+    rank on one device (``DLI_SAME_DEVICE=1``) so are every other rank's — summed over the
+    ranks, or 8 ranks each sizing against the empty device over-commit it (Llama-3-70B pp8 on
+    one GPU ran out of memory: profiles/r6/README.md)."""
+    pending = 0
+    if not loaded:                      # the shard-file path loads before sizing the pool
+        shapes = W.stage_param_shapes(cfg, plan.start_layer, plan.end_layer, plan.first,
+                                      plan.last)
+        pending = sum(int(np.prod(s)) for s in shapes.values()) * 2
+        if vocab_slice is not None:
+            pending += (vocab_slice[1] - vocab_slice[0]) * cfg.hidden_size * 2
+    if os.environ.get("DLI_SAME_DEVICE", "0") == "1" and dist.is_initialized():
+        t = torch.tensor([pending], dtype=torch.int64)
+        dist.all_reduce(t, group=_cpu_group())
+        pending = int(t.item())
     return auto_num_blocks(cfg, plan.end_layer - plan.start_layer, block_size, device,
-                           kv_fraction, cap_tokens=cap_tokens)
+                           kv_fraction, cap_tokens=cap_tokens, pending_bytes=pending)
+
+
+_CPU_GROUP = None
+
+
+def _cpu_group():
+    """A gloo group over every rank (host-side sums when the default group is RCCL)."""
+    global _CPU_GROUP
+    if _CPU_GROUP is None:
+        from datetime import timedelta
+        _CPU_GROUP = (dist.group.WORLD if dist.get_backend() == "gloo"
+                      else dist.new_group(backend="gloo", timeout=timedelta(minutes=30)))
+    return _CPU_GROUP
 
 
 class _TokenRing:
@@ -741,7 +772,8 @@ def build_stage(cfg: ModelConfig, rank: int, world: int, device, max_batch: int,
         # this stage's layers' KV from its free HBM (288 GB per MI355X); every stage holds
         # the same block ids (the head's allocator), so all take the smallest pool
         cap = _stage_capacity_blocks(cfg, plan, block_size, device, kv_fraction,
-                                     cap_tokens=max_kv_tokens)
+                                     cap_tokens=max_kv_tokens, vocab_slice=vs,
+                                     loaded=params is not None)
         t = torch.tensor([cap], dtype=torch.int64,
                          device=device if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MIN)     # block ids are global: same pool size

@@ -1,19 +1,16 @@
 #!/bin/bash
-# Session 6 (round 6): BASELINE config 4 in the driver's 8-rank form on one GPU — Llama-3-70B
+# Session 7 (round 6): BASELINE config 4 in the driver's 8-rank form on one GPU — Llama-3-70B
 # layer-sharded over 8 pipeline ranks (random init, then the reference flow: shard-model
 # --num_shards 8 export -> every rank loads its own shard file via --shard-dir).
 set -u
-O=gpurun_out/r6s06
+O=gpurun_out/r6s07
 mkdir -p $O
 : > $O/bench.jsonl
 step() { local name=$1 t=$2; shift 2; echo "== $name"; timeout -k 10 $t "$@" > $O/$name.log 2>&1; local rc=$?;
          echo "rc[$name]=$rc"; tail -2 $O/$name.log; [ $rc -eq 0 ] || exit $rc; }
 rec() { echo "{\"arm\": \"$1\", \"bench\": $(grep -h '^{"metric"' $O/$1.log)}" >> $O/bench.jsonl; }
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o wave -- python3 bench.py --steps 1 --warmup 1 > $O/prof.log 2>&1
-rc=$?; echo "rc[prof]=$rc"; [ $rc -eq 0 ] || exit $rc
-python3 scripts/prof_summary.py $O/prof 30 --tail-ms 800 --gaps 5 > $O/wave_summary.txt 2>&1
-rm -rf $O/prof
+# (s06: the rocprofv3 wave of the fp16-slab default, then 70B pp8 ran out of HBM: every rank
+# sized its KV pool before any weights were resident; fixed by counting pending weights)
 export DLI_SAME_DEVICE=1 DLI_GEMM_AUTOTUNE=0
 step llama70b_pp8 600 python3 -u bench.py --model llama3-70b --gpus 8 --batch 64 --steps 2 --warmup 1
 rec llama70b_pp8
