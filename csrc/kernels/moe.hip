@@ -162,6 +162,63 @@ extern "C" int dli_moe_combine(void* out, const void* y, const float* w, const i
   DLI_RETURN_LAUNCH();
 }
 
+// The combine fused with the down projection's split-K reduce: the grouped down GEMM leaves
+// S fp16 x 1/16 partial slabs [S, rows, dim] (EPI_SLAB16, permuted rows) instead of a bf16 y;
+// each (token, pick) row is summed over the slabs in slab order, rounded to bf16 exactly as
+// the bf16 GEMM output would be, weighted and accumulated as in moe_combine_kernel. The
+// expert output never makes the bf16 round trip through memory and no reduce kernel runs.
+template <int S>
+__global__ void __launch_bounds__(256) moe_combine_slabs_kernel(
+    u16* __restrict__ out, const u16* __restrict__ ws, long slab_stride,
+    const float* __restrict__ w, const int* __restrict__ pos, int T, int k, int dim) {
+  const int chunks = dim >> 3;
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (long)T * chunks) return;
+  const int t = (int)(gid / chunks), c = (int)(gid % chunks);
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int j = 0; j < k; ++j) {
+    const int p = pos[t * k + j];
+    if (p < 0) continue;
+    uint4 u[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+      u[s] = *reinterpret_cast<const uint4*>(ws + s * slab_stride + (long)p * dim + c * 8);
+    float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      float f[8];
+      unpack8h(u[s], f);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] += f[q];
+    }
+    const float ww = w[t * k + j];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] += ww * bf2f(f2bf(v[q]));
+  }
+  store8(out + (long)t * dim + c * 8, acc);
+}
+
+// ws: the fp16 slabs of a grouped split-K GEMM over `rows` permuted rows (slab stride rows x dim)
+extern "C" int dli_moe_combine_slabs(void* out, const void* ws, int splits, int rows,
+                                     const float* w, const int* pos, int T, int k, int dim,
+                                     hipStream_t st) {
+  if (T <= 0) return 0;
+  if (dim % 8) return (int)hipErrorInvalidValue;
+  const long total = (long)T * (dim / 8);
+  const int blocks = (int)((total + 255) / 256);
+  const long stride = (long)rows * dim;
+#define DLI_MCS(S) moe_combine_slabs_kernel<S><<<blocks, 256, 0, st>>>(               \
+      (u16*)out, (const u16*)ws, stride, w, pos, T, k, dim)
+  switch (splits) {
+    case 2: DLI_MCS(2); break;
+    case 4: DLI_MCS(4); break;
+    case 8: DLI_MCS(8); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef DLI_MCS
+  DLI_RETURN_LAUNCH();
+}
+
 // Expert-parallel dispatch pack (parallel/expert.py): every (token t, pick j) row goes to
 // the bucket of the rank that holds its expert:
 //   dest = id / e_per,  pos[t*k + j] = base[dest] + atomicAdd(&fill[dest], 1),

@@ -650,11 +650,38 @@ def moe_mlp(x, w_gu, w_down, topk_w, topk_ids, expert_offset: int = 0,
         p_dn = G.grouped_plan(plan_rows, D, F2 // 2, "none", E_local)
     _gemm_native(xp, w_gu, "silu_mul", out=act, groups=E_local, group_off=offsets,
                  rows_per_group=n, plan=p_gu)
+    p_dn = p_dn or G.grouped_plan(n, D, F2 // 2, "none", E_local)
+    if moe_slab_plan(p_dn):
+        out = torch.empty_like(x)
+        moe_down_combine(act, w_down, offsets, n, p_dn, topk_w, pos, out)
+        return out
     y = torch.empty(max(n, 1), D, dtype=x.dtype, device=dev)
     _gemm_native(act, w_down, "none", out=y, groups=E_local, group_off=offsets,
                  rows_per_group=n, plan=p_dn)
     out = torch.empty_like(x)
     _native_call("dli_moe_combine", _p(out), _p(y), _p(topk_w), _p(pos), T, k, D, _st())
+    return out
+
+
+def moe_slab_plan(p: Optional[G.GemmPlan]) -> bool:
+    """Whether a grouped down-projection plan runs as fp16 split-K slabs reduced inside the
+    combine (``moe_down_combine``) instead of GEMM -> fp32 slab reduce -> bf16 y -> combine."""
+    return (p is not None and G.SLAB16 and p.splits in (2, 4, 8)
+            and p.tile in G.SLAB16_TILES)
+
+
+def moe_down_combine(act, w_down, offsets, n: int, p: G.GemmPlan, topk_w, pos, out):
+    """Grouped down projection of the ``n`` permuted rows ``act`` as fp16 split-K slabs
+    (EPI "slab16"), reduced by the combine itself: out[t] = sum_j topk_w[t, j] *
+    bf16(sum_s slab_s[pos[t, j]]) (csrc/kernels/moe.hip moe_combine_slabs_kernel)."""
+    E_local, D, F = w_down.shape
+    ws = G.workspace(act.device, p.splits * max(n, 1) * D * 2)
+    _native_call("dli_gemm", _p(act), act.stride(0), _p(w_down), w_down.stride(-2), None, D,
+                 n, D, F, G.EPI["slab16"], p.tile, p.splits, None, _p(ws), _p(offsets),
+                 E_local, _st())
+    T, k = pos.shape
+    _native_call("dli_moe_combine_slabs", _p(out), _p(ws), p.splits, n, _p(topk_w), _p(pos),
+                 T, k, D, _st())
     return out
 
 

@@ -264,6 +264,11 @@ def autotune_grouped(rows: int, w: torch.Tensor, epi: str, iters: int = 5, log=N
     off = torch.tensor([0] + list(__import__("itertools").accumulate(counts)),
                        dtype=torch.int32, device=dev)
     x = (torch.randn(max(rows, 1), K, device=dev) * 0.5).to(w.dtype)
+    # the down projection's split plans on the fp16-slab tiles run fused with the combine
+    # (ops.moe_down_combine): time them that way (one pick per row, weight 1)
+    ones = torch.ones(max(rows, 1), 1, dtype=torch.float32, device=dev)
+    ident = torch.arange(max(rows, 1), dtype=torch.int32, device=dev).view(-1, 1)
+    comb = torch.empty(max(rows, 1), N, dtype=w.dtype, device=dev)
     best = None
     cands = []
     for tile in sorted(TILES):
@@ -273,10 +278,16 @@ def autotune_grouped(rows: int, w: torch.Tensor, epi: str, iters: int = 5, log=N
             if splits == 1 or (K % (64 * splits) == 0 and K // splits >= 2048):
                 cands.append(GemmPlan("dli", tile, splits))
     for p in cands:
+        fused = epi == "none" and ops.moe_slab_plan(p)
+
+        def run(p=p, fused=fused):
+            if fused:
+                ops.moe_down_combine(x, w, off, rows, p, ones, ident, comb)
+            else:
+                ops._gemm_native(x, w, epi, plan=p, groups=E, group_off=off,
+                                 rows_per_group=rows)
         try:
-            ms = ops.benchmark(lambda p=p: ops._gemm_native(
-                x, w, epi, plan=p, groups=E, group_off=off, rows_per_group=rows),
-                iters=iters, warmup=1, graph=_GRAPH_TUNE)
+            ms = ops.benchmark(run, iters=iters, warmup=1, graph=_GRAPH_TUNE)
         except Exception:  # noqa: BLE001
             continue
         if best is None or ms < best[1]:

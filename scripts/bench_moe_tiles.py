@@ -44,6 +44,9 @@ def main():
         x = (torch.randn(rows, K, device=dev) * 0.5).to(torch.bfloat16)
         out = []
         rpg = max(counts) if only else rows
+        ones = torch.ones(rows, 1, dtype=torch.float32, device=dev)
+        ident = torch.arange(rows, dtype=torch.int32, device=dev).view(-1, 1)
+        comb = torch.empty(rows, N, dtype=torch.bfloat16, device=dev)
         for tile in (only or sorted(G.TILES)):
             if not only and (G.TILES[tile][0] > 2 * max(64, rows // E + 32)
                              or not G.tile_ok(tile, epi)):
@@ -52,16 +55,24 @@ def main():
                 if splits > 1 and not (K % (64 * splits) == 0 and K // splits >= 2048):
                     continue
                 p = G.GemmPlan("dli", tile, splits)
+                # split down plans on the fp16-slab tiles: the fused slab combine as the
+                # model runs it (ops.moe_down_combine; one pick per row, weight 1)
+                fused = which == "down" and ops.moe_slab_plan(p) and not only
+
+                def run(p=p, fused=fused):
+                    if fused:
+                        ops.moe_down_combine(x, w, off, rows, p, ones, ident, comb)
+                    else:
+                        ops._gemm_native(x, w, epi, plan=p, groups=E, group_off=off,
+                                         rows_per_group=rpg)
                 try:
-                    ms = ops.benchmark(lambda p=p: ops._gemm_native(
-                        x, w, epi, plan=p, groups=E, group_off=off, rows_per_group=rpg),
-                        iters=a.iters, warmup=1)
+                    ms = ops.benchmark(run, iters=a.iters, warmup=1)
                 except Exception as e:  # noqa: BLE001
                     out.append({"which": which, "tile": tile, "splits": splits,
                                 "error": str(e)[:60]})
                     continue
                 out.append({"which": which, "rows": rows, "tile": tile,
-                            "bm_bn": G.TILES.get(tile), "splits": splits,
+                            "bm_bn": G.TILES.get(tile), "splits": splits, "fused": fused,
                             "us": round(ms * 1e3, 1),
                             "tflops": round(2.0 * rows * N * K / (ms * 1e-3) / 1e12, 1),
                             "weight_TBps": round(w.numel() * 2 / (ms * 1e-3) / 1e12, 2)})

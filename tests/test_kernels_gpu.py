@@ -704,6 +704,38 @@ def test_moe_route_and_mlp(gpu, T, E, k):
         close(out2, ref2, rtol=3e-2, atol=3e-2)
 
 
+@pytest.mark.parametrize("tile,splits", [(26, 2), (12, 4), (28, 2), (22, 4)])
+def test_moe_down_split_slabs_fused_combine(gpu, tile, splits):
+    """Decode-sized MoE whose grouped down projection runs as fp16 split-K slabs reduced
+    inside the combine (ops.moe_down_combine) == the fp32 reference, and == the unfused
+    path (GEMM with the bf16 y, then the combine) within bf16 rounding; the experts' rows
+    are uneven (seeded multinomial routing) and one expert gets no row."""
+    torch.manual_seed(21)
+    T, E, k, D, F = 96, 8, 2, 512, 1024
+    x = rnd(T, D, dev=gpu)
+    logits = rnd(T, E, dev=gpu)
+    logits[:, 5] = -30.0                          # expert 5 is never picked
+    rw, rids = R.router_topk(logits, k)
+    wgu = rnd(E, 2 * F, D, dev=gpu, scale=0.05)
+    wd = rnd(E, D, F, dev=gpu, scale=0.05)
+    key = (G._bucket(T * k), D, F, "none", E)
+    old = G._grouped_cache.get(key)
+    G._grouped_cache[key] = G.GemmPlan("dli", tile, splits)
+    try:
+        assert ops.moe_slab_plan(G.grouped_plan(T * k, D, F, "none", E))
+        out = ops.moe_mlp(x, wgu, wd, rw, rids)
+        G._grouped_cache[key] = G.GemmPlan("dli", tile, 1)
+        unfused = ops.moe_mlp(x, wgu, wd, rw, rids)
+    finally:
+        if old is None:
+            G._grouped_cache.pop(key, None)
+        else:
+            G._grouped_cache[key] = old
+    ref = R.moe_mlp(x, wgu, wd, rw, rids)
+    close(out, ref, rtol=3e-2, atol=3e-2)
+    close(out, unfused, rtol=2e-2, atol=2e-2)
+
+
 def test_sampling_fallback_path_adversarial(gpu):
     """Top-k values concentrated in ONE thread's strided slice force the exact radix-select
     fallback (the register top-8 fast path cannot prove completeness)."""
