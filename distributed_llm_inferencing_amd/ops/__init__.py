@@ -673,13 +673,13 @@ def moe_slab_plan(p: Optional[G.GemmPlan]) -> bool:
 def moe_down_combine(act, w_down, offsets, n: int, p: G.GemmPlan, topk_w, pos, out):
     """Grouped down projection of the ``n`` permuted rows ``act`` as fp16 split-K slabs
     (EPI "slab16"), reduced by the combine itself: out[t] = sum_j topk_w[t, j] *
-    bf16(sum_s slab_s[pos[t, j]]) (csrc/kernels/moe.hip moe_combine_slabs_kernel)."""
+    bf16(sum_s slab_s[pos[t * k + j]]) (csrc/kernels/moe.hip moe_combine_slabs_kernel)."""
     E_local, D, F = w_down.shape
     ws = G.workspace(act.device, p.splits * max(n, 1) * D * 2)
     _native_call("dli_gemm", _p(act), act.stride(0), _p(w_down), w_down.stride(-2), None, D,
                  n, D, F, G.EPI["slab16"], p.tile, p.splits, None, _p(ws), _p(offsets),
                  E_local, _st())
-    T, k = pos.shape
+    T, k = topk_w.shape                  # pos: [T * k] rows (flat, as moe_align writes it)
     _native_call("dli_moe_combine_slabs", _p(out), _p(ws), p.splits, n, _p(topk_w), _p(pos),
                  T, k, D, _st())
     return out
