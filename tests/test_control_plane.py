@@ -7,6 +7,7 @@ import time
 
 import pytest
 import requests
+import torch
 from werkzeug.serving import make_server
 
 from distributed_llm_inferencing_amd.config import Settings
@@ -353,6 +354,10 @@ def test_loadgen_end_to_end(tmp_path, master):
     # keeps the pollers from competing with the engine thread for the GIL on a loaded host.
     # Root cause of the earlier flake: 2 dispatcher slots serialised the 12 requests into 6
     # rounds of a 2-row batch, which took > 120 s under CPU contention.
+    # one intra-op thread: under pytest-xdist the OpenMP pools of several workers oversubscribe
+    # the host's CPUs and spin-wait into one another (every request hit its 60 s deadline)
+    threads = torch.get_num_threads()
+    torch.set_num_threads(1)
     master.extensions["dli"].shutdown()
     master = create_master_app(settings(tmp_path, master_db=str(tmp_path / "lg.sqlite3")),
                                start_background=True, dispatch_workers=6, health_interval=0.5)
@@ -371,6 +376,7 @@ def test_loadgen_end_to_end(tmp_path, master):
         assert rep["p50_latency_s"] <= rep["p99_latency_s"]
         assert rep["requests_per_s"] > 0
     finally:
+        torch.set_num_threads(threads)
         ms.close()
         w.close()
         master.extensions["dli"].shutdown()
