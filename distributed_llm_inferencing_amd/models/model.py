@@ -232,8 +232,8 @@ class TransformerLM:
         return ops.rmsnorm(hidden, p["final_norm"], cfg.norm_eps)
 
     def head_logits(self, h: torch.Tensor) -> torch.Tensor:
-        """LM head in the model dtype (``ops.HEAD_EPI``), as HF's ``lm_head(h).float()``:
-        the sampler reads the bf16 logits and compares their exact fp32 values."""
+        """LM head with fp32 logits (``ops.HEAD_EPI``: the GEMM's fp32 accumulators stored as
+        they are); the sampler compares their exact values."""
         p = self.params
         return ops.linear(h, p["embed"] if self.cfg.tie_embeddings else p["lm_head"],
                           epi=ops.HEAD_EPI)

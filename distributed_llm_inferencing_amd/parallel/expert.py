@@ -29,6 +29,7 @@ from __future__ import annotations
 
 import logging
 import os
+import threading
 import time
 from typing import List, Optional
 
@@ -341,6 +342,32 @@ class ExpertParallelEngine:
         self.board = self._open_board()
         self.control_plane = "shm" if self.board is not None else "gloo"
         self.lockstep_s = 0.0
+        # liveness watchdog: a peer that dies mid-forward would leave this rank's
+        # queue spinning in its mailbox waits for the whole wait budget; the board knows every
+        # rank's pid, so a death aborts the mailboxes within ~0.2 s and the next step raises
+        self.dead_peer: Optional[str] = None
+        self._wd_stop = threading.Event()
+        self._wd = None
+        if self.board is not None:
+            self._wd = threading.Thread(target=self._watch, args=(0.2,), daemon=True,
+                                        name=f"dli-ep-watchdog-{self.rank}")
+            self._wd.start()
+
+    def _watch(self, period: float) -> None:
+        while not self._wd_stop.wait(period):
+            board = self.board
+            d = board.dead() if board is not None else -1
+            if d < 0 or d == self.rank:
+                continue
+            self.dead_peer = f"expert-parallel rank {d} exited"
+            ep = self.moe.ep
+            if ep is not None and hasattr(ep, "abort"):
+                try:
+                    ep.abort(5.0)
+                except Exception:  # noqa: BLE001
+                    pass
+            board.close()               # a lockstep exchange blocked on it returns
+            return
 
     def _open_board(self):
         """A ``LockstepBoard`` shared by every rank of the group, or None when the ranks span
@@ -439,6 +466,9 @@ class ExpertParallelEngine:
         rank, then launch the forward (an empty one when this rank has none) and apply the
         tokens of the step that completes. Returns (outputs, any rank had work)."""
         eng = self.engine
+        if self.dead_peer is not None:
+            from .transport import PeerDied
+            raise PeerDied(self.dead_peer)
         if self.moe.ep is not None:
             bits = self.moe.ep.error()
             if bits:
@@ -466,10 +496,16 @@ class ExpertParallelEngine:
         run = eng.runner
         run.force_eager = max(toks) > self.max_batch
         replayed = run.replays
-        if meta is None:
-            self._idle_forward()
-        self.steps += 1
-        out = eng.finish_step(meta)
+        try:
+            if meta is None:
+                self._idle_forward()
+            self.steps += 1
+            out = eng.finish_step(meta)
+        except Exception as e:
+            if self.dead_peer is not None:      # stale rows after the abort: name the cause
+                from .transport import PeerDied
+                raise PeerDied(self.dead_peer) from e
+            raise
         self.graph_steps += run.replays - replayed
         return out, True
 
@@ -500,6 +536,9 @@ class ExpertParallelEngine:
                              "total_layers": self.cfg.num_layers}}
 
     def close(self) -> None:
+        self._wd_stop.set()
+        if self._wd is not None:
+            self._wd.join(1.0)
         self.moe.close()
         if self.board is not None:
             self.board.close()

@@ -100,6 +100,8 @@ class ShmMailboxTransport:
         t0 = time.monotonic()
         spins = 0
         while arr[idx] != 1:
+            if self.err & 4:             # aborted: sticky, every later wait passes (as on device)
+                return
             spins += 1
             if spins > 200:
                 time.sleep(0.0002 if spins < 5000 else 0.002)

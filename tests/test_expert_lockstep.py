@@ -150,3 +150,58 @@ def test_expert_service_idles_on_the_doorbell_and_stops_cleanly():
         assert frac < 0.05, (rank, frac)
         assert waits <= 6, (rank, waits)     # ~1 per second of idling, not one per 2 ms
         assert syncs < 200, (rank, syncs)
+
+
+def _dying_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), DLI_EP_COMM="ipc")
+    torch.set_num_threads(1)
+    from distributed_llm_inferencing_amd.parallel.expert import ExpertParallelEngine
+    eng = ExpertParallelEngine("mixtral-tiny", "cpu", max_batch=8, max_model_len=64,
+                               num_blocks=64, dtype=torch.float32)
+    assert eng.comm == "ipc" and eng.control_plane == "shm"
+    sp = SamplingParams(max_length=12, do_sample=False, ignore_eos=True)
+    eng.generate([[5, 6, 7]], sp)                     # both ranks healthy
+    if rank == 1:
+        inner = eng.moe.__class__.__call__
+
+        def die(self, h, lp, layer):
+            if layer == 1:
+                q.put((1, "exiting"))
+                q.close()
+                q.join_thread()
+                os._exit(0)                           # mid-forward: rank 0 waits on its rows
+            return inner(self, h, lp, layer)
+        eng.moe.__class__.__call__ = die
+    t0 = time.monotonic()
+    try:
+        eng.generate([[1, 2, 3, 4]], sp)
+        q.put((0, ("no error", time.monotonic() - t0)))
+    except Exception as e:  # noqa: BLE001
+        q.put((0, (f"{type(e).__name__}: {e}", time.monotonic() - t0)))
+    os._exit(0)
+
+
+def test_expert_rank_death_mid_forward_fails_fast():
+    """A rank that dies inside a forward (rank 0 waiting in its mailboxes for the dead rank's
+    rows) is seen by the board watchdog: the mailboxes are aborted and the survivor's next
+    step raises within seconds, not after the 120 s wait budget."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_dying_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = {}
+    try:
+        for _ in range(2):
+            r, v = q.get(timeout=300)
+            res[r] = v
+    finally:
+        for p in ps:
+            p.join(60)
+            if p.is_alive():
+                p.kill()
+    msg, dt = res[0]
+    assert dt < 10.0, (msg, dt)
+    assert "rank 1" in msg, msg
