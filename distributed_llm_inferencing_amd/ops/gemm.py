@@ -129,25 +129,6 @@ _workspaces: dict = {}
 _retired: list = []
 
 
-_tickets: dict = {}
-
-
-def tickets(device: torch.device, n: int, stream: int = 0) -> torch.Tensor:
-    """Zeroed uint32 arrival counters for in-launch split-K combines, one buffer per (device,
-    stream) — launches on one stream never overlap — grow-only and never freed (captured
-    graphs keep the pointer). Every launch's last arrivers reset the counters they used, so
-    they are zero again for the next launch on the stream."""
-    key = (device.type, device.index, int(stream))
-    with _ws_lock:
-        t = _tickets.get(key)
-        if t is None or t.numel() < n:
-            if t is not None:
-                _retired.append(t)
-            t = torch.zeros(max(n, 4096), dtype=torch.int32, device=device)
-            _tickets[key] = t
-        return t
-
-
 def workspace(device: torch.device, nbytes: int) -> torch.Tensor:
     """Grow-only scratch (bytes) per device. Never freed: see ``_retired``."""
     key = (device.type, device.index)
