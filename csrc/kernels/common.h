@@ -36,12 +36,16 @@ __device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
   return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
 }
 
-__device__ __forceinline__ void load8(const u16* p, float* f) {
-  uint4 v = *reinterpret_cast<const uint4*>(p);
+// 8 bf16 (one 16-B word) -> fp32
+__device__ __forceinline__ void unpack8bf(const uint4 v, float* f) {
   f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
   f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
   f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
   f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+}
+
+__device__ __forceinline__ void load8(const u16* p, float* f) {
+  unpack8bf(*reinterpret_cast<const uint4*>(p), f);
 }
 
 __device__ __forceinline__ void store8(u16* p, const float* f) {

@@ -217,8 +217,7 @@ class TransformerLM:
         return self._attend(qkv, b, kc, vc)
 
     def _moe_local(self, h: torch.Tensor, lp: dict, layer: int) -> torch.Tensor:
-        router_logits = ops.linear(h, lp["router"])
-        topk_w, topk_ids = ops.moe_route(router_logits, self.cfg.top_k_experts)
+        topk_w, topk_ids = ops.moe_router(h, lp["router"], self.cfg.top_k_experts)
         e0 = self.expert_range[0] if self.expert_range else 0
         return ops.moe_mlp(h, lp["w_gu"], lp["w_down"], topk_w, topk_ids, e0)
 

@@ -601,6 +601,23 @@ def moe_route(router_logits, k: int):
     return w, ids
 
 
+def moe_router(h, w_router, k: int):
+    """The MoE gate: logits = h @ w_router.T (bf16, as a GEMM would write them), softmax,
+    top-``k``, renormalised. On the GPU with <= 8 experts one kernel does all of it
+    (``moe_router_kernel``, a wave per token); else the GEMM then ``moe_route``."""
+    T, D = h.shape
+    E = w_router.shape[0]
+    if (_use_native(h) and E <= 8 and D % 8 == 0 and h.stride(-1) == 1
+            and h.stride(0) % 8 == 0 and w_router.is_contiguous()
+            and h.data_ptr() % 16 == 0 and w_router.data_ptr() % 16 == 0):
+        w = torch.empty(T, k, dtype=torch.float32, device=h.device)
+        ids = torch.empty(T, k, dtype=torch.int32, device=h.device)
+        _native_call("dli_moe_router", _p(w), _p(ids), _p(h), h.stride(0), _p(w_router), T, E,
+                     D, k, _st())
+        return w, ids
+    return moe_route(linear(h, w_router), k)
+
+
 def moe_mlp(x, w_gu, w_down, topk_w, topk_ids, expert_offset: int = 0,
             plan_rows: Optional[int] = None):
     """Experts [expert_offset, expert_offset+E_local) of one MoE layer; returns the weighted

@@ -6,7 +6,7 @@ Layout: data-parallel attention + expert-parallel MoE. Every rank holds the full
 / norm / embedding weights and its own requests + paged KV; rank r holds experts
 [r*E/N, (r+1)*E/N). Per MoE layer, all on device:
 
-    route (softmax -> top-2 -> renormalise)                  moe_route kernel
+    route (gate logits -> softmax -> top-2 -> renormalise)   moe_router kernel
     dispatch pack: (token, pick) rows into per-rank buckets  ep_pack kernel
     all_to_all_single (rows + their expert ids)              RCCL, all 7 xGMI links at once
     local expert MLPs on the rows received                   moe_align/gather + grouped GEMM
@@ -198,8 +198,7 @@ class ExpertParallelMoE:
             raise RuntimeError("ExpertParallelMoE: begin_step() must announce this step's "
                                "token counts before the forward")
         if T > 0:
-            router_logits = ops.linear(h, lp["router"])
-            topk_w, topk_ids = ops.moe_route(router_logits, k)
+            topk_w, topk_ids = ops.moe_router(h, lp["router"], k)
         else:
             topk_w = torch.zeros(0, k, dtype=torch.float32, device=dev)
             topk_ids = torch.zeros(0, k, dtype=torch.int32, device=dev)

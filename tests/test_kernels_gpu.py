@@ -931,6 +931,29 @@ def test_moe_route_wide(gpu, T, E, k):
     assert torch.allclose(w.sum(-1), torch.ones(T, device=gpu), atol=1e-5)
 
 
+@pytest.mark.parametrize("T,E,D", [(1, 8, 4096), (37, 8, 256), (512, 8, 4096), (64, 4, 512),
+                                   (9, 2, 128)])
+def test_moe_router_fused(gpu, T, E, D):
+    """The fused gate (moe_router_kernel: E <= 8 dot products per token, bf16 logits, softmax,
+    top-2, renormalise) against an fp32 reference: the picks are the top-2 of the bf16-rounded
+    logits up to near-ties (summation order may move a logit by one bf16 ulp), distinct per
+    token, and the weights are the renormalised softmax of the picked logits."""
+    torch.manual_seed(41)
+    k = 2
+    h = rnd(T, D, dev=gpu)
+    wr = rnd(E, D, dev=gpu, scale=0.05)
+    w, ids = ops.moe_router(h, wr, k)
+    lb = (h.float() @ wr.float().t()).to(BF).float()
+    il = ids.long()
+    assert ((il >= 0) & (il < E)).all() and (il[:, 0] != il[:, 1]).all()
+    kth = lb.topk(k, -1).values[:, -1:]
+    tol = 2 ** -7 * lb.abs().amax(-1, keepdim=True)
+    assert (lb.gather(1, il) >= kth - tol).all()
+    p = lb.softmax(-1).gather(1, il)
+    close(w, p / p.sum(-1, keepdim=True), rtol=2e-2, atol=2e-3)
+    assert torch.allclose(w.sum(-1), torch.ones(T, device=gpu), atol=1e-5)
+
+
 @pytest.mark.parametrize("S,V,c", [(37, 16032, 64), (5, 4008, 64), (3, 64, 64), (9, 50257, 50)])
 def test_topk_rows_kernel(gpu, S, V, c):
     """HIP per-row top-c (vocab-parallel head candidates) vs torch.topk: same value multiset,
