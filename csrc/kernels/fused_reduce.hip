@@ -112,6 +112,102 @@ static int launch_add_rmsnorm(u16* o, u16* r, const float* ws, int splits, int M
   DLI_RETURN_LAUNCH();
 }
 
+// The Mixtral O-projection reduce with the MoE gate fused in (fp16 slabs, rows of N = 512 x 8
+// columns: one 8-column vector per thread, 8 waves): residual += sum_s P_s; out =
+// rmsnorm(residual) * w; then the E <= 8 router logits of the bf16 output row (each thread's
+// 8 columns against the E router rows, requested with the slabs; per-wave sums added in LDS
+// in wave order), rounded to bf16, softmax, top-k (route_pick) — the separate gate kernel
+// (moe_router_kernel, 9 us per layer at batch 512) and its launch go away.
+template <int SPL>
+__global__ void __launch_bounds__(512) splitk_add_rmsnorm_route_kernel(
+    u16* __restrict__ out, u16* __restrict__ residual, const u16* __restrict__ ws16, int M,
+    int N, const u16* __restrict__ w, float eps, const u16* __restrict__ wr, int E, int k,
+    float* __restrict__ topk_w, int* __restrict__ topk_ids) {
+  constexpr int EM = 8;
+  __shared__ float red[16];
+  __shared__ float part[8][EM];
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const int lane = tid & 63, wv = tid >> 6;
+  const long off = (long)row * N + tid * 8;
+  uint4 pu[SPL], rv, wvv, ru[EM];
+#pragma unroll
+  for (int s = 0; s < SPL; ++s)
+    pu[s] = *reinterpret_cast<const uint4*>(ws16 + (long)s * M * N + off);
+  rv = *reinterpret_cast<const uint4*>(residual + off);
+  wvv = *reinterpret_cast<const uint4*>(w + tid * 8);
+#pragma unroll
+  for (int e = 0; e < EM; ++e)
+    ru[e] = *reinterpret_cast<const uint4*>(wr + (long)min(e, E - 1) * N + tid * 8);
+  __builtin_amdgcn_sched_barrier(0);
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int s = 0; s < SPL; ++s) {
+    float f[8];
+    unpack8h(pu[s], f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += f[j];
+  }
+  float r[8], v[8], ss = 0.f;
+  unpack8bf(rv, r);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    v[j] = bf2f(f2bf(r[j] + bf2f(f2bf(acc[j]))));
+    ss += v[j] * v[j];
+  }
+  store8(residual + off, v);
+  const float rstd = rsqrtf(block_sum(ss, red) / N + eps);
+  float wn[8], o[8];
+  unpack8bf(wvv, wn);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = bf2f(f2bf(v[j] * rstd * wn[j]));   // as stored
+  store8(out + off, o);
+  float lg[EM];
+#pragma unroll
+  for (int e = 0; e < EM; ++e) {
+    float we[8];
+    unpack8bf(ru[e], we);
+    float d = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d = fmaf(o[j], we[j], d);
+    lg[e] = wave_sum(d);
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int e = 0; e < EM; ++e) part[wv][e] = lg[e];
+  }
+  __syncthreads();
+  if (wv != 0) return;
+  float x = -INFINITY;
+  if (lane < E && lane < EM) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) t += part[q][lane];
+    x = bf2f(f2bf(t));
+  }
+  route_pick(x, lane, E, k, row, topk_w, topk_ids);
+}
+
+// N = 4096 (512 threads x 8), fp16 slabs, E <= 8
+extern "C" int dli_splitk_add_rmsnorm_route(void* out, void* residual, const void* ws,
+                                            int splits, int M, int N, const void* w, float eps,
+                                            const void* wr, int E, int k, float* topk_w,
+                                            int* topk_ids, hipStream_t st) {
+  if (M <= 0) return 0;
+  if (N != 4096 || E > 8 || k > E || w == nullptr || ((uintptr_t)wr & 15))
+    return (int)hipErrorInvalidValue;
+#define DLI_SRR(S) splitk_add_rmsnorm_route_kernel<S><<<M, 512, 0, st>>>((u16*)out, \
+      (u16*)residual, (const u16*)ws, M, N, (const u16*)w, eps, (const u16*)wr, E, k, topk_w, \
+      topk_ids)
+  switch (splits) {
+    case 2: DLI_SRR(2); break;
+    case 4: DLI_SRR(4); break;
+    case 8: DLI_SRR(8); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef DLI_SRR
+  DLI_RETURN_LAUNCH();
+}
+
 // fmt: 0 = fp32 slabs, 1 = fp16 x 1/16 slabs (EPI_SLAB16)
 extern "C" int dli_splitk_add_rmsnorm(void* out, void* residual, const float* ws, int splits,
                                       int M, int N, const void* w, float eps, int fmt,

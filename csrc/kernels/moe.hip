@@ -9,32 +9,6 @@
 // One wave per token, lane e holds expert e (E <= 64): softmax max / sum and each of the k
 // argmax rounds are wave-wide shuffle reductions, so no per-thread logits array (the former
 // float p[64] per thread spilled to scratch).
-// softmax over the E logits (lane e < E holds logit e, the others -inf) -> top-k (HF: lowest
-// index on ties) -> renormalised weights; one wave per token
-__device__ __forceinline__ void route_pick(float x, int lane, int E, int k, int t,
-                                           float* __restrict__ topk_w,
-                                           int* __restrict__ topk_ids) {
-  const float mx = wave_max(x);
-  float p = lane < E ? __expf(x - mx) : 0.f;
-  const float s = wave_sum(p);
-  float mine = 0.f, wsum = 0.f;                        // lane j keeps the j-th pick's weight
-  for (int j = 0; j < k; ++j) {
-    float bv = lane < E ? p : -3.f;
-    int bi = lane;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {                 // argmax, lowest index on ties (HF)
-      const float ov = __shfl_xor(bv, o, 64);
-      const int oi = __shfl_xor(bi, o, 64);
-      if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
-    }
-    const float w = bv / s;
-    wsum += w;
-    if (lane == j) { mine = w; topk_ids[t * k + j] = bi; }
-    if (lane == bi) p = -2.f;                          // taken
-  }
-  if (lane < k) topk_w[t * k + lane] = mine / wsum;
-}
-
 __global__ void __launch_bounds__(256) moe_route_kernel(float* __restrict__ topk_w,
                                                         int* __restrict__ topk_ids,
                                                         const u16* __restrict__ logits, int T,

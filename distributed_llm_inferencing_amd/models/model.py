@@ -161,6 +161,14 @@ class TransformerLM:
                                             self.cos_sin, kc, vc, cfg.num_heads,
                                             cfg.num_kv_heads, cfg.head_dim)
                 attn = self._attend(qkv, b, kc, vc)
+            if cfg.is_moe and self.tp_reduce is None and not defer:
+                # O projection + add + RMSNorm with the MoE gate of its output rows (one
+                # kernel when the slabs allow: ops.linear_add_rmsnorm route)
+                h, tw, ti = ops.linear_add_rmsnorm(attn, lp["wo"], residual, lp["mlp_norm"],
+                                                   eps, route=(lp["router"],
+                                                               cfg.top_k_experts))
+                pending = self.moe_fn(h, lp, self.layer_start + li, (tw, ti))
+                continue
             h = self._proj_add_norm(attn, lp["wo"], residual, lp["mlp_norm"], eps, defer)
             if cfg.is_moe:
                 pending = self.moe_fn(h, lp, self.layer_start + li)
@@ -216,8 +224,9 @@ class TransformerLM:
                            cfg.num_kv_heads, cfg.head_dim, use_rope=cfg.arch != "gpt2")
         return self._attend(qkv, b, kc, vc)
 
-    def _moe_local(self, h: torch.Tensor, lp: dict, layer: int) -> torch.Tensor:
-        topk_w, topk_ids = ops.moe_router(h, lp["router"], self.cfg.top_k_experts)
+    def _moe_local(self, h: torch.Tensor, lp: dict, layer: int, routing=None) -> torch.Tensor:
+        topk_w, topk_ids = (routing if routing is not None
+                            else ops.moe_router(h, lp["router"], self.cfg.top_k_experts))
         e0 = self.expert_range[0] if self.expert_range else 0
         return ops.moe_mlp(h, lp["w_gu"], lp["w_down"], topk_w, topk_ids, e0)
 

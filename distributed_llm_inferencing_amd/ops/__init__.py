@@ -247,11 +247,39 @@ def _splitk_plan(x, w):
     return p if p.splits > 1 else None
 
 
-def linear_add_rmsnorm(x, w, residual, norm_w, eps, plan: Optional[G.GemmPlan] = None):
+def linear_add_rmsnorm(x, w, residual, norm_w, eps, plan: Optional[G.GemmPlan] = None,
+                       route=None):
     """residual += x @ w.T (bf16-rounded, in place); returns rmsnorm(residual) * norm_w
     (None when norm_w is None). Split-K GEMMs reduce their partial slabs inside the norm
     kernel (fused_reduce.hip), so the bf16 GEMM output is never materialised.
-    ``plan`` forces the GEMM plan (the autotuner times every candidate with its consumer)."""
+    ``plan`` forces the GEMM plan (the autotuner times every candidate with its consumer).
+    ``route`` = (router weight [E, N], k): also the MoE gate of the output rows — returns
+    (out, topk_w, topk_ids); with fp16 slabs, N = 4096 and E <= 8 inside the same reduce
+    kernel (``dli_splitk_add_rmsnorm_route``), else by ``moe_router``."""
+    if route is not None:
+        wr, k = route
+        p = _splitk_plan(x, w) if plan is None else (plan if plan.splits > 1 else None)
+        M, K = x.shape
+        Nn = w.shape[0]
+        if (p is not None and norm_w is not None and Nn == 4096 and wr.shape[0] <= 8
+                and wr.is_contiguous() and residual.is_contiguous()
+                and wr.data_ptr() % 16 == 0):
+            ws = G.workspace(x.device, p.splits * M * Nn * 4)
+            fmt = _slab_gemm(x, w, p, ws)
+            if fmt == 1:
+                out = torch.empty_like(residual)
+                tw = torch.empty(M, k, dtype=torch.float32, device=x.device)
+                ti = torch.empty(M, k, dtype=torch.int32, device=x.device)
+                _native_call("dli_splitk_add_rmsnorm_route", _p(out), _p(residual), _p(ws),
+                             p.splits, M, Nn, _p(norm_w), eps, _p(wr), wr.shape[0], k, _p(tw),
+                             _p(ti), _st())
+                return out, tw, ti
+            out = torch.empty_like(residual)
+            _native_call("dli_splitk_add_rmsnorm", _p(out), _p(residual), _p(ws), p.splits, M,
+                         Nn, _p(norm_w), eps, fmt, _st())
+        else:
+            out = linear_add_rmsnorm(x, w, residual, norm_w, eps, plan=plan)
+        return (out,) + tuple(moe_router(out, wr, k))
     if plan is None:
         p = _splitk_plan(x, w)
     else:

@@ -63,6 +63,7 @@ _SIGS = {
     "dli_decode_attention_fused": [P, P, I, P, P, P, P, P, P, I, P, I, I, I, I, I, F, I, P],
     "dli_moe_route": [P, P, P, I, I, I, P],
     "dli_moe_router": [P, P, P, I, P, I, I, I, I, P],
+    "dli_splitk_add_rmsnorm_route": [P, P, P, I, I, I, P, F, P, I, I, P, P, P],
     "dli_moe_align": [P, P, P, P, I, I, I, I, P],
     "dli_moe_gather": [P, P, P, I, I, P, P],
     "dli_moe_combine": [P, P, P, P, I, I, I, P],

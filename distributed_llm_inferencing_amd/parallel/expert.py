@@ -189,7 +189,7 @@ class ExpertParallelMoE:
     def _a2a(self, out, inp, out_splits, in_splits):
         dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
 
-    def __call__(self, h: torch.Tensor, lp: dict, layer: int) -> torch.Tensor:
+    def __call__(self, h: torch.Tensor, lp: dict, layer: int, routing=None) -> torch.Tensor:
         T, D = h.shape
         dev = h.device
         k, N = self.k, self.world
@@ -198,7 +198,8 @@ class ExpertParallelMoE:
             raise RuntimeError("ExpertParallelMoE: begin_step() must announce this step's "
                                "token counts before the forward")
         if T > 0:
-            topk_w, topk_ids = ops.moe_router(h, lp["router"], k)
+            topk_w, topk_ids = (routing if routing is not None
+                                else ops.moe_router(h, lp["router"], k))
         else:
             topk_w = torch.zeros(0, k, dtype=torch.float32, device=dev)
             topk_ids = torch.zeros(0, k, dtype=torch.int32, device=dev)

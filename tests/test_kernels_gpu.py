@@ -954,6 +954,32 @@ def test_moe_router_fused(gpu, T, E, D):
     assert torch.allclose(w.sum(-1), torch.ones(T, device=gpu), atol=1e-5)
 
 
+@pytest.mark.parametrize("M,splits", [(512, 4), (37, 2), (5, 8)])
+def test_add_rmsnorm_with_fused_gate(gpu, M, splits):
+    """The Mixtral O-projection reduce with the MoE gate inside (dli_splitk_add_rmsnorm_route)
+    == the plain reduce followed by moe_router: the same output rows and residual bit for
+    bit, the same picks up to one-ulp near-ties of the bf16 logits, the same weights."""
+    torch.manual_seed(43)
+    K = N = 4096
+    x, w = rnd(M, K, dev=gpu), rnd(N, K, dev=gpu, scale=0.02)
+    r0, nw = rnd(M, N, dev=gpu), (1.0 + 0.1 * rnd(N, dev=gpu)).to(BF)
+    wr = rnd(8, N, dev=gpu, scale=0.05)
+    p = G.GemmPlan("dli", 28, splits)
+    assert p.tile in G.SLAB16_TILES
+    r1, r2 = r0.clone(), r0.clone()
+    o1, tw1, ti1 = ops.linear_add_rmsnorm(x, w, r1, nw, 1e-5, plan=p, route=(wr, 2))
+    o2 = ops.linear_add_rmsnorm(x, w, r2, nw, 1e-5, plan=p)
+    tw2, ti2 = ops.moe_router(o2, wr, 2)
+    assert torch.equal(o1, o2) and torch.equal(r1, r2)
+    lb = (o2.float() @ wr.float().t()).to(BF).float()
+    kth = lb.topk(2, -1).values[:, -1:]
+    tol = 2 ** -7 * lb.abs().amax(-1, keepdim=True)
+    assert (lb.gather(1, ti1.long()) >= kth - tol).all()
+    same = (ti1 == ti2).all(-1)
+    assert same.float().mean() > 0.95
+    close(tw1[same], tw2[same], rtol=1e-2, atol=1e-3)
+
+
 @pytest.mark.parametrize("S,V,c", [(37, 16032, 64), (5, 4008, 64), (3, 64, 64), (9, 50257, 50)])
 def test_topk_rows_kernel(gpu, S, V, c):
     """HIP per-row top-c (vocab-parallel head candidates) vs torch.topk: same value multiset,
