@@ -267,6 +267,76 @@ __global__ void __launch_bounds__(256) moe_combine_slabs_kernel(
   store8(out + (long)t * dim + c * 8, acc);
 }
 
+// The combine above, then the next layer's input norm in the same pass (one workgroup per
+// token, 512 threads x 8 columns = dim 4096): m = bf16(sum_j w_j bf16(sum_s P_s[pos_j]))
+// (what moe_combine_slabs_kernel stores), residual = bf16(residual + m), out =
+// rmsnorm(residual) * nw — the combine's bf16 output and the separate add + RMSNorm kernel
+// (norm_kernel, 7.5 us per layer at batch 512) go away. nw null: the residual add only (a
+// stage's last layer).
+template <int S>
+__global__ void __launch_bounds__(512) moe_combine_add_rmsnorm_kernel(
+    u16* __restrict__ out, u16* __restrict__ residual, const u16* __restrict__ ws,
+    long slab_stride, const float* __restrict__ w, const int* __restrict__ pos, int k, int dim,
+    const u16* __restrict__ nw, float eps) {
+  __shared__ float red[16];
+  const int t = blockIdx.x, c = threadIdx.x;
+  const long off = (long)t * dim + c * 8;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int j = 0; j < k; ++j) {
+    const int p = pos[t * k + j];
+    if (p < 0) continue;
+    uint4 u[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+      u[s] = *reinterpret_cast<const uint4*>(ws + s * slab_stride + (long)p * dim + c * 8);
+    float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      float f[8];
+      unpack8h(u[s], f);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] += f[q];
+    }
+    const float ww = w[t * k + j];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] += ww * bf2f(f2bf(v[q]));
+  }
+  float r[8], x[8], ss = 0.f;
+  load8(residual + off, r);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    x[q] = bf2f(f2bf(r[q] + bf2f(f2bf(acc[q]))));
+    ss += x[q] * x[q];
+  }
+  store8(residual + off, x);
+  if (nw == nullptr) return;                         // uniform
+  const float rstd = rsqrtf(block_sum(ss, red) / dim + eps);
+  float wn[8], o[8];
+  load8(nw + c * 8, wn);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) o[q] = x[q] * rstd * wn[q];
+  store8(out + off, o);
+}
+
+extern "C" int dli_moe_combine_add_rmsnorm(void* out, void* residual, const void* ws, int splits,
+                                           int rows, const float* w, const int* pos, int T,
+                                           int k, int dim, const void* nw, float eps,
+                                           hipStream_t st) {
+  if (T <= 0) return 0;
+  if (dim != 4096) return (int)hipErrorInvalidValue;
+  const long stride = (long)rows * dim;
+#define DLI_MCN(S) moe_combine_add_rmsnorm_kernel<S><<<T, 512, 0, st>>>(                   \
+      (u16*)out, (u16*)residual, (const u16*)ws, stride, w, pos, k, dim, (const u16*)nw, eps)
+  switch (splits) {
+    case 2: DLI_MCN(2); break;
+    case 4: DLI_MCN(4); break;
+    case 8: DLI_MCN(8); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef DLI_MCN
+  DLI_RETURN_LAUNCH();
+}
+
 // ws: the fp16 slabs of a grouped split-K GEMM over `rows` permuted rows (slab stride rows x dim)
 extern "C" int dli_moe_combine_slabs(void* out, const void* ws, int splits, int rows,
                                      const float* w, const int* pos, int T, int k, int dim,

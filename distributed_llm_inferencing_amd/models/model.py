@@ -177,7 +177,10 @@ class TransformerLM:
             nxt = self.layers[li + 1]["attn_norm"] if li + 1 < n else None
             h = self._proj_add_norm(act, lp["w_down"], residual, nxt, eps, defer)
         if pending is not None:
-            residual.add_(pending)
+            if isinstance(pending, ops.MoEPending):
+                pending.add_rmsnorm(residual, None, eps)
+            else:
+                residual.add_(pending)
         return residual
 
     def _proj_add_norm(self, x, w, residual, norm_w, eps, defer: bool = False):
@@ -224,11 +227,15 @@ class TransformerLM:
                            cfg.num_kv_heads, cfg.head_dim, use_rope=cfg.arch != "gpt2")
         return self._attend(qkv, b, kc, vc)
 
-    def _moe_local(self, h: torch.Tensor, lp: dict, layer: int, routing=None) -> torch.Tensor:
+    def _moe_local(self, h: torch.Tensor, lp: dict, layer: int, routing=None):
+        """The layer's experts on this device. With ``routing`` (the gate computed in the O
+        projection's reduce, ``_llama_layers``) a decode step returns an ``ops.MoEPending``:
+        its combine runs inside the next layer's add + RMSNorm."""
         topk_w, topk_ids = (routing if routing is not None
                             else ops.moe_router(h, lp["router"], self.cfg.top_k_experts))
         e0 = self.expert_range[0] if self.expert_range else 0
-        return ops.moe_mlp(h, lp["w_gu"], lp["w_down"], topk_w, topk_ids, e0)
+        return ops.moe_mlp(h, lp["w_gu"], lp["w_down"], topk_w, topk_ids, e0,
+                           defer_combine=routing is not None)
 
     def final_hidden(self, hidden: torch.Tensor, b: DeviceBatch) -> torch.Tensor:
         """Final norm of the last token of each sequence -> bf16 [S, D]."""

@@ -45,7 +45,11 @@ def rmsnorm(x, w, eps, residual_copy: Optional[torch.Tensor] = None):
 
 
 def add_rmsnorm(x, residual, w, eps):
-    """residual += x (in place); returns rmsnorm(residual)*w."""
+    """residual += x (in place); returns rmsnorm(residual)*w. ``x`` may be a ``MoEPending``
+    (a MoE layer's output not yet combined): the combine, the add and the norm then run as
+    one kernel."""
+    if isinstance(x, MoEPending):
+        return x.add_rmsnorm(residual, w, eps)
     if not _use_native(x):
         out, r = R.fused_add_rmsnorm(x, residual, w, eps)
         residual.copy_(r)
@@ -79,6 +83,44 @@ def add_layernorm(x, residual, w, b, eps):
     _native_call("dli_fused_add_layernorm", _p(out), _p(residual), _p(x), _p(w), _p(b), rows,
                  dim, eps, _st())
     return out
+
+
+class MoEPending:
+    """A decode MoE layer's output before its combine: the grouped down projection's fp16
+    split-K slabs, the routing weights and the row of each (token, pick). ``add_rmsnorm``
+    (the next layer's input norm, via ``ops.add_rmsnorm``) combines, adds into the residual
+    and normalises in one kernel (``dli_moe_combine_add_rmsnorm``); ``materialize()`` runs
+    the plain combine for any other consumer. The slab workspace must not be reused before
+    the consumer has run (the next GEMM to use it is the next layer's)."""
+
+    def __init__(self, ws, splits: int, rows: int, topk_w, pos, shape, dtype, device):
+        self.ws, self.splits, self.rows = ws, splits, rows
+        self.topk_w, self.pos = topk_w, pos
+        self.shape, self.dtype, self.device = shape, dtype, device
+
+    def materialize(self) -> torch.Tensor:
+        T, D = self.shape
+        out = torch.empty(T, D, dtype=self.dtype, device=self.device)
+        k = self.topk_w.shape[1]
+        _native_call("dli_moe_combine_slabs", _p(out), _p(self.ws), self.splits, self.rows,
+                     _p(self.topk_w), _p(self.pos), T, k, D, _st())
+        return out
+
+    def add_rmsnorm(self, residual, w, eps):
+        """w None: the residual add only (a stage's last layer); returns None then."""
+        T, D = self.shape
+        if D != 4096 or not residual.is_contiguous():
+            m = self.materialize()
+            if w is None:
+                residual.add_(m)
+                return None
+            return add_rmsnorm(m, residual, w, eps)
+        out = torch.empty(T, D, dtype=self.dtype, device=self.device) if w is not None else None
+        k = self.topk_w.shape[1]
+        _native_call("dli_moe_combine_add_rmsnorm", _p(out), _p(residual), _p(self.ws),
+                     self.splits, self.rows, _p(self.topk_w), _p(self.pos), T, k, D, _p(w),
+                     float(eps), _st())
+        return out
 
 
 class NormedRows:
@@ -647,7 +689,7 @@ def moe_router(h, w_router, k: int):
 
 
 def moe_mlp(x, w_gu, w_down, topk_w, topk_ids, expert_offset: int = 0,
-            plan_rows: Optional[int] = None):
+            plan_rows: Optional[int] = None, defer_combine: bool = False):
     """Experts [expert_offset, expert_offset+E_local) of one MoE layer; returns the weighted
     sum over the token's selected local experts (zeros for tokens routed elsewhere).
     ``plan_rows``: the routed rows these experts typically receive, when ``x`` is a region
@@ -697,6 +739,13 @@ def moe_mlp(x, w_gu, w_down, topk_w, topk_ids, expert_offset: int = 0,
                  rows_per_group=n, plan=p_gu)
     p_dn = p_dn or G.grouped_plan(n, D, F2 // 2, "none", E_local)
     if moe_slab_plan(p_dn):
+        if defer_combine:
+            # the down projection's slabs; the combine runs with the next layer's add + norm
+            ws = G.workspace(dev, p_dn.splits * max(n, 1) * D * 2)
+            _native_call("dli_gemm", _p(act), act.stride(0), _p(w_down), w_down.stride(-2),
+                         None, D, n, D, F2 // 2, G.EPI["slab16"], p_dn.tile, p_dn.splits, None,
+                         _p(ws), _p(offsets), E_local, _st())
+            return MoEPending(ws, p_dn.splits, n, topk_w, pos, (T, D), x.dtype, dev)
         out = torch.empty_like(x)
         moe_down_combine(act, w_down, offsets, n, p_dn, topk_w, pos, out)
         return out

@@ -980,6 +980,43 @@ def test_add_rmsnorm_with_fused_gate(gpu, M, splits):
     close(tw1[same], tw2[same], rtol=1e-2, atol=1e-3)
 
 
+@pytest.mark.parametrize("splits", [2, 4])
+def test_moe_combine_fused_with_next_norm(gpu, splits):
+    """A decode MoE layer's deferred combine (ops.MoEPending) run inside the next layer's
+    add + RMSNorm (dli_moe_combine_add_rmsnorm) == the plain combine, then the add + RMSNorm
+    kernel: the residual bit for bit, the normalised rows within one bf16 ulp (the row sum of
+    squares is reduced in another order); and the residual-only form of a last layer."""
+    torch.manual_seed(47)
+    T, E, k, D, F = 96, 8, 2, 4096, 512
+    x = rnd(T, D, dev=gpu)
+    logits = rnd(T, E, dev=gpu)
+    logits[:, 5] = -30.0                          # expert 5 is never picked
+    rw, rids = R.router_topk(logits, k)
+    wgu = rnd(E, 2 * F, D, dev=gpu, scale=0.05)
+    wd = rnd(E, D, F, dev=gpu, scale=0.05)
+    key = (G._bucket(T * k), D, F, "none", E)
+    old = G._grouped_cache.get(key)
+    G._grouped_cache[key] = G.GemmPlan("dli", 12, splits)
+    try:
+        pend = ops.moe_mlp(x, wgu, wd, rw, rids, defer_combine=True)
+        assert isinstance(pend, ops.MoEPending)
+        r0, nw = rnd(T, D, dev=gpu), (1.0 + 0.1 * rnd(D, dev=gpu)).to(BF)
+        r1, r2, r3 = r0.clone(), r0.clone(), r0.clone()
+        plain = pend.materialize()
+        close(plain, R.moe_mlp(x, wgu, wd, rw, rids), rtol=3e-2, atol=3e-2)
+        out_b = ops.add_rmsnorm(plain, r2, nw, 1e-5)
+        out_a = ops.add_rmsnorm(pend, r1, nw, 1e-5)
+        assert torch.equal(r1, r2)
+        close(out_a, out_b, rtol=1e-2, atol=1e-2)
+        assert pend.add_rmsnorm(r3, None, 1e-5) is None
+        assert torch.equal(r3, r2)
+    finally:
+        if old is None:
+            G._grouped_cache.pop(key, None)
+        else:
+            G._grouped_cache[key] = old
+
+
 @pytest.mark.parametrize("S,V,c", [(37, 16032, 64), (5, 4008, 64), (3, 64, 64), (9, 50257, 50)])
 def test_topk_rows_kernel(gpu, S, V, c):
     """HIP per-row top-c (vocab-parallel head candidates) vs torch.topk: same value multiset,
