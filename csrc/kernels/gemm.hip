@@ -55,6 +55,25 @@ extern "C" int dli_gemm_set_slab_store_family(int family, int mode) {
 // stream (16 / 32 rows per workgroup, dispatch_gemv); 55 = tile 45 persistent (one workgroup
 // per CU walks its tiles, no split-K / grouped mode). ws: fp32 [splits, M, N] when splits>1.
 // group_off (nullable): int[groups+1] row offsets; M is then the max rows of any group.
+// Grouped SiLU*up GEMM whose permuted row p reads activation row arow[p] (the MoE gate/up
+// projection without the gathered copy of its input rows): the generic tile family only,
+// unsplit. M: the row bound per group, as dli_gemm's grouped mode.
+extern "C" int dli_gemm_grouped_gather(const void* A, int lda, const void* W, int ldw, void* C,
+                                       int ldc, int M, int N, int K, int tile_cfg,
+                                       const int* arow, const int* group_off, int groups,
+                                       hipStream_t st) {
+  if (M <= 0 || N <= 0) return 0;
+  const bool generic = (tile_cfg >= 0 && tile_cfg <= 21) || (tile_cfg >= 23 && tile_cfg <= 25);
+  if (!generic || arow == nullptr || group_off == nullptr || groups < 1 || K % BK || lda % 8 ||
+      ldw % 8 || N % 32)
+    return (int)hipErrorInvalidValue;
+  const void* bias = arow;
+  void* ws = nullptr;
+  const int* go = group_off;
+  const int splits = 1;
+  return gemm_tiles_dispatch(EPI_SILU, tile_cfg, DLI_GEMM_PASS);
+}
+
 extern "C" int dli_gemm(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M,
                         int N, int K, int epi, int tile_cfg, int splits, const void* bias,
                         void* ws, const int* group_off, int groups, hipStream_t st) {

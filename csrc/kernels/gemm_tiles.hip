@@ -37,6 +37,11 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
   const u16* Ab = A + (long)row0 * lda;
+  // grouped SiLU*up with a row index (dli_gemm_grouped_gather passes it as `bias`, which the
+  // SiLU epilogue never reads): permuted row p of the group reads activation row arow[p], so
+  // the MoE gate/up projection streams the token rows in place (no gathered copy)
+  const int* arow = (EPI == EPI_SILU && group_off != nullptr)
+                        ? reinterpret_cast<const int*>(bias) : nullptr;
 
   // ---- per-lane glds source pointers (row clamped in range; swizzled chunk)
   // one glds wave-instruction stages 8 rows x 128 B; all NW waves share each tile
@@ -49,7 +54,8 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(
     const int r = (i * NW + wid) * 8 + (lane >> 3);
     const int c = (lane & 7) ^ ((r >> 1) & 7);
     const int gr = min(m0 + r, Mg - 1);
-    a_src[i] = Ab + (long)gr * lda + kb + c * 8;
+    a_src[i] = (arow != nullptr ? A + (long)arow[row0 + gr] * lda : Ab + (long)gr * lda) + kb +
+               c * 8;
   }
 #pragma unroll
   for (int i = 0; i < W_INSTR; ++i) {

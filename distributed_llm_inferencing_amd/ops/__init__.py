@@ -709,16 +709,16 @@ def moe_mlp(x, w_gu, w_down, topk_w, topk_ids, expert_offset: int = 0,
     src = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
     _native_call("dli_moe_align", _p(offsets), _p(pos), _p(src), _p(topk_ids), n, k,
                  expert_offset, E_local, _st())
-    # permuted rows: at most n (all local); rows past offsets[E_local] are never touched
-    xp = torch.empty(max(n, 1), D, dtype=x.dtype, device=dev)
-    _native_call("dli_moe_gather", _p(xp), _p(x), _p(src), n, D, _p(offsets[E_local:]), _st())
     act = torch.empty(max(n, 1), F2 // 2, dtype=x.dtype, device=dev)
     if n >= _MOE_PREFILL_ROWS * E_local and not torch.cuda.is_current_stream_capturing():
         # prefill-sized expert GEMMs (thousands of rows per expert) are compute-bound: a
         # grouped 256x256 kernel (G.MOE_PREFILL_TILE: the two-barrier 4-wave tile, grid.z =
-        # expert) with the fused SiLU*up epilogue. The largest expert's row count bounds the grid (one host read of the
-        # offsets per MoE layer, eager prefill only) instead of n, which would launch ~8x
-        # more (empty) row tiles per expert.
+        # expert) with the fused SiLU*up epilogue. The largest expert's row count bounds the
+        # grid (one host read of the offsets per MoE layer, eager prefill only) instead of n,
+        # which would launch ~8x more (empty) row tiles per expert.
+        xp = torch.empty(max(n, 1), D, dtype=x.dtype, device=dev)
+        _native_call("dli_moe_gather", _p(xp), _p(x), _p(src), n, D, _p(offsets[E_local:]),
+                     _st())
         offs = offsets.tolist()
         rows_max = max(b - a for a, b in zip(offs[:-1], offs[1:]))
         y = torch.empty(max(n, 1), D, dtype=x.dtype, device=dev)
@@ -731,13 +731,22 @@ def moe_mlp(x, w_gu, w_down, topk_w, topk_ids, expert_offset: int = 0,
         out = torch.empty_like(x)
         _native_call("dli_moe_combine", _p(out), _p(y), _p(topk_w), _p(pos), T, k, D, _st())
         return out
-    p_gu = p_dn = None
-    if plan_rows is not None:
-        p_gu = G.grouped_plan(plan_rows, F2, D, "silu_mul", E_local)
-        p_dn = G.grouped_plan(plan_rows, D, F2 // 2, "none", E_local)
-    _gemm_native(xp, w_gu, "silu_mul", out=act, groups=E_local, group_off=offsets,
-                 rows_per_group=n, plan=p_gu)
-    p_dn = p_dn or G.grouped_plan(n, D, F2 // 2, "none", E_local)
+    rows = plan_rows if plan_rows is not None else n
+    p_gu = G.grouped_plan(rows, F2, D, "silu_mul", E_local)
+    if p_gu.splits == 1 and p_gu.tile in G.GATHER_TILES and x.is_contiguous():
+        # the gate/up GEMM reads the token rows in place through the permutation (no gathered
+        # copy of them: dli_gemm_grouped_gather, the generic tile family)
+        _native_call("dli_gemm_grouped_gather", _p(x), x.stride(0), _p(w_gu), w_gu.stride(-2),
+                     _p(act), act.stride(0), n, F2, D, p_gu.tile, _p(src), _p(offsets),
+                     E_local, _st())
+    else:
+        # permuted rows: at most n (all local); rows past offsets[E_local] are never touched
+        xp = torch.empty(max(n, 1), D, dtype=x.dtype, device=dev)
+        _native_call("dli_moe_gather", _p(xp), _p(x), _p(src), n, D, _p(offsets[E_local:]),
+                     _st())
+        _gemm_native(xp, w_gu, "silu_mul", out=act, groups=E_local, group_off=offsets,
+                     rows_per_group=n, plan=p_gu)
+    p_dn = G.grouped_plan(rows, D, F2 // 2, "none", E_local)
     if moe_slab_plan(p_dn):
         if defer_combine:
             # the down projection's slabs; the combine runs with the next layer's add + norm

@@ -69,6 +69,7 @@ _SIGS = {
     "dli_moe_combine": [P, P, P, P, I, I, I, P],
     "dli_moe_combine_slabs": [P, P, I, I, P, P, I, I, I, P],
     "dli_moe_combine_add_rmsnorm": [P, P, P, I, I, P, P, I, I, I, P, F, P],
+    "dli_gemm_grouped_gather": [P, I, P, I, P, I, I, I, I, I, P, P, I, P],
     "dli_ep_pack": [P, P, P, P, P, P, P, I, I, I, I, P],
 }
 

@@ -109,6 +109,9 @@ EPI = {"none": 0, "f32": 1, "silu_mul": 2, "bias_gelu": 3, "bias": 4, "splitk": 
 # weight-streaming GEMVs and the 4-wave family keep fp32 slabs.
 SLAB16_TILES = frozenset(list(range(0, 22)) + [22, 23, 24, 25, 26, 28])
 SLAB16 = os.environ.get("DLI_SLAB_FP32", "0") != "1"      # A/B: fp32 partials everywhere
+# tiles whose grouped SiLU*up GEMM can read its rows through a permutation (the generic
+# family: dli_gemm_grouped_gather), so the MoE gate/up skips the gathered copy of its input
+GATHER_TILES = frozenset(list(range(0, 22)) + [23, 24, 25])
 NUM_CUS = 256
 
 

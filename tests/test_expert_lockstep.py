@@ -165,13 +165,13 @@ def _dying_worker(rank, world, port, q):
     if rank == 1:
         inner = eng.moe.__class__.__call__
 
-        def die(self, h, lp, layer):
+        def die(self, h, lp, layer, *rest):
             if layer == 1:
                 q.put((1, "exiting"))
                 q.close()
                 q.join_thread()
                 os._exit(0)                           # mid-forward: rank 0 waits on its rows
-            return inner(self, h, lp, layer)
+            return inner(self, h, lp, layer, *rest)
         eng.moe.__class__.__call__ = die
     t0 = time.monotonic()
     try:

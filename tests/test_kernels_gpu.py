@@ -1017,6 +1017,32 @@ def test_moe_combine_fused_with_next_norm(gpu, splits):
             G._grouped_cache[key] = old
 
 
+@pytest.mark.parametrize("tile", [12, 2, 10, 23])
+def test_grouped_gate_up_reads_rows_through_permutation(gpu, tile):
+    """dli_gemm_grouped_gather (the MoE gate/up without the gathered copy of its input) ==
+    the grouped SiLU*up GEMM of the gathered rows, bit for bit: same tile, same sums, only
+    the A-row addresses differ; uneven groups incl. an empty one and one past a tile."""
+    torch.manual_seed(53)
+    T, E, D, F2 = 150, 4, 512, 1024
+    sizes = [37, 0, 190, 73]
+    rows = sum(sizes)
+    x = rnd(T, D, dev=gpu)
+    src = torch.randint(0, T, (rows,), dtype=torch.int32, device=gpu)
+    off = torch.tensor([0] + list(__import__("itertools").accumulate(sizes)), dtype=torch.int32,
+                       device=gpu)
+    w = rnd(E, F2, D, dev=gpu, scale=0.05)
+    if not G.tile_ok(tile, "silu_mul"):
+        pytest.skip("tile without the SiLU pairing")
+    ref = ops._gemm_native(x[src.long()].contiguous(), w, "silu_mul",
+                           plan=G.GemmPlan("dli", tile, 1), groups=E, group_off=off,
+                           rows_per_group=rows)
+    out = torch.full((rows, F2 // 2), float("nan"), dtype=BF, device=gpu)
+    ops._native_call("dli_gemm_grouped_gather", ops._p(x), x.stride(0), ops._p(w), w.stride(-2),
+                     ops._p(out), out.stride(0), rows, F2, D, tile, ops._p(src), ops._p(off), E,
+                     ops._st())
+    assert torch.equal(out, ref)
+
+
 @pytest.mark.parametrize("S,V,c", [(37, 16032, 64), (5, 4008, 64), (3, 64, 64), (9, 50257, 50)])
 def test_topk_rows_kernel(gpu, S, V, c):
     """HIP per-row top-c (vocab-parallel head candidates) vs torch.topk: same value multiset,
