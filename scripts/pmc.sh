@@ -46,4 +46,9 @@ for pass in \
   [ $rc -ne 0 ] && { echo "stopping"; exit $rc; }
 done
 python3 scripts/pmc_report.py "$ABS"/pass* > "$ABS/pmc_report.txt" 2>&1
+# PMC_TAIL=N: a second table over each pass's last N dispatches only (a bench's timed wave,
+# without the capture-time autotune probes)
+if [ -n "${PMC_TAIL:-}" ]; then
+  python3 scripts/pmc_report.py --tail "$PMC_TAIL" "$ABS"/pass* > "$ABS/pmc_report_tail.txt" 2>&1
+fi
 head -40 "$ABS/pmc_report.txt"

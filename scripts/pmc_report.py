@@ -1,10 +1,12 @@
 #!/usr/bin/env python3
 """Merge rocprofv3 --pmc pass directories into one per-kernel counter table.
 
-    pmc_report.py <pass_dir> [<pass_dir> ...]
+    pmc_report.py [--tail N] <pass_dir> [<pass_dir> ...]
 
 Every ``*counter_collection.csv`` under the given directories is read; values are averaged
-per (kernel, counter) over the dispatches of that kernel. Derived columns, where their
+per (kernel, grid size, counter) over the dispatches of that kernel at that grid (one row per
+GEMM shape / plan). ``--tail N`` keeps only the last N dispatches of each pass (by
+Dispatch_Id): the timed waves of a bench run, without its capture-time autotune probes. Derived columns, where their
 inputs were collected (gfx94x formulas, the only ones ROCm 7.2 ships for gfx950):
 
 * mfma_busy%  = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / XCDs * CUs * 4 SIMDs).
@@ -35,13 +37,25 @@ def short(name: str) -> str:
 
 
 def main():
+    args = sys.argv[1:]
+    tail = 0
+    if len(args) >= 2 and args[0] == "--tail":
+        tail, args = int(args[1]), args[2:]
     vals = defaultdict(lambda: defaultdict(list))
-    for d in sys.argv[1:]:
+    for d in args:
         for f in Path(d).rglob("*counter_collection.csv"):
-            for r in csv.DictReader(open(f)):
+            rows = list(csv.DictReader(open(f)))
+            if tail:
+                ids = sorted({int(r.get("Dispatch_Id", 0) or 0) for r in rows})
+                cut = ids[-tail] if len(ids) >= tail else ids[0] if ids else 0
+                rows = [r for r in rows if int(r.get("Dispatch_Id", 0) or 0) >= cut]
+            for r in rows:
                 k = short(r.get("Kernel_Name", "?"))
+                g = r.get("Grid_Size")
+                if g:
+                    k = f"{k} g={g}"
                 try:
-                    # one row per (dispatch, counter); keep the dispatch id to average per call
+                    # one row per (dispatch, counter); averaged per call below
                     vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
                 except (KeyError, ValueError):
                     continue
@@ -53,7 +67,7 @@ def main():
     for k in sorted(vals):
         m = {c: sum(x) / len(x) for c, x in vals[k].items()}
         calls = max(len(x) for x in vals[k].values())
-        line = [f"{k:44s} n={calls:3d}"]
+        line = [f"{k:58s} n={calls:5d}"]
         gui = m.get("GRBM_GUI_ACTIVE")
         if gui and "SQ_VALU_MFMA_BUSY_CYCLES" in m:
             line.append(f"mfma_busy%="
